@@ -1,0 +1,171 @@
+/*
+ * poms_hip.h -- C ABI of libpoms_hip.so, the MI355X (gfx950) hot path of the
+ * POMS tensor-product B-spline multigrid.
+ *
+ * Every entry point is plain C: integers, doubles, raw pointers, an opaque
+ * handle and a hipStream_t passed as `void*`.  No torch or C++ types cross
+ * this boundary.  Each function returns 0 on success and a non-zero status
+ * otherwise; `poms_last_error()` then returns a thread-local message.
+ *
+ * Memory: the caller owns every vector buffer.  Vector arguments are DEVICE
+ * pointers to padded C-order arrays with the spl `StencilVector._data`
+ * layout (`slides/content.tex:256-264`): local extent n_d plus `pads[d]`
+ * ghost cells on each side of every axis (2D: n0 = 1, pads[0] = 0;
+ * 1D additionally n1 = 1, pads[1] = 0).  Kernels read ghost cells and never
+ * write them; halo transport of the axis-0 ghost planes is the caller's
+ * (RCCL send/recv via torch.distributed), see INTEGRATION.md.
+ *
+ * Band convention for every 1D factor: row-major (n, 2*pmax+1) doubles,
+ * F_band[i*(2*pmax+1) + k] = F[i, i + k - pmax] -- the 1D StencilMatrix
+ * layout `A[i1, k]` of `pyccel/pyccel_functions.py:4-21`.
+ *
+ * Streams: every kernel is enqueued on the given stream (NULL = default);
+ * nothing synchronises the host except `poms_kron_dot_2d` (host-pointer
+ * drop-in) and the `*_host` getters.  Handles are not thread-safe; one
+ * context per device per host thread.
+ */
+#ifndef POMS_HIP_H
+#define POMS_HIP_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define POMS_ABI_VERSION 1
+
+/* operator forms (see poms_op_create) */
+#define POMS_FORM_SINGLE 0 /* y = F0 (x) F1 (x) F2 x                                  */
+#define POMS_FORM_SUM    1 /* y = A0(x)M1(x)M2 x + M0(x)(K1(x)M2 + M1(x)K2) x (3D)   */
+                           /* y = A1(x)M2 x + M1(x)K2 x                      (2D/1D)  */
+
+typedef struct poms_ctx poms_ctx;           /* per-device context + scratch      */
+typedef struct poms_op poms_op;             /* Kronecker(-sum) banded operator   */
+typedef struct poms_transfer poms_transfer; /* knot-insertion R = P^T / P        */
+
+/* Grid layout of a (local) padded vector.  ndim in {1,2,3}; unused leading
+ * axes have n = 1 and pad = 0.  Axis order is C order: axis 2 is unit-stride. */
+typedef struct poms_layout {
+    int64_t n[3];    /* local interior extent per axis                       */
+    int64_t pads[3]; /* ghost width per axis (storage pad)                   */
+} poms_layout;
+
+/* ---- library / context ---------------------------------------------------- */
+int         poms_abi_version(void);
+const char* poms_last_error(void);
+int         poms_device_count(int* count);
+/* Creates a context on `device` (hipSetDevice) with reduction scratch.
+ * Replaces: the per-process MPI/spl setup of `sources/mg_jac.py:19-46`.       */
+int         poms_ctx_create(int device, poms_ctx** ctx);
+int         poms_ctx_destroy(poms_ctx* ctx);
+int         poms_synchronize(poms_ctx* ctx, void* stream);
+
+/* ---- banded Kronecker operator ------------------------------------------- */
+/* Create an operator on a local slab.  `layout` is the vector layout.  Axis-0
+ * rows are global: local plane z is global plane g0 + z, n0_global planes.
+ * Factor arrays are HOST pointers, band rows of width 2*pmax+1, copied to the
+ * device:
+ *   POMS_FORM_SINGLE (3D): f[0]=F0 (n0_global rows), f[2]=F1, f[4]=F2
+ *   POMS_FORM_SUM    (3D): f[0]=A0 (= M0+K0), f[1]=M0, f[2]=M1, f[3]=K1,
+ *                          f[4]=M2, f[5]=K2
+ *   2D/1D: axis-0 factors are ignored (pass NULL); SINGLE: f[2]=F1, f[4]=F2;
+ *          SUM: f[2]=A1 (= M1+K1), f[3]=M1, f[4]=M2, f[5]=K2
+ * Replaces: the operator built by `assembly_2d` (`sources/matrix_assembler.py:84-179`)
+ * whose `StencilMatrix.dot` is called at `sources/solvers.py:85,103,109,209`
+ * and `sources/mg_jac.py:93`; and the (A, B) pair of `kron_dot_v2`
+ * (`sources/kron_product.py:56`).  pmax in 1..5.                               */
+int poms_op_create(poms_ctx* ctx, int ndim, const poms_layout* layout, int form,
+                   int pmax, const double* const* factors, int64_t g0,
+                   int64_t n0_global, poms_op** op);
+int poms_op_destroy(poms_op* op);
+/* Planes per workgroup along axis 0 (3D); 0 = automatic. */
+int poms_op_set_chunk(poms_op* op, int chunk);
+
+/* y = A x on output planes [z_begin, z_end) (local axis-0 indices; 2D/1D: 0,1).
+ * x must have current ghosts on the planes the range touches.
+ * Replaces: `kron_dot_pyccel_2d` (`pyccel/pyccel_functions.py:4-21`) and
+ * spl `StencilMatrix.dot` (`sources/solvers.py:103`).                         */
+int poms_op_apply(poms_op* op, const double* x, double* y, int64_t z_begin,
+                  int64_t z_end, void* stream);
+/* r = b - A x (fused).  Replaces: `r = b - A.dot(x)` at `sources/solvers.py:85`,
+ * `sources/solvers.py:209`, `sources/mg_jac.py:93`.                           */
+int poms_op_residual(poms_op* op, const double* b, const double* x, double* r,
+                     int64_t z_begin, int64_t z_end, void* stream);
+/* One damped-Jacobi sweep, fused:  dr = omega (b - A x_in) / diag(A);
+ * x_out = x_in + dr;  if norm_dev != NULL, per-block partial sums of dr.dr are
+ * written to the context scratch and reduced into norm_dev[0] (device double)
+ * by poms_reduce_partials.  x_out must not alias x_in.
+ * Replaces: the body of `damped_jacobi`, `sources/solvers.py:207-219`.        */
+int poms_op_jacobi_sweep(poms_op* op, double omega, const double* b,
+                         const double* x_in, double* x_out, int64_t z_begin,
+                         int64_t z_end, int want_norm, void* stream);
+/* x = scale * b / diag(A) on the interior.  With scale = 1 this is
+ * `jacobi(A, b)` (`sources/solvers.py:139-163`); with scale = omega it is the
+ * first damped-Jacobi sweep from x0 = 0 (A.0 = 0 exactly).                    */
+int poms_op_diag_scale(poms_op* op, double scale, const double* b, double* x,
+                       int want_norm, void* stream);
+/* Number of norm partials the last want_norm launch on this op produced. */
+int poms_op_last_partials(poms_op* op, int64_t* count);
+
+/* Host-pointer drop-in for the pyccel kernel `kron_dot_pyccel_2d(starts, ends,
+ * pads, X, X_tmp, Y, A, B)` (`pyccel/pyccel_functions.py:3-21`).  X, X_tmp, Y
+ * are the local padded arrays ((e0-s0+1+2p0) x (e1-s1+1+2p1), C order); A, B
+ * are GLOBAL band arrays ((n_global_d) x (2p_d+1)).  X_tmp is accepted for
+ * signature parity and left untouched (the intermediate lives in LDS).
+ * Synchronous.  starts/ends are global indices as in spl.                     */
+int poms_kron_dot_2d(poms_ctx* ctx, const int64_t* starts, const int64_t* ends,
+                     const int64_t* pads, const double* X, double* X_tmp,
+                     double* Y, const double* A, int64_t a_rows,
+                     const double* B, int64_t b_rows);
+
+/* ---- vector kernels (interior only; ghosts untouched) --------------------- */
+/* z = a*x + b*y.  Replaces spl StencilVector `a*v + w` algebra used at
+ * `sources/solvers.py:106,107,124,217`.  z may alias x or y.                  */
+int poms_vec_axpby(poms_ctx* ctx, const poms_layout* L, double a, const double* x,
+                   double b, const double* y, double* z, void* stream);
+/* z = a*x (b-free form, safe on uninitialised z) */
+int poms_vec_scale(poms_ctx* ctx, const poms_layout* L, double a, const double* x,
+                   double* z, void* stream);
+int poms_vec_fill(poms_ctx* ctx, const poms_layout* L, double v, double* z, void* stream);
+/* Local (un-reduced across ranks) inner product over the interior; result to
+ * out_dev[0].  Replaces `StencilVector.dot` (`sources/solvers.py:87,91,104,111`). */
+int poms_vec_dot(poms_ctx* ctx, const poms_layout* L, const double* x,
+                 const double* y, double* out_dev, void* stream);
+/* PCG update, fused: x += alpha p; r -= alpha q; out_dev[0] = r.r (local).
+ * Replaces `sources/solvers.py:106-111` (minus the discarded A.dot(r) at :109). */
+int poms_pcg_update(poms_ctx* ctx, const poms_layout* L, double alpha, double* x,
+                    const double* p, double* r, const double* q, double* out_dev,
+                    void* stream);
+/* Reduce `count` partials from the context scratch into out_dev[0]. */
+int poms_reduce_partials(poms_ctx* ctx, int64_t count, double* out_dev, void* stream);
+
+/* ---- inter-grid transfer (knot insertion) --------------------------------- */
+/* P_d are HOST dense row-major (nf_global_d x nc_d) prolongation factors
+ * (`P1 = matrix_multi_stages(Ts, nc, p, Tc)`, `sources/mg_jac.py:67-70`).
+ * Fine vectors use `fine` layout (local slab, axis-0 global offset g0);
+ * coarse vectors are dense (no ghosts) C-order nc0*nc1*nc2 (2D: nc0 = 1).
+ * nc_d <= 32.                                                                 */
+int poms_transfer_create(poms_ctx* ctx, int ndim, const poms_layout* fine,
+                         int64_t g0, const int64_t* nf_global, const int64_t* nc,
+                         const double* const* P, poms_transfer** tr);
+int poms_transfer_destroy(poms_transfer* tr);
+/* coarse = (P0 (x) P1 (x) P2)^T fine  (local slab contribution; the caller
+ * all-reduces across ranks).  Replaces `rc = R.dot(rf.toarray())`,
+ * `sources/mg_jac.py:94`.                                                     */
+int poms_restrict(poms_transfer* tr, const double* fine, double* coarse, void* stream);
+/* fine += (P0 (x) P1 (x) P2) coarse on the local slab.
+ * Replaces `xc_p = P.dot(xc)` + `xf = xf + rf` (`sources/mg_jac.py:102-112`). */
+int poms_prolong_add(poms_transfer* tr, const double* coarse, double* fine, void* stream);
+
+/* ---- coarse solve ---------------------------------------------------------- */
+/* y = Minv x with a dense (n x n) row-major DEVICE matrix (the factorised
+ * Galerkin coarse operator).  Replaces `splu(Ac).solve(rc)`,
+ * `sources/mg_jac.py:98-99`.                                                  */
+int poms_dense_matvec(poms_ctx* ctx, int64_t n, const double* Minv, const double* x,
+                      double* y, void* stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* POMS_HIP_H */

@@ -1,0 +1,239 @@
+"""CPU ORACLE -- test infrastructure only, never part of the product path.
+
+Only ``tests/``, ``__graft_entry__.smoke()`` and ``bench.py``'s ``cpu_baseline``
+leg may import this module, and only as the checker.  It restates the
+reference algorithm of the hot path in NumPy/SciPy on global arrays (no
+padding tricks, no sum factorisation of the test operator), each function
+citing the reference line it follows.
+
+Pinning: ``tests/test_oracle_golden.py`` checks these functions against the
+golden vectors generated from the reference itself (``tests/golden/make_golden.py``
+imports `pyccel/pyccel_functions.py`, `sources/solvers.py`,
+`sources/matrix_assembler.py`, `sources/multilevels.py`, `sources/utils.py`
+and runs `sources/mg_jac.py` in this container).  The spl library the
+reference delegates to is absent (`requirements.txt:4`, unpinned); where a
+result depends only on spl (`matrix_multi_stages`) parity is pinned by
+properties instead.
+"""
+from __future__ import annotations
+
+from math import sqrt
+
+import numpy as np
+import scipy.sparse as sp
+from scipy.sparse.linalg import splu
+
+__all__ = [
+    "band_dense", "band_csr", "kron_dot_pyccel_2d", "kron_product_apply", "kron_sum_apply",
+    "kron_sum_csr", "kron_sum_diag", "residual", "damped_jacobi", "jacobi", "pcg",
+    "vcycle_two_level", "knots_to_insert",
+]
+
+
+# ---------------------------------------------------------------------------
+# 1D band helpers (spl 1D StencilMatrix: M[i, k] = a(i, i+k-p))
+# ---------------------------------------------------------------------------
+def band_dense(band: np.ndarray) -> np.ndarray:
+    n, w = band.shape
+    p = (w - 1) // 2
+    A = np.zeros((n, n))
+    for k in range(w):
+        off = k - p
+        i = np.arange(max(0, -off), min(n, n - off))
+        A[i, i + off] = band[i, k]
+    return A
+
+
+def band_csr(band: np.ndarray) -> sp.csr_matrix:
+    return sp.csr_matrix(band_dense(band))
+
+
+# ---------------------------------------------------------------------------
+# pyccel/pyccel_functions.py:4-21 -- the native Kron kernel, loop semantics
+# ---------------------------------------------------------------------------
+def kron_dot_pyccel_2d(starts, ends, pads, X, X_tmp, Y, A, B):
+    """Restatement of `kron_dot_pyccel_2d` (`pyccel/pyccel_functions.py:4-21`).
+
+    Pass 1 (:12-15) runs over the first-axis rows INCLUDING ghosts
+    ``j1 in [s1-p1, e1+p1]`` and the owned columns; pass 2 (:17-19) over owned
+    rows.  Vectorised over the owned column range, loops kept over rows/taps.
+    """
+    s1, s2 = int(starts[0]), int(starts[1])
+    e1, e2 = int(ends[0]), int(ends[1])
+    p1, p2 = int(pads[0]), int(pads[1])
+    cols = np.arange(s2, e2 + 1)
+    lc = cols - s2 + p2                         # local padded column of i2
+    for j1 in range(s1 - p1, e1 + p1 + 1):      # :12
+        acc = np.zeros(len(cols))
+        for k in range(2 * p2 + 1):             # :15 sum over k
+            acc += X[j1 + p1 - s1, cols - s2 + k] * B[cols, k]
+        X_tmp[j1 + p1 - s1, lc] = acc
+    for i1 in range(s1, e1 + 1):                # :17
+        acc = np.zeros(len(cols))
+        for k in range(2 * p1 + 1):             # :19
+            acc += A[i1, k] * X_tmp[i1 - s1 + k, lc]
+        Y[i1 - s1 + p1, lc] = acc
+    return Y
+
+
+# ---------------------------------------------------------------------------
+# Operators on global (unpadded) arrays, zero ghosts (non-periodic)
+# ---------------------------------------------------------------------------
+def _axis_apply(F: sp.csr_matrix, X: np.ndarray, axis: int) -> np.ndarray:
+    Xm = np.moveaxis(X, axis, 0)
+    sh = Xm.shape
+    Y = F @ Xm.reshape(sh[0], -1)
+    return np.moveaxis(np.asarray(Y).reshape((F.shape[0],) + sh[1:]), 0, axis)
+
+
+def kron_product_apply(X: np.ndarray, F: list) -> np.ndarray:
+    """(F0 ⊗ F1 ⊗ ...) vec(X), C order (`utils.kron_dot_ref`, `sources/utils.py:43-62`)."""
+    Y = X
+    for d, f in enumerate(F):
+        Y = _axis_apply(band_csr(f) if not sp.issparse(f) else f, Y, d)
+    return Y
+
+
+def kron_sum_apply(X: np.ndarray, M: list, K: list, c: float = 1.0) -> np.ndarray:
+    """``c ⊗M + Σ_d (K on axis d, M elsewhere)`` applied term by term.
+
+    This is the operator the reference assembles for ``-Δu + u``
+    (`sources/matrix_assembler.py:173`: ``bi0*bj0 + bix*bjx + biy*bjy``), one
+    Kronecker term at a time (no shared partial products, unlike the kernel).
+    """
+    nd = X.ndim
+    Mc = [band_csr(m) for m in M]
+    Kc = [band_csr(k) for k in K]
+    Y = c * kron_product_apply(X, Mc)
+    for d in range(nd):
+        Y = Y + kron_product_apply(X, [Kc[e] if e == d else Mc[e] for e in range(nd)])
+    return Y
+
+
+def kron_sum_csr(M: list, K: list, c: float = 1.0) -> sp.csr_matrix:
+    nd = len(M)
+    Mc = [band_csr(m) for m in M]
+    Kc = [band_csr(k) for k in K]
+
+    def kr(ms):
+        out = ms[0]
+        for m in ms[1:]:
+            out = sp.kron(out, m, format="csr")
+        return out
+
+    A = c * kr(Mc)
+    for d in range(nd):
+        A = A + kr([Kc[e] if e == d else Mc[e] for e in range(nd)])
+    return A.tocsr()
+
+
+def kron_sum_diag(M: list, K: list, c: float = 1.0) -> np.ndarray:
+    nd = len(M)
+    dM = [m[:, (m.shape[1] - 1) // 2] for m in M]
+    dK = [k[:, (k.shape[1] - 1) // 2] for k in K]
+
+    def outer(vs):
+        out = vs[0]
+        for v in vs[1:]:
+            out = np.multiply.outer(out, v)
+        return out
+
+    D = c * outer(dM)
+    for d in range(nd):
+        D = D + outer([dK[e] if e == d else dM[e] for e in range(nd)])
+    return D
+
+
+def residual(apply, b, x):
+    """``r = b - A.dot(x)`` (`sources/solvers.py:85`)."""
+    return b - apply(x)
+
+
+# ---------------------------------------------------------------------------
+# sources/solvers.py restated on NumPy arrays
+# ---------------------------------------------------------------------------
+def jacobi(diag, b):
+    """`sources/solvers.py:139-163`: x = b / diag(A)."""
+    return b / diag
+
+
+def damped_jacobi(apply, diag, b, x0=None, tol=1e-6, maxiter=10, return_info=False):
+    """`sources/solvers.py:167-235` (omega = 2/3, break after the update)."""
+    omega = 2.0 / 3
+    x = 0.0 * b.copy() if x0 is None else x0.copy()
+    tol_sqr = tol ** 2
+    k, nrmr = 0, 0.0
+    for k in range(1, maxiter + 1):
+        r = b - apply(x)                # :209
+        dr = omega * r / diag           # :211-213
+        x = x + dr                      # :217
+        nrmr = float(np.vdot(dr, dr))   # :219
+        if nrmr < tol_sqr:
+            k -= 1
+            break
+    if return_info:
+        return x, {"niter": k, "success": nrmr < tol_sqr, "res_norm": sqrt(nrmr)}
+    return x
+
+
+def pcg(apply, psolve, b, x0=None, tol=1e-6, maxiter=100):
+    """`sources/solvers.py:69-135` (stop test ``r.r < tol*||r0||``, :113)."""
+    x = 0.0 * b.copy() if x0 is None else x0.copy()
+    r = b - apply(x)
+    nrmr0 = sqrt(float(np.vdot(r, r)))
+    s = psolve(r)
+    p = s
+    sr = float(np.vdot(s, r))
+    k, nrmr = 0, nrmr0 * nrmr0
+    for k in range(1, maxiter + 1):
+        q = apply(p)
+        alpha = sr / float(np.vdot(p, q))
+        x = x + alpha * p
+        r = r - alpha * q
+        nrmr = float(np.vdot(r, r))
+        if nrmr < tol * nrmr0:
+            k -= 1
+            break
+        s = psolve(r)
+        srold = sr
+        sr = float(np.vdot(s, r))
+        beta = sr / srold
+        p = s + beta * p
+    return x, {"niter": k, "success": nrmr < tol * nrmr0, "res_norm": sqrt(nrmr)}
+
+
+# ---------------------------------------------------------------------------
+# sources/multilevels.py:7-33 and the mg_jac.py V-cycle
+# ---------------------------------------------------------------------------
+def knots_to_insert(Tf, nf, pf, Tc, nc, pc):
+    """Interior knots ``Tf[pf+1:nf]`` absent (exact equality) from ``Tc[pc+1:nc+1]``.
+
+    The reference scans ``Tc`` from ``pc+1`` until the first larger knot or
+    ``j > nc`` (`sources/multilevels.py:17-29`); on a sorted ``Tc`` that is
+    membership in ``Tc[pc+1 .. nc]``.
+    """
+    coarse = set(float(t) for t in Tc[pc + 1:nc + 1])
+    return np.array([t for t in Tf[pf + 1:nf] if float(t) not in coarse], dtype=np.float64)
+
+
+def vcycle_two_level(M, K, P1, b, c=1.0, tol=1e-6, maxiter=10, x0=None):
+    """`sources/mg_jac.py:84-119` on global arrays with materialised R, P, Ac, splu."""
+    nd = b.ndim
+    A = kron_sum_csr(M, K, c)
+    D = kron_sum_diag(M, K, c).reshape(-1)
+    apply = lambda v: A @ v
+    psolve = lambda r: damped_jacobi(apply, D, r)
+    bf = b.reshape(-1)
+    xf, info_pre = pcg(apply, psolve, bf, x0=None if x0 is None else x0.reshape(-1), tol=tol, maxiter=maxiter)
+    Pm = sp.csr_matrix(P1)
+    P = Pm
+    for _ in range(nd - 1):
+        P = sp.kron(P, Pm, format="csr")
+    R = P.T.tocsr()
+    Ac = (R @ A @ P).tocsc()
+    rf = bf - apply(xf)
+    rc = R @ rf
+    xc = splu(Ac).solve(rc)
+    xf = xf + P @ xc
+    xf2, info_pos = pcg(apply, psolve, bf, x0=xf, tol=tol, maxiter=maxiter)
+    return xf2.reshape(b.shape), info_pre, info_pos

@@ -1,0 +1,108 @@
+"""ctypes binding of ``libpoms_hip.so`` (the C-ABI declared in ``include/poms_hip.h``).
+
+This is the reference-side binding a maintainer would add: a
+thin loader, one ``argtypes`` line per entry point, and a status check that
+turns a non-zero return into ``PomsError(poms_last_error())``.  There is no
+fallback: if the library is missing or cannot be loaded the import fails
+loudly.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+import re
+from pathlib import Path
+
+_HERE = Path(__file__).resolve().parent
+LIB_PATH = Path(os.environ.get("POMS_HIP_LIB", _HERE / "libpoms_hip.so"))
+HEADER_PATH = _HERE.parent / "include" / "poms_hip.h"
+
+FORM_SINGLE = 0
+FORM_SUM = 1
+
+
+class PomsError(RuntimeError):
+    """A libpoms_hip entry point returned a non-zero status."""
+
+
+class Layout(C.Structure):
+    _fields_ = [("n", C.c_int64 * 3), ("pads", C.c_int64 * 3)]
+
+    @classmethod
+    def make(cls, n, pads):
+        lay = cls()
+        for d in range(3):
+            lay.n[d] = int(n[d])
+            lay.pads[d] = int(pads[d])
+        return lay
+
+
+_vp = C.c_void_p
+_i64 = C.c_int64
+_d = C.c_double
+_i = C.c_int
+_pp = C.POINTER(C.c_void_p)
+_LP = C.POINTER(Layout)
+
+# name -> argtypes (restype is int unless listed in _RESTYPES)
+_SIGS = {
+    "poms_abi_version": [],
+    "poms_last_error": [],
+    "poms_device_count": [C.POINTER(_i)],
+    "poms_ctx_create": [_i, _pp],
+    "poms_ctx_destroy": [_vp],
+    "poms_synchronize": [_vp, _vp],
+    "poms_op_create": [_vp, _i, _LP, _i, _i, C.POINTER(C.c_void_p), _i64, _i64, _pp],
+    "poms_op_destroy": [_vp],
+    "poms_op_set_chunk": [_vp, _i],
+    "poms_op_apply": [_vp, _vp, _vp, _i64, _i64, _vp],
+    "poms_op_residual": [_vp, _vp, _vp, _vp, _i64, _i64, _vp],
+    "poms_op_jacobi_sweep": [_vp, _d, _vp, _vp, _vp, _i64, _i64, _i, _vp],
+    "poms_op_diag_scale": [_vp, _d, _vp, _vp, _i, _vp],
+    "poms_op_last_partials": [_vp, C.POINTER(_i64)],
+    "poms_kron_dot_2d": [_vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _i64, _vp, _i64],
+    "poms_vec_axpby": [_vp, _LP, _d, _vp, _d, _vp, _vp, _vp],
+    "poms_vec_scale": [_vp, _LP, _d, _vp, _vp, _vp],
+    "poms_vec_fill": [_vp, _LP, _d, _vp, _vp],
+    "poms_vec_dot": [_vp, _LP, _vp, _vp, _vp, _vp],
+    "poms_pcg_update": [_vp, _LP, _d, _vp, _vp, _vp, _vp, _vp, _vp],
+    "poms_reduce_partials": [_vp, _i64, _vp, _vp],
+    "poms_transfer_create": [_vp, _i, _LP, _i64, _vp, _vp, C.POINTER(C.c_void_p), _pp],
+    "poms_transfer_destroy": [_vp],
+    "poms_restrict": [_vp, _vp, _vp, _vp],
+    "poms_prolong_add": [_vp, _vp, _vp, _vp],
+    "poms_dense_matvec": [_vp, _i64, _vp, _vp, _vp, _vp],
+}
+_RESTYPES = {"poms_last_error": C.c_char_p}
+
+
+def header_symbols(path: Path = HEADER_PATH) -> list[str]:
+    """Every function the C header declares (used by the export test)."""
+    text = path.read_text()
+    return sorted(set(re.findall(r"^\s*(?:int|const char\*)\s+(poms_\w+)\s*\(", text, re.M)))
+
+
+def _load() -> C.CDLL:
+    if not LIB_PATH.exists():
+        raise ImportError(
+            f"libpoms_hip.so not found at {LIB_PATH}: build it with "
+            "`python -c 'import __graft_entry__ as g; g.build()'` (hipcc, gfx950)")
+    lib = C.CDLL(str(LIB_PATH))
+    for name, args in _SIGS.items():
+        fn = getattr(lib, name)
+        fn.argtypes = args
+        fn.restype = _RESTYPES.get(name, C.c_int)
+    return lib
+
+
+lib = _load()
+
+
+def check(status: int, what: str = "") -> None:
+    if status != 0:
+        msg = lib.poms_last_error().decode(errors="replace")
+        raise PomsError(f"{what}: {msg}" if what else msg)
+
+
+def call(name: str, *args) -> None:
+    check(getattr(lib, name)(*args), name)

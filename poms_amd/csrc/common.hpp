@@ -1,0 +1,75 @@
+// Shared definitions for the gfx950 kernels of libpoms_hip.so.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <cstdint>
+#include <string>
+
+namespace poms {
+
+constexpr int kBlock = 256;  // 4 wave64s per workgroup
+
+enum Form : int { FORM_SINGLE = 0, FORM_SUM = 1 };
+enum Epi : int { EPI_APPLY = 0, EPI_RESID = 1, EPI_JACOBI = 2 };
+
+// Geometry of one fused Kronecker launch (all extents local to this rank's slab).
+struct KronGeom {
+    int64_t s0, s1;      // plane / row strides of the padded layout (doubles)
+    int n0, n1, n2;      // interior extents
+    int pd0, pd1, pd2;   // storage pads (ghost widths)
+    int g0;              // global index of local plane 0 (axis-0 coefficient rows)
+    int z_begin, z_end;  // output planes [z_begin, z_end)
+    int chunk;           // output planes per workgroup (3D)
+    int tiles2, tiles1, nchunks;
+};
+
+// Padded row layout used by the row-wise vector kernels.
+struct RowGeom {
+    int64_t s0, s1;
+    int n0, n1, n2;
+    int pd0, pd1, pd2;
+};
+
+// One axis of a Kronecker transfer (restriction / prolongation), see transfer.hip.
+struct AxisPass {
+    int64_t nA, nB1, nB2;                     // independent thread space
+    int64_t in_base, in_sa, in_sb1, in_sb2, in_si;
+    int64_t out_base, out_sa, out_sb1, out_sb2, out_si;
+    int nI;          // fine extent of the contracted / expanded axis (local)
+    int nJ;          // coarse extent
+    int goff;        // global fine row of local i = 0
+    int accumulate;  // prolongation: out += (1) or out = (0)
+};
+
+// Device pointers of one fused Kronecker launch.
+struct KronPtrs {
+    const double* x;
+    double* y;
+    const double* b;
+    const double *a0t, *b0t, *a1, *b1, *a2, *b2;
+    double* partial;
+};
+
+void set_error(const std::string& msg);
+
+// Block-wide (256 threads) sum; result valid in thread 0.
+__device__ inline double block_sum_256(double v, double* red4) {
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off, 64);
+    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    if (lane == 0) red4[wv] = v;
+    __syncthreads();
+    double s = 0.0;
+    if (threadIdx.x == 0) s = (red4[0] + red4[1]) + (red4[2] + red4[3]);
+    return s;
+}
+
+}  // namespace poms
+
+#define POMS_HIP_CHECK(expr)                                                   \
+    do {                                                                       \
+        hipError_t _e = (expr);                                                \
+        if (_e != hipSuccess) {                                                \
+            ::poms::set_error(std::string(#expr) + ": " + hipGetErrorString(_e)); \
+            return 1;                                                          \
+        }                                                                      \
+    } while (0)

@@ -1,0 +1,532 @@
+// extern "C" boundary of libpoms_hip.so (declared in include/poms_hip.h).
+#include "common.hpp"
+#include "../../include/poms_hip.h"
+
+#include <algorithm>
+#include <cstring>
+#include <vector>
+
+namespace poms {
+
+static thread_local std::string g_err;
+void set_error(const std::string& msg) { g_err = msg; }
+
+int kron_launch(int pmax, bool is3d, int form, int epi, const KronPtrs& p, const KronGeom& g,
+                double omega, hipStream_t st);
+int kron_tile_rows();
+int kron_tile_cols();
+int vec_launch(int op, const RowGeom& g, double a, double b, const double* x, const double* y,
+               double* z, double* w, const double* q, double* partial, hipStream_t st,
+               int* nblk_out);
+int reduce_launch(const double* partial, int count, double* out, hipStream_t st);
+int diag_scale_launch(bool is3d, int form, const RowGeom& g, int P, int g0, double scale,
+                      const double* b, double* x, const double* a0t, const double* b0t,
+                      const double* a1, const double* b1, const double* a2, const double* b2,
+                      double* partial, hipStream_t st, int* nblk_out);
+int dense_matvec_launch(int n, const double* M, const double* x, double* y, hipStream_t st);
+int transfer_pass_launch(bool restrict_dir, int ncm, const AxisPass& ps, const double* Pm,
+                         const double* in, double* out, hipStream_t st);
+
+enum { V_AXPBY = 0, V_SCALE = 1, V_FILL = 2, V_DOT = 3, V_PCGUPD = 4 };
+constexpr int64_t kScratch = 1 << 16;
+
+}  // namespace poms
+
+using namespace poms;
+
+struct poms_ctx {
+    int device = 0;
+    double* scratch = nullptr;  // reduction partials
+};
+
+struct poms_op {
+    poms_ctx* ctx = nullptr;
+    int ndim = 3, form = FORM_SUM, pmax = 1, chunk = 0;
+    poms_layout L{};
+    int64_t g0 = 0, n0g = 1;
+    double *a0t = nullptr, *b0t = nullptr, *a1 = nullptr, *b1 = nullptr, *a2 = nullptr, *b2 = nullptr;
+    int64_t last_partials = 0;
+};
+
+struct poms_transfer {
+    poms_ctx* ctx = nullptr;
+    int ndim = 3, ncm = 16;
+    poms_layout L{};
+    int64_t g0 = 0;
+    int64_t nf[3]{}, nc[3]{};
+    double* Pm[3]{};
+    double *t0 = nullptr, *t1 = nullptr;
+};
+
+static hipStream_t as_stream(void* s) { return reinterpret_cast<hipStream_t>(s); }
+
+static bool layout_ok(const poms_layout* L) {
+    if (!L) return false;
+    for (int d = 0; d < 3; ++d)
+        if (L->n[d] < 1 || L->pads[d] < 0) return false;
+    return true;
+}
+
+static RowGeom row_geom(const poms_layout* L) {
+    RowGeom g;
+    const int64_t c2 = L->n[2] + 2 * L->pads[2];
+    const int64_t c1 = L->n[1] + 2 * L->pads[1];
+    g.s1 = c2;
+    g.s0 = c1 * c2;
+    g.n0 = (int)L->n[0];
+    g.n1 = (int)L->n[1];
+    g.n2 = (int)L->n[2];
+    g.pd0 = (int)L->pads[0];
+    g.pd1 = (int)L->pads[1];
+    g.pd2 = (int)L->pads[2];
+    return g;
+}
+
+static int upload(const double* host, size_t n, double** dev) {
+    POMS_HIP_CHECK(hipMalloc(reinterpret_cast<void**>(dev), std::max<size_t>(n, 1) * sizeof(double)));
+    if (n) POMS_HIP_CHECK(hipMemcpy(*dev, host, n * sizeof(double), hipMemcpyHostToDevice));
+    return 0;
+}
+
+extern "C" {
+
+int poms_abi_version(void) { return POMS_ABI_VERSION; }
+
+const char* poms_last_error(void) { return g_err.c_str(); }
+
+int poms_device_count(int* count) {
+    if (!count) { set_error("null count"); return 1; }
+    POMS_HIP_CHECK(hipGetDeviceCount(count));
+    return 0;
+}
+
+int poms_ctx_create(int device, poms_ctx** ctx) {
+    if (!ctx) { set_error("null ctx out"); return 1; }
+    POMS_HIP_CHECK(hipSetDevice(device));
+    auto* c = new poms_ctx();
+    c->device = device;
+    if (hipMalloc(reinterpret_cast<void**>(&c->scratch), kScratch * sizeof(double)) != hipSuccess) {
+        delete c;
+        set_error("hipMalloc scratch failed");
+        return 1;
+    }
+    *ctx = c;
+    return 0;
+}
+
+int poms_ctx_destroy(poms_ctx* ctx) {
+    if (!ctx) return 0;
+    if (ctx->scratch) (void)hipFree(ctx->scratch);
+    delete ctx;
+    return 0;
+}
+
+int poms_synchronize(poms_ctx* ctx, void* stream) {
+    (void)ctx;
+    POMS_HIP_CHECK(hipStreamSynchronize(as_stream(stream)));
+    return 0;
+}
+
+int poms_op_create(poms_ctx* ctx, int ndim, const poms_layout* layout, int form, int pmax,
+                   const double* const* f, int64_t g0, int64_t n0_global, poms_op** op) {
+    if (!ctx || !op || !f) { set_error("poms_op_create: null argument"); return 1; }
+    if (ndim < 1 || ndim > 3) { set_error("poms_op_create: ndim must be 1..3"); return 1; }
+    if (pmax < 1 || pmax > 5) { set_error("poms_op_create: pmax must be 1..5"); return 1; }
+    if (form != FORM_SUM && form != FORM_SINGLE) { set_error("poms_op_create: bad form"); return 1; }
+    if (!layout_ok(layout)) { set_error("poms_op_create: bad layout"); return 1; }
+    const bool is3d = ndim == 3;
+    if (!is3d && (layout->n[0] != 1 || layout->pads[0] != 0)) {
+        set_error("poms_op_create: 1D/2D layouts need n[0]=1, pads[0]=0");
+        return 1;
+    }
+    for (int d = 0; d < 3; ++d)
+        if (layout->pads[d] > pmax) { set_error("poms_op_create: storage pad exceeds pmax"); return 1; }
+    if (is3d && (g0 < 0 || g0 + layout->n[0] > n0_global)) {
+        set_error("poms_op_create: slab [g0, g0+n0) outside [0, n0_global)");
+        return 1;
+    }
+    const bool sum = form == FORM_SUM;
+    if (!f[2] || !f[4] || (sum && (!f[3] || !f[5])) || (is3d && (!f[0] || (sum && !f[1])))) {
+        set_error("poms_op_create: missing factor array");
+        return 1;
+    }
+    POMS_HIP_CHECK(hipSetDevice(ctx->device));
+    const int W = 2 * pmax + 1;
+    auto* o = new poms_op();
+    o->ctx = ctx;
+    o->ndim = ndim;
+    o->form = form;
+    o->pmax = pmax;
+    o->L = *layout;
+    o->g0 = is3d ? g0 : 0;
+    o->n0g = is3d ? n0_global : 1;
+    int rc = 0;
+    if (is3d) {
+        // Transposed (column) bands of the axis-0 factors, padded by pmax rows on
+        // both sides: at[(j+P)*W + s] = F[j-P+s][2P-s].
+        const int64_t nrow = n0_global + 2 * pmax;
+        std::vector<double> ta(nrow * W, 0.0), tb(nrow * W, 0.0);
+        for (int64_t j = -pmax; j < n0_global + pmax; ++j)
+            for (int s = 0; s < W; ++s) {
+                const int64_t i = j - pmax + s;
+                if (i < 0 || i >= n0_global) continue;
+                ta[(j + pmax) * W + s] = f[0][i * W + (2 * pmax - s)];
+                if (sum) tb[(j + pmax) * W + s] = f[1][i * W + (2 * pmax - s)];
+            }
+        rc |= upload(ta.data(), ta.size(), &o->a0t);
+        if (sum) rc |= upload(tb.data(), tb.size(), &o->b0t);
+    }
+    rc |= upload(f[2], (size_t)layout->n[1] * W, &o->a1);
+    rc |= upload(f[4], (size_t)layout->n[2] * W, &o->a2);
+    if (sum) {
+        rc |= upload(f[3], (size_t)layout->n[1] * W, &o->b1);
+        rc |= upload(f[5], (size_t)layout->n[2] * W, &o->b2);
+    }
+    if (rc) { poms_op_destroy(o); return 1; }
+    *op = o;
+    return 0;
+}
+
+int poms_op_destroy(poms_op* o) {
+    if (!o) return 0;
+    for (double* p : {o->a0t, o->b0t, o->a1, o->b1, o->a2, o->b2})
+        if (p) (void)hipFree(p);
+    delete o;
+    return 0;
+}
+
+int poms_op_set_chunk(poms_op* op, int chunk) {
+    if (!op || chunk < 0) { set_error("poms_op_set_chunk: bad argument"); return 1; }
+    op->chunk = chunk;
+    return 0;
+}
+
+static int op_geom(poms_op* o, int64_t zb, int64_t ze, KronGeom& g) {
+    const bool is3d = o->ndim == 3;
+    const RowGeom r = row_geom(&o->L);
+    g.s0 = r.s0;
+    g.s1 = r.s1;
+    g.n0 = r.n0; g.n1 = r.n1; g.n2 = r.n2;
+    g.pd0 = r.pd0; g.pd1 = r.pd1; g.pd2 = r.pd2;
+    g.g0 = (int)o->g0;
+    g.tiles2 = (int)((o->L.n[2] + kron_tile_cols() - 1) / kron_tile_cols());
+    g.tiles1 = (int)((o->L.n[1] + kron_tile_rows() - 1) / kron_tile_rows());
+    if (!is3d) {
+        g.z_begin = 0; g.z_end = 1; g.chunk = 1; g.nchunks = 1;
+        return 0;
+    }
+    if (zb < 0 || ze > o->L.n[0] || zb > ze) { set_error("plane range outside the slab"); return 1; }
+    g.z_begin = (int)zb;
+    g.z_end = (int)ze;
+    const int nz = (int)(ze - zb);
+    int chunk = o->chunk;
+    if (chunk <= 0) {
+        const int tiles = g.tiles2 * g.tiles1;
+        const int want = std::max(1, (2048 + tiles - 1) / tiles);
+        chunk = std::max(16, (nz + want - 1) / want);
+    }
+    chunk = std::max(1, std::min(chunk, std::max(nz, 1)));
+    g.chunk = chunk;
+    g.nchunks = nz == 0 ? 0 : (nz + chunk - 1) / chunk;
+    return 0;
+}
+
+static int op_run(poms_op* o, int epi, double omega, const double* x, double* y, const double* b,
+                  int64_t zb, int64_t ze, int want_norm, void* stream) {
+    if (!o || !x || !y) { set_error("null operator or vector"); return 1; }
+    if (epi != EPI_APPLY && !b) { set_error("null right-hand side"); return 1; }
+    KronGeom g;
+    if (op_geom(o, zb, ze, g)) return 1;
+    const int64_t nblk = (int64_t)g.tiles2 * g.tiles1 * g.nchunks;
+    if (nblk == 0) { o->last_partials = 0; return 0; }
+    if (want_norm && nblk > kScratch) { set_error("too many blocks for norm scratch"); return 1; }
+    KronPtrs p{x, y, b, o->a0t, o->b0t, o->a1, o->b1, o->a2, o->b2,
+               want_norm ? o->ctx->scratch : nullptr};
+    if (kron_launch(o->pmax, o->ndim == 3, o->form, epi, p, g, omega, as_stream(stream))) return 1;
+    POMS_HIP_CHECK(hipGetLastError());
+    o->last_partials = want_norm ? nblk : 0;
+    return 0;
+}
+
+int poms_op_apply(poms_op* op, const double* x, double* y, int64_t zb, int64_t ze, void* stream) {
+    return op_run(op, EPI_APPLY, 0.0, x, y, nullptr, zb, ze, 0, stream);
+}
+
+int poms_op_residual(poms_op* op, const double* b, const double* x, double* r, int64_t zb,
+                     int64_t ze, void* stream) {
+    return op_run(op, EPI_RESID, 0.0, x, r, b, zb, ze, 0, stream);
+}
+
+int poms_op_jacobi_sweep(poms_op* op, double omega, const double* b, const double* x_in,
+                         double* x_out, int64_t zb, int64_t ze, int want_norm, void* stream) {
+    if (x_in == x_out) { set_error("jacobi sweep: x_out must not alias x_in"); return 1; }
+    return op_run(op, EPI_JACOBI, omega, x_in, x_out, b, zb, ze, want_norm, stream);
+}
+
+int poms_op_diag_scale(poms_op* o, double scale, const double* b, double* x, int want_norm,
+                       void* stream) {
+    if (!o || !b || !x) { set_error("poms_op_diag_scale: null argument"); return 1; }
+    const RowGeom g = row_geom(&o->L);
+    int nb = 0;
+    diag_scale_launch(o->ndim == 3, o->form, g, o->pmax, (int)o->g0, scale, b, x, o->a0t, o->b0t,
+                      o->a1, o->b1, o->a2, o->b2, want_norm ? o->ctx->scratch : nullptr,
+                      as_stream(stream), &nb);
+    POMS_HIP_CHECK(hipGetLastError());
+    o->last_partials = want_norm ? nb : 0;
+    return 0;
+}
+
+int poms_op_last_partials(poms_op* op, int64_t* count) {
+    if (!op || !count) { set_error("null argument"); return 1; }
+    *count = op->last_partials;
+    return 0;
+}
+
+int poms_kron_dot_2d(poms_ctx* ctx, const int64_t* starts, const int64_t* ends,
+                     const int64_t* pads, const double* X, double* X_tmp, double* Y,
+                     const double* A, int64_t a_rows, const double* B, int64_t b_rows) {
+    (void)X_tmp;
+    if (!ctx || !starts || !ends || !pads || !X || !Y || !A || !B) {
+        set_error("poms_kron_dot_2d: null argument");
+        return 1;
+    }
+    const int64_t n1 = ends[0] - starts[0] + 1, n2 = ends[1] - starts[1] + 1;
+    const int p1 = (int)pads[0], p2 = (int)pads[1];
+    if (n1 < 1 || n2 < 1 || p1 < 1 || p2 < 1 || p1 > 5 || p2 > 5) {
+        set_error("poms_kron_dot_2d: bad extents or pads (1..5)");
+        return 1;
+    }
+    if (starts[0] < 0 || ends[0] >= a_rows || starts[1] < 0 || ends[1] >= b_rows) {
+        set_error("poms_kron_dot_2d: starts/ends outside the band arrays");
+        return 1;
+    }
+    const int pm = std::max(p1, p2), W = 2 * pm + 1;
+    // local, re-centred band rows of width 2*pm+1
+    std::vector<double> fa(n1 * W, 0.0), fb(n2 * W, 0.0);
+    for (int64_t i = 0; i < n1; ++i)
+        for (int k = 0; k < 2 * p1 + 1; ++k) fa[i * W + k + pm - p1] = A[(starts[0] + i) * (2 * p1 + 1) + k];
+    for (int64_t i = 0; i < n2; ++i)
+        for (int k = 0; k < 2 * p2 + 1; ++k) fb[i * W + k + pm - p2] = B[(starts[1] + i) * (2 * p2 + 1) + k];
+    poms_layout L{{1, n1, n2}, {0, p1, p2}};
+    const double* f[6] = {nullptr, nullptr, fa.data(), nullptr, fb.data(), nullptr};
+    poms_op* op = nullptr;
+    if (poms_op_create(ctx, 2, &L, FORM_SINGLE, pm, f, 0, 1, &op)) return 1;
+    const size_t nel = (size_t)(n1 + 2 * p1) * (n2 + 2 * p2);
+    double *dx = nullptr, *dy = nullptr;
+    int rc = 0;
+    if (hipMalloc(reinterpret_cast<void**>(&dx), nel * sizeof(double)) != hipSuccess ||
+        hipMalloc(reinterpret_cast<void**>(&dy), nel * sizeof(double)) != hipSuccess) {
+        set_error("poms_kron_dot_2d: hipMalloc failed");
+        rc = 1;
+    }
+    if (!rc && (hipMemcpy(dx, X, nel * sizeof(double), hipMemcpyHostToDevice) != hipSuccess ||
+                hipMemcpy(dy, Y, nel * sizeof(double), hipMemcpyHostToDevice) != hipSuccess)) {
+        set_error("poms_kron_dot_2d: upload failed");
+        rc = 1;
+    }
+    if (!rc) rc = poms_op_apply(op, dx, dy, 0, 1, nullptr);
+    if (!rc && hipMemcpy(Y, dy, nel * sizeof(double), hipMemcpyDeviceToHost) != hipSuccess) {
+        set_error("poms_kron_dot_2d: download failed");
+        rc = 1;
+    }
+    if (dx) (void)hipFree(dx);
+    if (dy) (void)hipFree(dy);
+    poms_op_destroy(op);
+    return rc;
+}
+
+// ---- vector kernels -----------------------------------------------------------
+static int vec_common(poms_ctx* ctx, const poms_layout* L, int op, double a, double b,
+                      const double* x, const double* y, double* z, double* w, const double* q,
+                      double* out_dev, void* stream) {
+    if (!ctx || !layout_ok(L)) { set_error("vector op: bad context or layout"); return 1; }
+    const RowGeom g = row_geom(L);
+    int nb = 0;
+    const bool red = (op == V_DOT || op == V_PCGUPD);
+    if (vec_launch(op, g, a, b, x, y, z, w, q, red ? ctx->scratch : nullptr, as_stream(stream), &nb))
+        return 1;
+    if (red) reduce_launch(ctx->scratch, nb, out_dev, as_stream(stream));
+    POMS_HIP_CHECK(hipGetLastError());
+    return 0;
+}
+
+int poms_vec_axpby(poms_ctx* ctx, const poms_layout* L, double a, const double* x, double b,
+                   const double* y, double* z, void* stream) {
+    if (!x || !y || !z) { set_error("axpby: null vector"); return 1; }
+    return vec_common(ctx, L, V_AXPBY, a, b, x, y, z, nullptr, nullptr, nullptr, stream);
+}
+
+int poms_vec_scale(poms_ctx* ctx, const poms_layout* L, double a, const double* x, double* z,
+                   void* stream) {
+    if (!x || !z) { set_error("scale: null vector"); return 1; }
+    return vec_common(ctx, L, V_SCALE, a, 0.0, x, nullptr, z, nullptr, nullptr, nullptr, stream);
+}
+
+int poms_vec_fill(poms_ctx* ctx, const poms_layout* L, double v, double* z, void* stream) {
+    if (!z) { set_error("fill: null vector"); return 1; }
+    return vec_common(ctx, L, V_FILL, v, 0.0, nullptr, nullptr, z, nullptr, nullptr, nullptr, stream);
+}
+
+int poms_vec_dot(poms_ctx* ctx, const poms_layout* L, const double* x, const double* y,
+                 double* out_dev, void* stream) {
+    if (!x || !y || !out_dev) { set_error("dot: null argument"); return 1; }
+    return vec_common(ctx, L, V_DOT, 0.0, 0.0, x, y, nullptr, nullptr, nullptr, out_dev, stream);
+}
+
+int poms_pcg_update(poms_ctx* ctx, const poms_layout* L, double alpha, double* x, const double* p,
+                    double* r, const double* q, double* out_dev, void* stream) {
+    if (!x || !p || !r || !q || !out_dev) { set_error("pcg_update: null argument"); return 1; }
+    return vec_common(ctx, L, V_PCGUPD, alpha, 0.0, nullptr, p, x, r, q, out_dev, stream);
+}
+
+int poms_reduce_partials(poms_ctx* ctx, int64_t count, double* out_dev, void* stream) {
+    if (!ctx || !out_dev || count < 0 || count > kScratch) { set_error("reduce: bad argument"); return 1; }
+    reduce_launch(ctx->scratch, (int)count, out_dev, as_stream(stream));
+    POMS_HIP_CHECK(hipGetLastError());
+    return 0;
+}
+
+// ---- transfer -------------------------------------------------------------------
+int poms_transfer_create(poms_ctx* ctx, int ndim, const poms_layout* fine, int64_t g0,
+                         const int64_t* nf_global, const int64_t* nc, const double* const* P,
+                         poms_transfer** tr) {
+    if (!ctx || !tr || !nf_global || !nc || !P || !layout_ok(fine)) {
+        set_error("poms_transfer_create: bad argument");
+        return 1;
+    }
+    if (ndim < 1 || ndim > 3) { set_error("poms_transfer_create: ndim 1..3"); return 1; }
+    const bool is3d = ndim == 3;
+    const int d0 = is3d ? 0 : 1;
+    int64_t ncmax = 0;
+    for (int d = d0; d < 3; ++d) {
+        if (!P[d] || nc[d] < 1 || nf_global[d] < 1) { set_error("poms_transfer_create: bad axis"); return 1; }
+        ncmax = std::max(ncmax, nc[d]);
+    }
+    if (ncmax > 32) { set_error("poms_transfer_create: coarse extent > 32"); return 1; }
+    if (!is3d && (fine->n[0] != 1 || fine->pads[0] != 0)) {
+        set_error("poms_transfer_create: 1D/2D layouts need n[0]=1, pads[0]=0");
+        return 1;
+    }
+    for (int d = 1; d < 3; ++d)
+        if (nf_global[d] != fine->n[d]) { set_error("poms_transfer_create: only axis 0 may be sliced"); return 1; }
+    if (is3d && (g0 < 0 || g0 + fine->n[0] > nf_global[0])) { set_error("poms_transfer_create: bad slab"); return 1; }
+    POMS_HIP_CHECK(hipSetDevice(ctx->device));
+    auto* t = new poms_transfer();
+    t->ctx = ctx;
+    t->ndim = ndim;
+    t->ncm = ncmax <= 16 ? 16 : 32;
+    t->L = *fine;
+    t->g0 = is3d ? g0 : 0;
+    int rc = 0;
+    for (int d = 0; d < 3; ++d) {
+        t->nf[d] = (d < d0) ? 1 : nf_global[d];
+        t->nc[d] = (d < d0) ? 1 : nc[d];
+        if (d < d0) continue;
+        std::vector<double> pm(t->nf[d] * t->ncm, 0.0);
+        for (int64_t i = 0; i < t->nf[d]; ++i)
+            for (int64_t j = 0; j < t->nc[d]; ++j) pm[i * t->ncm + j] = P[d][i * t->nc[d] + j];
+        rc |= upload(pm.data(), pm.size(), &t->Pm[d]);
+    }
+    const int64_t n1 = fine->n[1], n2 = fine->n[2];
+    const size_t sz0 = (size_t)t->nc[0] * n1 * n2;
+    const size_t sz1 = (size_t)t->nc[0] * t->nc[1] * n2;
+    if (!rc && hipMalloc(reinterpret_cast<void**>(&t->t0), std::max<size_t>(sz0, 1) * sizeof(double)) != hipSuccess) rc = 1;
+    if (!rc && hipMalloc(reinterpret_cast<void**>(&t->t1), std::max<size_t>(sz1, 1) * sizeof(double)) != hipSuccess) rc = 1;
+    if (rc) {
+        if (g_err.empty()) set_error("poms_transfer_create: allocation failed");
+        poms_transfer_destroy(t);
+        return 1;
+    }
+    *tr = t;
+    return 0;
+}
+
+int poms_transfer_destroy(poms_transfer* t) {
+    if (!t) return 0;
+    for (double* p : {t->Pm[0], t->Pm[1], t->Pm[2], t->t0, t->t1})
+        if (p) (void)hipFree(p);
+    delete t;
+    return 0;
+}
+
+int poms_restrict(poms_transfer* t, const double* fine, double* coarse, void* stream) {
+    if (!t || !fine || !coarse) { set_error("poms_restrict: null argument"); return 1; }
+    const RowGeom g = row_geom(&t->L);
+    const int64_t n0 = g.n0, n1 = g.n1, n2 = g.n2;
+    const int64_t c0 = t->nc[0], c1 = t->nc[1], c2 = t->nc[2];
+    hipStream_t st = as_stream(stream);
+    const int64_t fbase = (int64_t)g.pd0 * g.s0 + (int64_t)g.pd1 * g.s1 + g.pd2;
+    const double* src1;  // input of the axis-1 pass (dense [c0][n1][n2] or the fine vector)
+    AxisPass a1{};
+    if (t->ndim == 3) {
+        AxisPass a0{};
+        a0.nA = 1; a0.nB1 = n1; a0.nB2 = n2;
+        a0.in_base = fbase; a0.in_sb1 = g.s1; a0.in_sb2 = 1; a0.in_si = g.s0;
+        a0.out_sb1 = n2; a0.out_sb2 = 1; a0.out_si = n1 * n2;
+        a0.nI = (int)n0; a0.nJ = (int)c0; a0.goff = (int)t->g0;
+        if (transfer_pass_launch(true, t->ncm, a0, t->Pm[0], fine, t->t0, st)) return 1;
+        src1 = t->t0;
+        a1.nA = c0; a1.nB1 = 1; a1.nB2 = n2;
+        a1.in_base = 0; a1.in_sa = n1 * n2; a1.in_sb2 = 1; a1.in_si = n2;
+    } else {
+        src1 = fine;
+        a1.nA = 1; a1.nB1 = 1; a1.nB2 = n2;
+        a1.in_base = fbase; a1.in_sb2 = 1; a1.in_si = g.s1;
+    }
+    a1.out_sa = c1 * n2; a1.out_sb2 = 1; a1.out_si = n2;
+    a1.nI = (int)n1; a1.nJ = (int)c1; a1.goff = 0;
+    if (transfer_pass_launch(true, t->ncm, a1, t->Pm[1], src1, t->t1, st)) return 1;
+    AxisPass a2{};
+    a2.nA = c0 * c1; a2.nB1 = 1; a2.nB2 = 1;
+    a2.in_sa = n2; a2.in_si = 1;
+    a2.out_sa = c2; a2.out_si = 1;
+    a2.nI = (int)n2; a2.nJ = (int)c2; a2.goff = 0;
+    if (transfer_pass_launch(true, t->ncm, a2, t->Pm[2], t->t1, coarse, st)) return 1;
+    POMS_HIP_CHECK(hipGetLastError());
+    return 0;
+}
+
+int poms_prolong_add(poms_transfer* t, const double* coarse, double* fine, void* stream) {
+    if (!t || !fine || !coarse) { set_error("poms_prolong_add: null argument"); return 1; }
+    const RowGeom g = row_geom(&t->L);
+    const int64_t n0 = g.n0, n1 = g.n1, n2 = g.n2;
+    const int64_t c0 = t->nc[0], c1 = t->nc[1], c2 = t->nc[2];
+    hipStream_t st = as_stream(stream);
+    const int64_t fbase = (int64_t)g.pd0 * g.s0 + (int64_t)g.pd1 * g.s1 + g.pd2;
+    // axis 2: coarse [c0*c1][c2] -> t1 [c0*c1][n2]
+    AxisPass a2{};
+    a2.nA = c0 * c1; a2.nB1 = 1; a2.nB2 = 1;
+    a2.in_sa = c2; a2.in_si = 1; a2.nJ = (int)c2;
+    a2.out_sa = n2; a2.out_si = 1; a2.nI = (int)n2; a2.goff = 0; a2.accumulate = 0;
+    if (transfer_pass_launch(false, t->ncm, a2, t->Pm[2], coarse, t->t1, st)) return 1;
+    // axis 1: t1 [c0][c1][n2] -> t0 [c0][n1][n2] (3D) or fine (2D, accumulate)
+    AxisPass a1{};
+    a1.nA = c0; a1.nB1 = 1; a1.nB2 = n2;
+    a1.in_sa = c1 * n2; a1.in_sb2 = 1; a1.in_si = n2; a1.nJ = (int)c1;
+    a1.nI = (int)n1; a1.goff = 0;
+    if (t->ndim == 3) {
+        a1.out_sa = n1 * n2; a1.out_sb2 = 1; a1.out_si = n2; a1.accumulate = 0;
+        if (transfer_pass_launch(false, t->ncm, a1, t->Pm[1], t->t1, t->t0, st)) return 1;
+        AxisPass a0{};
+        a0.nA = 1; a0.nB1 = n1; a0.nB2 = n2;
+        a0.in_sb1 = n2; a0.in_sb2 = 1; a0.in_si = n1 * n2; a0.nJ = (int)c0;
+        a0.out_base = fbase; a0.out_sb1 = g.s1; a0.out_sb2 = 1; a0.out_si = g.s0;
+        a0.nI = (int)n0; a0.goff = (int)t->g0; a0.accumulate = 1;
+        if (transfer_pass_launch(false, t->ncm, a0, t->Pm[0], t->t0, fine, st)) return 1;
+    } else {
+        a1.out_base = fbase; a1.out_sb2 = 1; a1.out_si = g.s1; a1.accumulate = 1;
+        if (transfer_pass_launch(false, t->ncm, a1, t->Pm[1], t->t1, fine, st)) return 1;
+    }
+    POMS_HIP_CHECK(hipGetLastError());
+    return 0;
+}
+
+int poms_dense_matvec(poms_ctx* ctx, int64_t n, const double* Minv, const double* x, double* y,
+                      void* stream) {
+    if (!ctx || !Minv || !x || !y || n < 1 || n > (1 << 20)) { set_error("dense_matvec: bad argument"); return 1; }
+    dense_matvec_launch((int)n, Minv, x, y, as_stream(stream));
+    POMS_HIP_CHECK(hipGetLastError());
+    return 0;
+}
+
+}  // extern "C"

@@ -1,0 +1,93 @@
+// Knot-insertion restriction / prolongation as a sequence of 1D Kronecker
+// axis passes (R = P^T with P = P0 (x) P1 (x) P2, sources/mg_jac.py:67-70).
+//
+// restrict pass:  out[a][J][b] = sum_i P[goff+i][J] * in[a][i][b]
+// prolong  pass:  out[a][i][b] (+)= sum_J P[goff+i][J] * in[a][J][b]
+//
+// One thread per independent (a, b1, b2) line; the thread marches along the
+// contracted axis with the NCM coarse values / accumulators in registers and
+// wave-uniform (scalar) rows of P (P is stored fine-row-major, padded to NCM
+// columns with zeros).  The dominant pass (axis 0 of the fine slab) streams the
+// fine vector once: 8 B/DOF for restriction, 16 B/DOF for prolong-add.
+#include "common.hpp"
+
+namespace poms {
+
+template <int NCM>
+__global__ void __launch_bounds__(256)
+restrict_pass_kernel(const AxisPass ps, const double* __restrict__ Pm,
+                     const double* __restrict__ in, double* __restrict__ out) {
+    const int64_t tid = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    const int64_t nline = ps.nA * ps.nB1 * ps.nB2;
+    if (tid >= nline) return;
+    const int64_t b2 = tid % ps.nB2;
+    const int64_t t1 = tid / ps.nB2;
+    const int64_t b1 = t1 % ps.nB1;
+    const int64_t a = t1 / ps.nB1;
+    const double* src = in + ps.in_base + a * ps.in_sa + b1 * ps.in_sb1 + b2 * ps.in_sb2;
+    double acc[NCM];
+#pragma unroll
+    for (int j = 0; j < NCM; ++j) acc[j] = 0.0;
+    for (int i = 0; i < ps.nI; ++i) {
+        const double v = src[(int64_t)i * ps.in_si];
+        const double* prow = Pm + (int64_t)(ps.goff + i) * NCM;
+#pragma unroll
+        for (int j = 0; j < NCM; ++j) acc[j] = fma(prow[j], v, acc[j]);
+    }
+    double* dst = out + ps.out_base + a * ps.out_sa + b1 * ps.out_sb1 + b2 * ps.out_sb2;
+#pragma unroll
+    for (int j = 0; j < NCM; ++j)
+        if (j < ps.nJ) dst[(int64_t)j * ps.out_si] = acc[j];
+}
+
+template <int NCM>
+__global__ void __launch_bounds__(256)
+prolong_pass_kernel(const AxisPass ps, const double* __restrict__ Pm,
+                    const double* __restrict__ in, double* __restrict__ out) {
+    const int64_t tid = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    const int64_t nline = ps.nA * ps.nB1 * ps.nB2;
+    if (tid >= nline) return;
+    const int64_t b2 = tid % ps.nB2;
+    const int64_t t1 = tid / ps.nB2;
+    const int64_t b1 = t1 % ps.nB1;
+    const int64_t a = t1 / ps.nB1;
+    const double* src = in + ps.in_base + a * ps.in_sa + b1 * ps.in_sb1 + b2 * ps.in_sb2;
+    double cv[NCM];
+#pragma unroll
+    for (int j = 0; j < NCM; ++j) cv[j] = (j < ps.nJ) ? src[(int64_t)j * ps.in_si] : 0.0;
+    double* dst = out + ps.out_base + a * ps.out_sa + b1 * ps.out_sb1 + b2 * ps.out_sb2;
+    for (int i = 0; i < ps.nI; ++i) {
+        const double* prow = Pm + (int64_t)(ps.goff + i) * NCM;
+        double s = 0.0;
+#pragma unroll
+        for (int j = 0; j < NCM; ++j) s = fma(prow[j], cv[j], s);
+        double* o = dst + (int64_t)i * ps.out_si;
+        if (ps.accumulate) *o += s;
+        else *o = s;
+    }
+}
+
+int transfer_pass_launch(bool restrict_dir, int ncm, const AxisPass& ps, const double* Pm,
+                         const double* in, double* out, hipStream_t st) {
+    const int64_t nline = ps.nA * ps.nB1 * ps.nB2;
+    const int nb = (int)((nline + 255) / 256);
+    if (nb == 0) return 0;
+    if (ncm == 16) {
+        if (restrict_dir)
+            hipLaunchKernelGGL(restrict_pass_kernel<16>, dim3(nb), dim3(256), 0, st, ps, Pm, in, out);
+        else
+            hipLaunchKernelGGL(prolong_pass_kernel<16>, dim3(nb), dim3(256), 0, st, ps, Pm, in, out);
+        return 0;
+    }
+    if (ncm == 32) {
+        if (restrict_dir)
+            hipLaunchKernelGGL(restrict_pass_kernel<32>, dim3(nb), dim3(256), 0, st, ps, Pm, in, out);
+        else
+            hipLaunchKernelGGL(prolong_pass_kernel<32>, dim3(nb), dim3(256), 0, st, ps, Pm, in, out);
+        return 0;
+    }
+    set_error("transfer: coarse extent must be <= 32");
+    return 1;
+}
+
+}  // namespace poms

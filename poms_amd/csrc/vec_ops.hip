@@ -1,0 +1,188 @@
+// Interior-only vector kernels on the padded stencil layout (spl StencilVector
+// algebra used by sources/solvers.py) plus deterministic reductions and the
+// dense coarse-grid mat-vec.
+//
+// Layout walk: one wave64 per interior row (i0, i1); lanes stride the
+// unit-stride axis i2 (coalesced 8-B accesses); grid-stride over rows.
+// HBM-bound: 16-32 B per DOF, no reuse.
+#include "common.hpp"
+
+namespace poms {
+
+enum VecOp : int { V_AXPBY = 0, V_SCALE = 1, V_FILL = 2, V_DOT = 3, V_PCGUPD = 4 };
+
+constexpr int kMaxPartials = 4096;
+
+template <int OP>
+__global__ void __launch_bounds__(256)
+vec_rows_kernel(const RowGeom g, const double a, const double b,
+                const double* __restrict__ x, const double* __restrict__ yv,
+                double* __restrict__ z, double* __restrict__ w, const double* __restrict__ q,
+                double* __restrict__ partial) {
+    __shared__ double red[4];
+    const int lane = threadIdx.x & 63;
+    const int wv = threadIdx.x >> 6;
+    const int64_t nrows = (int64_t)g.n0 * g.n1;
+    double s = 0.0;
+    for (int64_t row = (int64_t)blockIdx.x * 4 + wv; row < nrows; row += (int64_t)gridDim.x * 4) {
+        const int i0 = (int)(row / g.n1);
+        const int i1 = (int)(row - (int64_t)i0 * g.n1);
+        const int64_t base = (int64_t)(i0 + g.pd0) * g.s0 + (int64_t)(i1 + g.pd1) * g.s1 + g.pd2;
+        for (int c = lane; c < g.n2; c += 64) {
+            const int64_t o = base + c;
+            if constexpr (OP == V_AXPBY) {
+                z[o] = a * x[o] + b * yv[o];
+            } else if constexpr (OP == V_SCALE) {
+                z[o] = a * x[o];
+            } else if constexpr (OP == V_FILL) {
+                z[o] = a;
+            } else if constexpr (OP == V_DOT) {
+                s = fma(x[o], yv[o], s);
+            } else {  // V_PCGUPD: z = x += a*p (yv = p), w = r -= a*q
+                z[o] = fma(a, yv[o], z[o]);
+                const double rn = fma(-a, q[o], w[o]);
+                w[o] = rn;
+                s = fma(rn, rn, s);
+            }
+        }
+    }
+    if constexpr (OP == V_DOT || OP == V_PCGUPD) {
+        const double t = block_sum_256(s, red);
+        if (threadIdx.x == 0) partial[blockIdx.x] = t;
+    }
+}
+
+// Deterministic single-block reduction of `count` partials.
+__global__ void __launch_bounds__(256)
+reduce_partials_kernel(const double* __restrict__ partial, int count, double* __restrict__ out) {
+    __shared__ double red[4];
+    double s = 0.0;
+    for (int i = threadIdx.x; i < count; i += 256) s += partial[i];
+    const double t = block_sum_256(s, red);
+    if (threadIdx.x == 0) out[0] = t;
+}
+
+// x = scale * b / diag(A), optional ||x||^2 partials.  diag from the 1D band
+// diagonals exactly as in kron_fused_kernel's JACOBI epilogue.
+template <bool IS3D, int FORM>
+__global__ void __launch_bounds__(256)
+diag_scale_kernel(const RowGeom g, const int P, const int g0, const double scale,
+                  const double* __restrict__ bvec, double* __restrict__ xout,
+                  const double* __restrict__ a0t, const double* __restrict__ b0t,
+                  const double* __restrict__ a1, const double* __restrict__ b1,
+                  const double* __restrict__ a2, const double* __restrict__ b2,
+                  double* __restrict__ partial) {
+    __shared__ double red[4];
+    const int W = 2 * P + 1;
+    const int lane = threadIdx.x & 63;
+    const int wv = threadIdx.x >> 6;
+    const int64_t nrows = (int64_t)g.n0 * g.n1;
+    double s = 0.0;
+    for (int64_t row = (int64_t)blockIdx.x * 4 + wv; row < nrows; row += (int64_t)gridDim.x * 4) {
+        const int i0 = (int)(row / g.n1);
+        const int i1 = (int)(row - (int64_t)i0 * g.n1);
+        const int64_t base = (int64_t)(i0 + g.pd0) * g.s0 + (int64_t)(i1 + g.pd1) * g.s1 + g.pd2;
+        const double d1a = a1[i1 * W + P];
+        const double d1b = (FORM == FORM_SUM) ? b1[i1 * W + P] : 0.0;
+        double d0a = 1.0, d0b = 0.0;
+        if constexpr (IS3D) {
+            d0a = a0t[(g0 + i0 + P) * W + P];
+            if constexpr (FORM == FORM_SUM) d0b = b0t[(g0 + i0 + P) * W + P];
+        }
+        for (int c = lane; c < g.n2; c += 64) {
+            const double d2a = a2[c * W + P];
+            double diag;
+            if constexpr (FORM == FORM_SUM) {
+                const double d2b = b2[c * W + P];
+                if constexpr (IS3D) diag = d0a * (d1a * d2a) + d0b * (d1b * d2a + d1a * d2b);
+                else diag = d1a * d2a + d1b * d2b;
+            } else {
+                diag = d0a * d1a * d2a;
+            }
+            const double v = scale * bvec[base + c] / diag;
+            xout[base + c] = v;
+            s = fma(v, v, s);
+        }
+    }
+    if (partial != nullptr) {
+        const double t = block_sum_256(s, red);
+        if (threadIdx.x == 0) partial[blockIdx.x] = t;
+    }
+}
+
+// y = M x, dense row-major n x n; one wave per row.
+__global__ void __launch_bounds__(256)
+dense_matvec_kernel(const int n, const double* __restrict__ M, const double* __restrict__ x,
+                    double* __restrict__ y) {
+    const int lane = threadIdx.x & 63;
+    const int row = blockIdx.x * 4 + (threadIdx.x >> 6);
+    if (row >= n) return;
+    const double* mr = M + (int64_t)row * n;
+    double s = 0.0;
+    for (int j = lane; j < n; j += 64) s = fma(mr[j], x[j], s);
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) s += __shfl_xor(s, off, 64);
+    if (lane == 0) y[row] = s;
+}
+
+static int row_blocks(const RowGeom& g) {
+    const int64_t nrows = (int64_t)g.n0 * g.n1;
+    int64_t nb = (nrows + 3) / 4;
+    if (nb > kMaxPartials) nb = kMaxPartials;
+    if (nb < 1) nb = 1;
+    return (int)nb;
+}
+
+int vec_launch(int op, const RowGeom& g, double a, double b, const double* x, const double* y,
+               double* z, double* w, const double* q, double* partial, hipStream_t st,
+               int* nblk_out) {
+    const int nb = row_blocks(g);
+    if (nblk_out) *nblk_out = nb;
+    switch (op) {
+#define POMS_VL(OPV)                                                                        \
+    case OPV:                                                                               \
+        hipLaunchKernelGGL(vec_rows_kernel<OPV>, dim3(nb), dim3(256), 0, st, g, a, b, x, y, z, \
+                           w, q, partial);                                                  \
+        return 0;
+        POMS_VL(V_AXPBY)
+        POMS_VL(V_SCALE)
+        POMS_VL(V_FILL)
+        POMS_VL(V_DOT)
+        POMS_VL(V_PCGUPD)
+#undef POMS_VL
+    }
+    set_error("unknown vector op");
+    return 1;
+}
+
+int reduce_launch(const double* partial, int count, double* out, hipStream_t st) {
+    hipLaunchKernelGGL(reduce_partials_kernel, dim3(1), dim3(256), 0, st, partial, count, out);
+    return 0;
+}
+
+int diag_scale_launch(bool is3d, int form, const RowGeom& g, int P, int g0, double scale,
+                      const double* b, double* x, const double* a0t, const double* b0t,
+                      const double* a1, const double* b1, const double* a2, const double* b2,
+                      double* partial, hipStream_t st, int* nblk_out) {
+    const int nb = row_blocks(g);
+    if (nblk_out) *nblk_out = nb;
+#define POMS_DS(I3, F)                                                                          \
+    hipLaunchKernelGGL((diag_scale_kernel<I3, F>), dim3(nb), dim3(256), 0, st, g, P, g0, scale, b, \
+                       x, a0t, b0t, a1, b1, a2, b2, partial)
+    if (is3d) {
+        if (form == FORM_SUM) POMS_DS(true, FORM_SUM); else POMS_DS(true, FORM_SINGLE);
+    } else {
+        if (form == FORM_SUM) POMS_DS(false, FORM_SUM); else POMS_DS(false, FORM_SINGLE);
+    }
+#undef POMS_DS
+    return 0;
+}
+
+int dense_matvec_launch(int n, const double* M, const double* x, double* y, hipStream_t st) {
+    hipLaunchKernelGGL(dense_matvec_kernel, dim3((n + 3) / 4), dim3(256), 0, st, n, M, x, y);
+    return 0;
+}
+
+int max_partials() { return kMaxPartials; }
+
+}  // namespace poms

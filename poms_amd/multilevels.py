@@ -1,0 +1,91 @@
+"""Knot-insertion multilevel set-up and the device transfer operators.
+
+* :func:`knots_to_insert` -- interior knots of the fine knot vector that are
+  absent from the coarse one, same loop and float comparisons as
+  `sources/multilevels.py:7-33`.
+* :class:`KronTransfer` -- ``R = (P0⊗P1⊗P2)^T`` and ``P = P0⊗P1⊗P2`` applied
+  by sum-factorised device passes (``poms_restrict`` / ``poms_prolong_add``),
+  replacing the materialised ``scipy.sparse.kron`` products of
+  `sources/mg_jac.py:67-70,94,102`.
+"""
+from __future__ import annotations
+
+import ctypes as C
+from typing import Sequence
+
+import numpy as np
+import torch
+
+from . import _lib
+from . import runtime as rt
+from .stencil import StencilVector, StencilVectorSpace, F64
+
+
+def knots_to_insert(Tf, nf, pf, Tc, nc, pc):
+    """Knots of ``Tf`` (interior) not present in ``Tc`` (`sources/multilevels.py:7-33`).
+
+    The reference scans ``Tc[pc+1], Tc[pc+2], ...`` until the first knot larger
+    than ``t`` or past index ``nc`` and inserts ``t`` when no exact match was
+    seen; on a sorted knot vector that is exact-equality membership in
+    ``Tc[pc+1 .. nc]``.  Multiplicities are ignored exactly as there.
+    """
+    Tf = np.asarray(Tf, dtype=np.float64)
+    Tc = np.asarray(Tc, dtype=np.float64)
+    cand = Tf[pf + 1:nf]
+    present = np.isin(cand, Tc[pc + 1:nc + 1])
+    return np.ascontiguousarray(cand[~present])
+
+
+class KronTransfer:
+    """Restriction / prolongation between a fine :class:`StencilVectorSpace`
+    (possibly a slab) and a dense, replicated coarse vector of ``prod(nc)`` doubles."""
+
+    def __init__(self, V: StencilVectorSpace, P: Sequence[np.ndarray]):
+        nd = V.ndim
+        if len(P) != nd:
+            raise ValueError("need one 1D prolongation factor per axis")
+        self.space = V
+        self.P = [np.ascontiguousarray(p, dtype=np.float64) for p in P]
+        for d, p in enumerate(self.P):
+            if p.shape[0] != V.npts[d]:
+                raise ValueError(f"axis {d}: P has {p.shape[0]} rows, space has {V.npts[d]} points")
+        self.nc = tuple(p.shape[1] for p in self.P)
+        lead = 3 - nd
+        nf3 = (1,) * lead + tuple(V.npts)
+        nc3 = (1,) * lead + self.nc
+        ones = np.ones((1, 1))
+        P3 = [ones] * lead + self.P
+        self._keep = P3
+        nf_arr = (C.c_int64 * 3)(*nf3)
+        nc_arr = (C.c_int64 * 3)(*nc3)
+        parr = (C.c_void_p * 3)(*[p.ctypes.data_as(C.c_void_p) for p in P3])
+        self._h = C.c_void_p()
+        _lib.call("poms_transfer_create", V.ctx, 3 if nd == 3 else 2, C.byref(V.layout),
+                  V.starts[0] if nd == 3 else 0, nf_arr, nc_arr, parr, C.byref(self._h))
+        self.ncoarse = int(np.prod(self.nc))
+
+    def __del__(self):
+        h = getattr(self, "_h", None)
+        if h is not None and h.value:
+            try:
+                _lib.lib.poms_transfer_destroy(h)
+            except Exception:
+                pass
+            self._h = None
+
+    def coarse_empty(self) -> torch.Tensor:
+        return torch.empty(self.ncoarse, dtype=F64, device=f"cuda:{self.space.device}")
+
+    def restrict(self, fine: StencilVector, out: torch.Tensor | None = None, allreduce: bool = True) -> torch.Tensor:
+        """``rc = R rf`` (+ sum over slabs, `sources/mg_jac.py:94-95`)."""
+        out = self.coarse_empty() if out is None else out
+        _lib.call("poms_restrict", self._h, rt.ptr(fine._data), rt.ptr(out), rt.stream_handle())
+        if allreduce and self.space.is_distributed:
+            rt.Comm.from_env(self.space.dist.group).allreduce_sum_(out)
+        return out
+
+    def prolong_add(self, coarse: torch.Tensor, fine: StencilVector) -> StencilVector:
+        """``fine += P xc`` on the owned slab (`sources/mg_jac.py:102-112`)."""
+        _lib.call("poms_prolong_add", self._h, rt.ptr(coarse), rt.ptr(fine._data), rt.stream_handle())
+        fine._mark_written()
+        return fine

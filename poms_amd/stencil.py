@@ -1,0 +1,628 @@
+"""Device-backed, spl-compatible stencil types.
+
+The reference solvers (`sources/solvers.py`) duck-type spl's
+``StencilVectorSpace`` / ``StencilVector`` / ``StencilMatrix``
+(SURVEY §8b): ``A.shape``, ``A.dot(x)``, ``A[i1, i2, 0, 0]``;
+``v.space.starts/ends/pads/npts``, ``v[:, :] = c``, ``v[i1, i2]``,
+``v.copy()``, ``a*v``, ``v + w``, ``v - w``, ``v.dot(w)``,
+``v.update_ghost_regions()``, ``v.toarray()``.  These classes provide that
+surface over HBM-resident padded arrays (the spl ``_data`` layout,
+`slides/content.tex:256-264`), and dispatch whole-vector work to
+``libpoms_hip.so``.  Per-element ``__getitem__``/``__setitem__`` exist for API
+parity only (each is a device round trip).
+
+``KronOperator`` is the banded Kronecker(-sum) operator: the V-cycle's fine
+matrix (the assembled ``-Δu + u`` of `sources/matrix_assembler.py:84-179`,
+applied by spl ``StencilMatrix.dot``) and the ``(A, B)`` pair of
+``kron_dot_v2`` (`sources/kron_product.py:56-89`).
+"""
+from __future__ import annotations
+
+import ctypes as C
+import math
+from typing import Sequence
+
+import numpy as np
+import torch
+
+from . import _lib
+from . import runtime as rt
+from .dist import SlabDistribution
+
+F64 = torch.float64
+
+
+class StencilVectorSpace:
+    """Padded, possibly slab-distributed, 1D/2D/3D vector space on one GPU.
+
+    ``npts``: global number of coefficients per axis; ``pads``: ghost width per
+    axis (the spline degree).  Non-periodic only -- every driver of the
+    reference is non-periodic (`sources/mg_jac.py`).  With
+    ``dist`` the slowest axis is split into slabs (3D only).
+    """
+
+    def __init__(self, npts: Sequence[int], pads: Sequence[int], periods=None, *,
+                 dist: SlabDistribution | None = None, device=None):
+        npts, pads = tuple(int(v) for v in npts), tuple(int(v) for v in pads)
+        if not 1 <= len(npts) <= 3 or len(pads) != len(npts):
+            raise ValueError("npts/pads must have 1..3 equal-length entries")
+        if periods is not None and any(periods):
+            raise NotImplementedError("periodic spaces are not supported (reference drivers are non-periodic)")
+        if any(n < 1 for n in npts) or any(p < 0 for p in pads):
+            raise ValueError("bad npts/pads")
+        if dist is not None:
+            if len(npts) != 3:
+                raise NotImplementedError("slab distribution is implemented for 3D spaces")
+            if dist.n0_global != npts[0]:
+                raise ValueError("distribution does not match npts[0]")
+        self.npts, self.pads, self.ndim = npts, pads, len(npts)
+        self.periods = (False,) * self.ndim
+        self.dist = dist
+        s0, e0 = (dist.start, dist.end - 1) if dist is not None else (0, npts[0] - 1)
+        self.starts = (s0,) + (0,) * (self.ndim - 1)
+        self.ends = (e0,) + tuple(n - 1 for n in npts[1:])
+        self.local_npts = tuple(e - s + 1 for s, e in zip(self.starts, self.ends))
+        lead = 3 - self.ndim
+        self.n3 = (1,) * lead + self.local_npts
+        self.p3 = (0,) * lead + self.pads
+        self.layout = _lib.Layout.make(self.n3, self.p3)
+        self.padded_shape = tuple(n + 2 * p for n, p in zip(self.local_npts, self.pads))
+        self.dimension = int(np.prod(npts))
+        self.device = rt.device_index(device)
+        self.ctx = rt.ctx(self.device)
+        self._scal = None
+
+    # ------------------------------------------------------------------
+    @property
+    def is_distributed(self) -> bool:
+        return self.dist is not None and self.dist.world > 1
+
+    def interior(self, data: torch.Tensor) -> torch.Tensor:
+        """View of the owned (interior) entries of a padded array."""
+        return data[tuple(slice(p, p + n) for p, n in zip(self.pads, self.local_npts))]
+
+    def zeros(self) -> "StencilVector":
+        return StencilVector(self)
+
+    def empty(self) -> "StencilVector":
+        """Vector with unspecified interior and zero ghost cells (no full memset)."""
+        t = torch.empty(self.padded_shape, dtype=F64, device=f"cuda:{self.device}")
+        for ax, p in enumerate(self.pads):
+            if p:
+                idx = [slice(None)] * self.ndim
+                idx[ax] = slice(0, p)
+                t[tuple(idx)] = 0.0
+                idx[ax] = slice(t.shape[ax] - p, t.shape[ax])
+                t[tuple(idx)] = 0.0
+        return StencilVector(self, _data=t)
+
+    def scalar_buffer(self) -> torch.Tensor:
+        if self._scal is None:
+            self._scal = torch.zeros(8, dtype=F64, device=f"cuda:{self.device}")
+        return self._scal
+
+    def global_dot(self, local: float) -> float:
+        if self.is_distributed:
+            comm = rt.Comm.from_env(self.dist.group)
+            return comm.allreduce_scalar(local)
+        return local
+
+    def __repr__(self):
+        return f"StencilVectorSpace(npts={self.npts}, pads={self.pads}, starts={self.starts}, ends={self.ends})"
+
+
+def _stream():
+    return rt.stream_handle()
+
+
+class StencilVector:
+    """Vector of a :class:`StencilVectorSpace`, stored padded in HBM."""
+
+    __array_priority__ = 100
+
+    def __init__(self, V: StencilVectorSpace, *, _data: torch.Tensor | None = None):
+        self._space = V
+        if _data is None:
+            _data = torch.zeros(V.padded_shape, dtype=F64, device=f"cuda:{V.device}")
+        if tuple(_data.shape) != V.padded_shape or _data.dtype != F64 or not _data.is_contiguous():
+            raise ValueError("data does not match the space layout")
+        self._data = _data
+        self._ghost_valid = True
+
+    # -- spl surface ----------------------------------------------------
+    @property
+    def space(self) -> StencilVectorSpace:
+        return self._space
+
+    @property
+    def shape(self):
+        return (self._space.dimension,)
+
+    @property
+    def starts(self):
+        return self._space.starts
+
+    @property
+    def ends(self):
+        return self._space.ends
+
+    @property
+    def pads(self):
+        return self._space.pads
+
+    def _mark_written(self):
+        self._ghost_valid = not self._space.is_distributed
+
+    def copy(self) -> "StencilVector":
+        out = StencilVector(self._space, _data=self._data.clone())
+        out._ghost_valid = self._ghost_valid
+        return out
+
+    def assign(self, other: "StencilVector") -> "StencilVector":
+        """self <- other (interior), no allocation."""
+        _lib.call("poms_vec_scale", self._space.ctx, C.byref(self._space.layout), 1.0,
+                  rt.ptr(other._data), rt.ptr(self._data), _stream())
+        self._mark_written()
+        return self
+
+    def axpby_(self, a: float, x: "StencilVector", b: float) -> "StencilVector":
+        """self <- a*x + b*self (interior)."""
+        _lib.call("poms_vec_axpby", self._space.ctx, C.byref(self._space.layout), float(a),
+                  rt.ptr(x._data), float(b), rt.ptr(self._data), rt.ptr(self._data), _stream())
+        self._mark_written()
+        return self
+
+    def _lin(self, a: float, other, b: float) -> "StencilVector":
+        out = self._space.empty()
+        if other is None:
+            _lib.call("poms_vec_scale", self._space.ctx, C.byref(self._space.layout), float(a),
+                      rt.ptr(self._data), rt.ptr(out._data), _stream())
+        else:
+            if not isinstance(other, StencilVector) or other._space is not self._space:
+                raise TypeError("operands must belong to the same StencilVectorSpace")
+            _lib.call("poms_vec_axpby", self._space.ctx, C.byref(self._space.layout), float(a),
+                      rt.ptr(self._data), float(b), rt.ptr(other._data), rt.ptr(out._data), _stream())
+        out._mark_written()
+        return out
+
+    def __add__(self, other):
+        return self._lin(1.0, other, 1.0)
+
+    def __sub__(self, other):
+        return self._lin(1.0, other, -1.0)
+
+    def __mul__(self, a):
+        if not isinstance(a, (int, float, np.floating, np.integer)):
+            return NotImplemented
+        return self._lin(float(a), None, 0.0)
+
+    __rmul__ = __mul__
+
+    def __neg__(self):
+        return self._lin(-1.0, None, 0.0)
+
+    def __iadd__(self, other):
+        _lib.call("poms_vec_axpby", self._space.ctx, C.byref(self._space.layout), 1.0,
+                  rt.ptr(self._data), 1.0, rt.ptr(other._data), rt.ptr(self._data), _stream())
+        self._mark_written()
+        return self
+
+    def __isub__(self, other):
+        _lib.call("poms_vec_axpby", self._space.ctx, C.byref(self._space.layout), 1.0,
+                  rt.ptr(self._data), -1.0, rt.ptr(other._data), rt.ptr(self._data), _stream())
+        self._mark_written()
+        return self
+
+    def __imul__(self, a):
+        _lib.call("poms_vec_scale", self._space.ctx, C.byref(self._space.layout), float(a),
+                  rt.ptr(self._data), rt.ptr(self._data), _stream())
+        self._mark_written()
+        return self
+
+    def dot(self, other: "StencilVector") -> float:
+        """Global inner product (RCCL all-reduce across slabs), as spl ``StencilVector.dot``."""
+        V = self._space
+        buf = V.scalar_buffer()
+        _lib.call("poms_vec_dot", V.ctx, C.byref(V.layout), rt.ptr(self._data), rt.ptr(other._data),
+                  rt.ptr(buf), _stream())
+        return V.global_dot(float(buf[0].item()))
+
+    def update_ghost_regions(self, direction=None) -> None:
+        V = self._space
+        if V.is_distributed and (direction is None or direction == 0):
+            V.dist.exchange(self._data, width=V.pads[0], pad=V.pads[0])
+            self._ghost_valid = True
+
+    def toarray(self) -> np.ndarray:
+        """Global-size flat array holding this rank's entries (zeros elsewhere)."""
+        V = self._space
+        out = np.zeros(V.npts)
+        loc = V.interior(self._data).cpu().numpy()
+        out[tuple(slice(s, e + 1) for s, e in zip(V.starts, V.ends))] = loc
+        return out.reshape(-1)
+
+    def to_local_numpy(self) -> np.ndarray:
+        return self._space.interior(self._data).cpu().numpy()
+
+    def from_numpy(self, arr: np.ndarray) -> "StencilVector":
+        """Set the owned entries from a global-shaped (or local-shaped) array."""
+        V = self._space
+        arr = np.asarray(arr, dtype=np.float64)
+        if arr.shape == V.npts:
+            arr = arr[tuple(slice(s, e + 1) for s, e in zip(V.starts, V.ends))]
+        if arr.shape != V.local_npts:
+            raise ValueError(f"array shape {arr.shape} matches neither {V.npts} nor {V.local_npts}")
+        V.interior(self._data).copy_(torch.from_numpy(np.ascontiguousarray(arr)))
+        self._mark_written()
+        return self
+
+    # -- element access with spl's global indices -------------------------------
+    def _index(self, key):
+        V = self._space
+        if not isinstance(key, tuple):
+            key = (key,)
+        if len(key) != V.ndim:
+            raise IndexError("need one index per axis")
+        out = []
+        for k, s, e, p in zip(key, V.starts, V.ends, V.pads):
+            if isinstance(k, slice):
+                if k == slice(None):
+                    out.append(slice(p, p + e - s + 1))
+                else:
+                    a = s if k.start is None else k.start
+                    b = e + 1 if k.stop is None else k.stop
+                    out.append(slice(a - s + p, b - s + p, k.step))
+            else:
+                out.append(int(k) - s + p)
+        return tuple(out)
+
+    def __getitem__(self, key):
+        v = self._data[self._index(key)]
+        return float(v.item()) if v.dim() == 0 else v.cpu().numpy()
+
+    def __setitem__(self, key, value):
+        self._data[self._index(key)] = torch.as_tensor(value, dtype=F64)
+        self._mark_written()
+
+    def __repr__(self):
+        return f"StencilVector({self._space!r})"
+
+
+class StencilMatrix1D:
+    """Host 1D banded ``StencilMatrix`` (spl layout ``M[i, k]``, ``k in [-p, p]``).
+
+    Used to hand band factors to :func:`poms_amd.kron_product.kron_dot_v2`
+    (as `sources/tests/test_kron_dot.py:21-29` builds them).
+    """
+
+    def __init__(self, n: int, p: int, band: np.ndarray | None = None):
+        self.n, self.p = int(n), int(p)
+        self.band = np.zeros((self.n, 2 * self.p + 1)) if band is None else np.array(band, dtype=np.float64)
+        if self.band.shape != (self.n, 2 * self.p + 1):
+            raise ValueError("band shape mismatch")
+
+    starts = property(lambda self: (0,))
+    ends = property(lambda self: (self.n - 1,))
+    pads = property(lambda self: (self.p,))
+    shape = property(lambda self: (self.n, self.n))
+
+    def __getitem__(self, key):
+        i, k = key
+        return self.band[i, k + self.p]
+
+    def __setitem__(self, key, value):
+        i, k = key
+        if isinstance(i, slice):
+            self.band[i, k + self.p] = value
+        else:
+            self.band[i, k + self.p] = value
+
+    def remove_spurious_entries(self):
+        for i in range(self.n):
+            for k in range(-self.p, self.p + 1):
+                if not 0 <= i + k < self.n:
+                    self.band[i, k + self.p] = 0.0
+
+    def toarray(self) -> np.ndarray:
+        from .splines import band_to_dense
+        return band_to_dense(self.band)
+
+    def tocsr(self):
+        import scipy.sparse as sp
+        return sp.csr_matrix(self.toarray())
+
+
+def _band_of(F) -> np.ndarray:
+    if isinstance(F, StencilMatrix1D):
+        return F.band
+    b = np.asarray(F, dtype=np.float64)
+    if b.ndim != 2 or b.shape[1] % 2 != 1:
+        raise ValueError("band factor must be (n, 2p+1)")
+    return b
+
+
+def _widen(band: np.ndarray, pmax: int) -> np.ndarray:
+    n, w = band.shape
+    p = (w - 1) // 2
+    out = np.zeros((n, 2 * pmax + 1))
+    out[:, pmax - p:pmax + p + 1] = band
+    return np.ascontiguousarray(out)
+
+
+def _unit_band(pmax: int, value: float = 1.0) -> np.ndarray:
+    b = np.zeros((1, 2 * pmax + 1))
+    b[0, pmax] = value
+    return b
+
+
+class KronOperator:
+    """Banded Kronecker(-sum) operator on a :class:`StencilVectorSpace`.
+
+    ``form='sum'``:  A = c M⊗M⊗M + K⊗M⊗M + M⊗K⊗M + M⊗M⊗K  (``-Δu + c u`` with
+    natural BCs; 2D/1D analogues).  ``form='single'``: A = F0⊗F1⊗F2.
+    """
+
+    def __init__(self, V: StencilVectorSpace, form: str, bands: dict, pmax: int):
+        self.space, self.form = V, form
+        self.pmax = int(pmax)
+        self.bands = bands  # host copies (global rows) by role name
+        self._h = C.c_void_p()
+        nd = V.ndim
+        W = 2 * self.pmax + 1
+        keep = []
+
+        def arr(b):
+            a = np.ascontiguousarray(b, dtype=np.float64)
+            assert a.shape[1] == W
+            keep.append(a)
+            return a.ctypes.data_as(C.c_void_p)
+
+        f = [None] * 6
+        if form == "sum":
+            if nd == 3:
+                f[0], f[1] = arr(bands["A0"]), arr(bands["M0"])
+            f[2], f[3], f[4], f[5] = arr(bands["A1"]), arr(bands["B1"]), arr(bands["M2"]), arr(bands["K2"])
+            cform = _lib.FORM_SUM
+        else:
+            if nd == 3:
+                f[0] = arr(bands["F0"])
+            f[2], f[4] = arr(bands["F1"]), arr(bands["F2"])
+            cform = _lib.FORM_SINGLE
+        farr = (C.c_void_p * 6)(*f)
+        g0 = V.starts[0] if nd == 3 else 0
+        n0g = V.npts[0] if nd == 3 else 1
+        _lib.call("poms_op_create", V.ctx, 3 if nd == 3 else 2, C.byref(V.layout), cform, self.pmax,
+                  farr, g0, n0g, C.byref(self._h))
+        self.timer = None  # list -> (kind, start_event, end_event) per kernel launch
+
+    # -- constructors ------------------------------------------------------------
+    @classmethod
+    def laplace(cls, V: StencilVectorSpace, M: Sequence, K: Sequence, mass_coef: float = 1.0):
+        """-Δu + c u in Kronecker-sum form from per-axis 1D (mass, stiffness) bands."""
+        nd = V.ndim
+        M = [_band_of(m) for m in M]
+        K = [_band_of(k) for k in K]
+        if len(M) != nd or len(K) != nd:
+            raise ValueError("need one (M, K) pair per axis")
+        for d in range(nd):
+            if M[d].shape[0] != V.npts[d] or K[d].shape != M[d].shape:
+                raise ValueError(f"axis {d}: factor rows do not match npts")
+        pmax = max(max((m.shape[1] - 1) // 2 for m in M), max(V.pads), 1)
+        Mw = [_widen(m, pmax) for m in M]
+        Kw = [_widen(k, pmax) for k in K]
+        c = float(mass_coef)
+        if nd == 3:
+            bands = {"A0": c * Mw[0] + Kw[0], "M0": Mw[0], "A1": Mw[1], "B1": Kw[1], "M2": Mw[2], "K2": Kw[2]}
+        elif nd == 2:
+            bands = {"A1": c * Mw[0] + Kw[0], "B1": Mw[0], "M2": Mw[1], "K2": Kw[1]}
+        else:
+            bands = {"A1": _unit_band(pmax, c), "B1": _unit_band(pmax, 1.0), "M2": Mw[0], "K2": Kw[0]}
+        op = cls(V, "sum", bands, pmax)
+        op.M, op.K, op.mass_coef = M, K, c
+        return op
+
+    @classmethod
+    def product(cls, V: StencilVectorSpace, F: Sequence):
+        """Single Kronecker product F0⊗F1(⊗F2) (``kron_dot``)."""
+        nd = V.ndim
+        F = [_band_of(f) for f in F]
+        if len(F) != nd:
+            raise ValueError("need one factor per axis")
+        for d in range(nd):
+            if F[d].shape[0] != V.npts[d]:
+                raise ValueError(f"axis {d}: factor rows do not match npts")
+        pmax = max(max((f.shape[1] - 1) // 2 for f in F), max(V.pads), 1)
+        Fw = [_widen(f, pmax) for f in F]
+        if nd == 3:
+            bands = {"F0": Fw[0], "F1": Fw[1], "F2": Fw[2]}
+        elif nd == 2:
+            bands = {"F1": Fw[0], "F2": Fw[1]}
+        else:
+            bands = {"F1": _unit_band(pmax), "F2": Fw[0]}
+        op = cls(V, "single", bands, pmax)
+        op.F = F
+        return op
+
+    def __del__(self):
+        h = getattr(self, "_h", None)
+        if h is not None and h.value:
+            try:
+                _lib.lib.poms_op_destroy(h)
+            except Exception:
+                pass
+            self._h = None
+
+    # -- spl surface -------------------------------------------------------------
+    @property
+    def shape(self):
+        return (self.space.dimension, self.space.dimension)
+
+    def set_chunk(self, chunk: int) -> None:
+        _lib.call("poms_op_set_chunk", self._h, int(chunk))
+
+    def _check(self, *vs):
+        for v in vs:
+            if not isinstance(v, StencilVector) or v.space is not self.space:
+                raise TypeError("vector does not belong to this operator's space")
+
+    def _launch(self, fn, x: StencilVector, *args, want_norm=False, norm_buf=None, kind="apply"):
+        """Run one kernel over all local planes; overlap the RCCL ghost exchange
+        with the interior planes when x's ghosts are stale."""
+        V = self.space
+        n0 = V.local_npts[0] if V.ndim == 3 else 1
+        st = _stream()
+        ranges = [(0, n0)]
+        handle = None
+        if V.is_distributed and not x._ghost_valid:
+            p0 = V.pads[0]
+            handle = V.dist.start_exchange(x._data, width=p0, pad=p0)
+            if handle is not None and n0 > 2 * self.pmax:
+                ranges = [(self.pmax, n0 - self.pmax), (0, self.pmax), (n0 - self.pmax, n0)]
+            else:
+                V.dist.finish_exchange(handle)
+                handle = None
+        total = 0
+        for idx, (zb, ze) in enumerate(ranges):
+            if idx == 1 and handle is not None:
+                V.dist.finish_exchange(handle)
+                handle = None
+            if self.timer is not None:
+                e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                e0.record()
+                fn(*args, zb, ze, st)
+                e1.record()
+                self.timer.append((kind, e0, e1))
+            else:
+                fn(*args, zb, ze, st)
+            if want_norm:
+                cnt = C.c_int64()
+                _lib.call("poms_op_last_partials", self._h, C.byref(cnt))
+                _lib.call("poms_reduce_partials", V.ctx, cnt.value, rt.ptr(norm_buf[idx:idx + 1]), st)
+                total += 1
+        if handle is not None:
+            V.dist.finish_exchange(handle)
+        x._ghost_valid = True
+        return total
+
+    def dot(self, x: StencilVector, out: StencilVector | None = None) -> StencilVector:
+        """y = A x (spl ``StencilMatrix.dot``)."""
+        self._check(x)
+        y = self.space.empty() if out is None else out
+        self._check(y)
+        if y is x:
+            raise ValueError("out must not alias x")
+
+        def fn(zb, ze, st):
+            _lib.call("poms_op_apply", self._h, rt.ptr(x._data), rt.ptr(y._data), zb, ze, st)
+
+        self._launch(fn, x)
+        y._mark_written()
+        return y
+
+    def residual(self, b: StencilVector, x: StencilVector, out: StencilVector | None = None) -> StencilVector:
+        """r = b - A x, fused (`sources/solvers.py:85`, `sources/mg_jac.py:93`)."""
+        self._check(b, x)
+        r = self.space.empty() if out is None else out
+        if r is x:
+            raise ValueError("out must not alias x")
+
+        def fn(zb, ze, st):
+            _lib.call("poms_op_residual", self._h, rt.ptr(b._data), rt.ptr(x._data), rt.ptr(r._data), zb, ze, st)
+
+        self._launch(fn, x, kind="residual")
+        r._mark_written()
+        return r
+
+    def jacobi_sweep(self, b: StencilVector, x_in: StencilVector, x_out: StencilVector,
+                     omega: float, want_norm: bool = False):
+        """x_out = x_in + omega (b - A x_in)/diag(A); returns global ||dr||^2 or None."""
+        self._check(b, x_in, x_out)
+        if x_in is x_out:
+            raise ValueError("x_out must not alias x_in")
+        V = self.space
+        nb = V.scalar_buffer()
+
+        def fn(zb, ze, st):
+            _lib.call("poms_op_jacobi_sweep", self._h, float(omega), rt.ptr(b._data), rt.ptr(x_in._data),
+                      rt.ptr(x_out._data), zb, ze, int(want_norm), st)
+
+        n = self._launch(fn, x_in, want_norm=want_norm, norm_buf=nb, kind="jacobi")
+        x_out._mark_written()
+        if not want_norm:
+            return None
+        return V.global_dot(float(nb[:n].sum().item()))
+
+    def diag_scale(self, b: StencilVector, out: StencilVector, scale: float = 1.0, want_norm: bool = False):
+        """out = scale * b / diag(A); returns global ||out||^2 or None."""
+        self._check(b, out)
+        V = self.space
+        st = _stream()
+        _lib.call("poms_op_diag_scale", self._h, float(scale), rt.ptr(b._data), rt.ptr(out._data),
+                  int(want_norm), st)
+        out._mark_written()
+        if not want_norm:
+            return None
+        cnt = C.c_int64()
+        _lib.call("poms_op_last_partials", self._h, C.byref(cnt))
+        nb = V.scalar_buffer()
+        _lib.call("poms_reduce_partials", V.ctx, cnt.value, rt.ptr(nb), st)
+        return V.global_dot(float(nb[0].item()))
+
+    # -- host-side views of the operator (set-up / API parity) --------------------
+    def diagonal_axes(self):
+        """Per-axis 1D diagonals of the global factors, by role name."""
+        P = self.pmax
+        return {k: v[:, P].copy() for k, v in self.bands.items()}
+
+    def __getitem__(self, key):
+        """Stencil entry ``A[i1, i2(, i3), k1, k2(, k3)]`` (global indices, offsets in [-p, p])."""
+        nd = self.space.ndim
+        if not isinstance(key, tuple) or len(key) != 2 * nd:
+            raise IndexError("expected (i..., k...) with one index and one offset per axis")
+        idx, off = key[:nd], key[nd:]
+        P = self.pmax
+
+        def ent(name, axis_rows_key, i, k):
+            b = self.bands[name]
+            if not 0 <= P + k < b.shape[1]:
+                return 0.0
+            return b[0 if b.shape[0] == 1 else i, P + k]
+
+        if self.form == "sum":
+            if nd == 3:
+                return (ent("A0", 0, idx[0], off[0]) * ent("A1", 1, idx[1], off[1]) * ent("M2", 2, idx[2], off[2])
+                        + ent("M0", 0, idx[0], off[0]) * (ent("B1", 1, idx[1], off[1]) * ent("M2", 2, idx[2], off[2])
+                                                          + ent("A1", 1, idx[1], off[1]) * ent("K2", 2, idx[2], off[2])))
+            if nd == 2:
+                return (ent("A1", 1, idx[0], off[0]) * ent("M2", 2, idx[1], off[1])
+                        + ent("B1", 1, idx[0], off[0]) * ent("K2", 2, idx[1], off[1]))
+            return ent("A1", 1, 0, 0) * ent("M2", 2, idx[0], off[0]) + ent("B1", 1, 0, 0) * ent("K2", 2, idx[0], off[0])
+        if nd == 3:
+            return ent("F0", 0, idx[0], off[0]) * ent("F1", 1, idx[1], off[1]) * ent("F2", 2, idx[2], off[2])
+        if nd == 2:
+            return ent("F1", 1, idx[0], off[0]) * ent("F2", 2, idx[1], off[1])
+        return ent("F2", 2, idx[0], off[0])
+
+    def tosparse(self):
+        """Global sparse matrix (small sizes; tests and coarse-grid set-up)."""
+        import scipy.sparse as sp
+        from .splines import band_to_dense
+        D = {k: sp.csr_matrix(band_to_dense(v)) if v.shape[0] > 1 else sp.csr_matrix(v[:, self.pmax:self.pmax + 1])
+             for k, v in self.bands.items()}
+        nd = self.space.ndim
+        kr = lambda *ms: _kron_all(ms)
+        if self.form == "sum":
+            if nd == 3:
+                return kr(D["A0"], D["A1"], D["M2"]) + kr(D["M0"], D["B1"], D["M2"]) + kr(D["M0"], D["A1"], D["K2"])
+            return kr(D["A1"], D["M2"]) + kr(D["B1"], D["K2"])
+        if nd == 3:
+            return kr(D["F0"], D["F1"], D["F2"])
+        return kr(D["F1"], D["F2"])
+
+
+def _kron_all(ms):
+    import scipy.sparse as sp
+    out = ms[0]
+    for m in ms[1:]:
+        out = sp.kron(out, m, format="csr")
+    return out.tocsr()

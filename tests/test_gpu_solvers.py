@@ -1,0 +1,114 @@
+"""GPU parity of pcg / damped_jacobi / jacobi / two-level V-cycle vs the oracle.
+
+Tolerance after m PCG iterations or a V-cycle: <= 1e-9 normwise relative AND
+identical ``niter``; fixed-count comparisons use ``tol=0``.
+"""
+import numpy as np
+import pytest
+
+from oracle import poms_oracle as orc
+from poms_amd.splines import assemble_1d, uniform_knots
+
+pytestmark = pytest.mark.gpu
+
+
+def rel(a, b):
+    return float(np.linalg.norm((a - b).ravel()) / max(np.linalg.norm(b.ravel()), 1e-300))
+
+
+def _problem(ndim, N, p):
+    from poms_amd.stencil import KronOperator, StencilVectorSpace
+    M, K = assemble_1d(uniform_knots(p, N), p)
+    n = N + p
+    V = StencilVectorSpace([n] * ndim, [p] * ndim)
+    A = KronOperator.laplace(V, [M] * ndim, [K] * ndim)
+    Ms, Ks = [M] * ndim, [K] * ndim
+    Acsr = orc.kron_sum_csr(Ms, Ks)
+    D = orc.kron_sum_diag(Ms, Ks).reshape(-1)
+    return V, A, Acsr, D, n
+
+
+@pytest.mark.parametrize("ndim,N,p", [(2, 16, 1), (2, 12, 3), (3, 8, 2), (3, 10, 3)])
+@pytest.mark.parametrize("maxiter", [1, 4, 10])
+def test_damped_jacobi(gpu, ndim, N, p, maxiter):
+    from poms_amd.solvers import damped_jacobi
+    V, A, Acsr, D, n = _problem(ndim, N, p)
+    x0 = np.fromfunction(lambda *i: sum(i) + 1.0, (n,) * ndim)
+    b = (Acsr @ x0.reshape(-1)).reshape(x0.shape)
+    bv = V.zeros().from_numpy(b)
+    for tol in (0.0, 1e-6):
+        x = damped_jacobi(A, bv, tol=tol, maxiter=maxiter).to_local_numpy()
+        xr = orc.damped_jacobi(lambda v: Acsr @ v, D, b.reshape(-1), tol=tol, maxiter=maxiter)
+        assert rel(x.reshape(-1), xr) <= 1e-12
+    # with a starting guess
+    xs = np.random.default_rng(0).uniform(-1, 1, b.shape)
+    x = damped_jacobi(A, bv, x0=V.zeros().from_numpy(xs), tol=0.0, maxiter=maxiter).to_local_numpy()
+    xr = orc.damped_jacobi(lambda v: Acsr @ v, D, b.reshape(-1), x0=xs.reshape(-1), tol=0.0, maxiter=maxiter)
+    assert rel(x.reshape(-1), xr) <= 1e-12
+
+
+@pytest.mark.parametrize("ndim,N,p", [(2, 16, 1), (2, 12, 3), (3, 10, 3)])
+def test_pcg_fixed_count(gpu, ndim, N, p):
+    from poms_amd.solvers import damped_jacobi, pcg
+    V, A, Acsr, D, n = _problem(ndim, N, p)
+    b = np.ones((n,) * ndim)
+    bv = V.zeros().from_numpy(b)
+    apply = lambda v: Acsr @ v
+    for m in (1, 3, 6):
+        x, info = pcg(A, lambda AA, r: damped_jacobi(AA, r, tol=0.0), bv, tol=0.0, maxiter=m)
+        xr, ir = orc.pcg(apply, lambda r: orc.damped_jacobi(apply, D, r, tol=0.0), b.reshape(-1), tol=0.0, maxiter=m)
+        assert info["niter"] == ir["niter"] == m
+        assert rel(x.to_local_numpy().reshape(-1), xr) <= 1e-9
+        assert info["res_norm"] == pytest.approx(ir["res_norm"], rel=1e-8)
+
+
+@pytest.mark.parametrize("ndim,N,p", [(2, 16, 1), (3, 8, 3)])
+def test_pcg_reference_defaults(gpu, ndim, N, p):
+    """The V-cycle's call: pcg(A, damped_jacobi, b, tol=1e-6, maxiter=10) (`sources/mg_jac.py:87`)."""
+    from poms_amd.solvers import damped_jacobi, pcg
+    V, A, Acsr, D, n = _problem(ndim, N, p)
+    x0 = np.fromfunction(lambda *i: sum(i) + 1.0, (n,) * ndim)
+    b = (Acsr @ x0.reshape(-1)).reshape(x0.shape)
+    apply = lambda v: Acsr @ v
+    x, info = pcg(A, damped_jacobi, V.zeros().from_numpy(b), tol=1e-6, maxiter=10)
+    xr, ir = orc.pcg(apply, lambda r: orc.damped_jacobi(apply, D, r), b.reshape(-1), tol=1e-6, maxiter=10)
+    assert info["niter"] == ir["niter"]
+    assert info["success"] == ir["success"]
+    assert rel(x.to_local_numpy().reshape(-1), xr) <= 1e-9
+
+
+def test_jacobi_point(gpu):
+    from poms_amd.solvers import jacobi
+    V, A, Acsr, D, n = _problem(2, 9, 2)
+    b = np.random.default_rng(4).uniform(-1, 1, (n, n))
+    x = jacobi(A, V.zeros().from_numpy(b)).to_local_numpy()
+    assert rel(x.reshape(-1), orc.jacobi(D, b.reshape(-1))) <= 1e-15
+
+
+@pytest.mark.parametrize("ndim,p,Nf,Nc", [(2, 1, 16, 8), (2, 3, 32, 8), (3, 2, 16, 8), (3, 3, 16, 4)])
+def test_two_level_vcycle(gpu, ndim, p, Nf, Nc):
+    from poms_amd.mg import TwoLevelVCycle
+    mg = TwoLevelVCycle(p, Nf, Nc, ndim=ndim)
+    b = mg.rhs_ones()
+    x, ipre, ipos = mg.cycle(b)
+    xr, rpre, rpos = orc.vcycle_two_level([mg.M1d] * ndim, [mg.K1d] * ndim, mg.P1, np.ones((mg.n,) * ndim))
+    assert ipre["niter"] == rpre["niter"] and ipos["niter"] == rpos["niter"]
+    assert rel(x.to_local_numpy(), xr) <= 1e-9
+
+
+def test_transfer_restrict_prolong(gpu):
+    from poms_amd.mg import TwoLevelVCycle
+    import torch
+    mg = TwoLevelVCycle(3, 32, 8, ndim=3)
+    rng = np.random.default_rng(9)
+    f = rng.uniform(-1, 1, (mg.n,) * 3)
+    fv = mg.space.zeros().from_numpy(f)
+    rc = mg.transfer.restrict(fv).cpu().numpy()
+    P = mg.P1
+    ref = np.einsum("ia,jb,kc,ijk->abc", P, P, P, f).reshape(-1)
+    assert rel(rc, ref) <= 1e-13
+    xc = rng.uniform(-1, 1, rc.shape)
+    out = mg.space.zeros().from_numpy(f)
+    mg.transfer.prolong_add(torch.from_numpy(xc).cuda(), out)
+    ref2 = f + np.einsum("ia,jb,kc,abc->ijk", P, P, P, xc.reshape((P.shape[1],) * 3))
+    assert rel(out.to_local_numpy(), ref2) <= 1e-13
