@@ -216,12 +216,20 @@ def knots_to_insert(Tf, nf, pf, Tc, nc, pc):
     return np.array([t for t in Tf[pf + 1:nf] if float(t) not in coarse], dtype=np.float64)
 
 
-def vcycle_two_level(M, K, P1, b, c=1.0, tol=1e-6, maxiter=10, x0=None):
-    """`sources/mg_jac.py:84-119` on global arrays with materialised R, P, Ac, splu."""
+def vcycle_two_level(M, K, P1, b, c=1.0, tol=1e-6, maxiter=10, x0=None, reorder=False):
+    """`sources/mg_jac.py:84-119` on global arrays with materialised R, P, Ac, splu.
+
+    ``reorder=True`` applies the fine operator term by term instead of through
+    the assembled CSR matrix: same arithmetic, different summation order (used
+    to measure how much the reference algorithm amplifies roundoff).
+    """
     nd = b.ndim
     A = kron_sum_csr(M, K, c)
     D = kron_sum_diag(M, K, c).reshape(-1)
-    apply = lambda v: A @ v
+    if reorder:
+        apply = lambda v: kron_sum_apply(v.reshape(b.shape), M, K, c).reshape(-1)
+    else:
+        apply = lambda v: A @ v
     psolve = lambda r: damped_jacobi(apply, D, r)
     bf = b.reshape(-1)
     xf, info_pre = pcg(apply, psolve, bf, x0=None if x0 is None else x0.reshape(-1), tol=tol, maxiter=maxiter)

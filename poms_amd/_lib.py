@@ -83,6 +83,10 @@ def header_symbols(path: Path = HEADER_PATH) -> list[str]:
 
 
 def _load() -> C.CDLL:
+    # torch bundles its own libamdhip64.so.7 (same SONAME as /opt/rocm's).  Load
+    # it first so that torch and libpoms_hip.so share ONE HIP runtime in the
+    # process (device pointers and streams are passed between them).
+    import torch  # noqa: F401
     if not LIB_PATH.exists():
         raise ImportError(
             f"libpoms_hip.so not found at {LIB_PATH}: build it with "

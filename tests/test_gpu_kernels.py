@@ -30,7 +30,8 @@ def _factors(p, N, rng=None, kind="spline"):
             for k in range(2 * p + 1):
                 if not 0 <= i + k - p < n:
                     B[i, k] = 0.0
-    M[:, p] += 4.0  # keep the diagonal away from zero for Jacobi
+    M[:, p] += 4.0  # keep diag(A) away from zero (Jacobi divides by it)
+    K[:, p] = np.abs(K[:, p]) + 1.0
     return M, K
 
 
