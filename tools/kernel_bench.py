@@ -1,0 +1,85 @@
+#!/usr/bin/env python3
+"""Micro-benchmark of the fused Kronecker kernels (apply / residual / Jacobi sweep).
+
+Interleaves variants (chunk sizes, kernel variants) in ONE process, reporting
+median / min per-launch time from HIP events on the launch stream and the
+algorithmic GB/s (apply 16 B/DOF, residual and Jacobi 24 B/DOF).
+
+    python tools/kernel_bench.py --cells 512 --p 3 --reps 10 --chunks 0,32,64
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import statistics
+import sys
+from pathlib import Path
+
+ROOT = Path(__file__).resolve().parents[1]
+sys.path.insert(0, str(ROOT))
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--cells", type=int, default=512)
+    ap.add_argument("--p", type=int, default=3)
+    ap.add_argument("--ndim", type=int, default=3)
+    ap.add_argument("--reps", type=int, default=10)
+    ap.add_argument("--rounds", type=int, default=3)
+    ap.add_argument("--chunks", type=str, default="0")
+    ap.add_argument("--variants", type=str, default="")
+    ap.add_argument("--kinds", type=str, default="apply,jacobi")
+    ap.add_argument("--json", type=str, default="")
+    a = ap.parse_args()
+
+    import torch
+    from poms_amd.splines import assemble_1d, uniform_knots
+    from poms_amd.stencil import KronOperator, StencilVectorSpace
+
+    p, N, nd = a.p, a.cells, a.ndim
+    M, K = assemble_1d(uniform_knots(p, N), p)
+    n = N + p
+    V = StencilVectorSpace([n] * nd, [p] * nd)
+    A = KronOperator.laplace(V, [M] * nd, [K] * nd)
+    x, b, y = V.zeros(), V.zeros(), V.zeros()
+    V.interior(x._data).uniform_(-1, 1)
+    V.interior(b._data).uniform_(-1, 1)
+    dof = n ** nd
+    chunks = [int(c) for c in a.chunks.split(",")]
+    variants = [int(v) for v in a.variants.split(",")] if a.variants else [None]
+    kinds = a.kinds.split(",")
+    res = {}
+    for rnd in range(a.rounds):
+        for ch in chunks:
+            A.set_chunk(ch)
+            for var in variants:
+                if var is not None:
+                    A.set_variant(var)
+                for kind in kinds:
+                    fn = {"apply": lambda: A.dot(x, out=y),
+                          "residual": lambda: A.residual(b, x, out=y),
+                          "jacobi": lambda: A.jacobi_sweep(b, x, y, 2.0 / 3.0, want_norm=False)}[kind]
+                    for _ in range(2):
+                        fn()
+                    torch.cuda.synchronize()
+                    A.timer = []
+                    for _ in range(a.reps):
+                        fn()
+                    torch.cuda.synchronize()
+                    ts = [e0.elapsed_time(e1) * 1e3 for _, e0, e1 in A.timer]
+                    A.timer = None
+                    res.setdefault((ch, var, kind), []).extend(ts)
+    out = []
+    for (ch, var, kind), ts in res.items():
+        med = statistics.median(ts)
+        bpd = 16 if kind == "apply" else 24
+        row = {"chunk": ch, "variant": var, "kind": kind, "median_us": med, "min_us": min(ts),
+               "GBps": bpd * dof / med / 1e3, "GDOFps": dof / med / 1e3}
+        out.append(row)
+        print(json.dumps(row), flush=True)
+    if a.json:
+        Path(a.json).write_text(json.dumps(out, indent=1))
+
+
+if __name__ == "__main__":
+    main()
