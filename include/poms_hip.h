@@ -81,6 +81,12 @@ int poms_op_create(poms_ctx* ctx, int ndim, const poms_layout* layout, int form,
 int poms_op_destroy(poms_op* op);
 /* Planes per workgroup along axis 0 (3D); 0 = automatic. */
 int poms_op_set_chunk(poms_op* op, int chunk);
+/* Kernel variant: 0 = general (any band rows, any pads), 1 = Toeplitz-interior
+ * fast path, 4 waves x 4 rows, 2 = same with 8 waves x 2 rows.  Variants 1/2
+ * need storage pads == pmax on every used axis; the default is 1 when that
+ * holds, else 0.  All variants compute the same operator.                     */
+int poms_op_set_variant(poms_op* op, int variant);
+int poms_op_get_variant(poms_op* op, int* variant);
 
 /* y = A x on output planes [z_begin, z_end) (local axis-0 indices; 2D/1D: 0,1).
  * x must have current ghosts on the planes the range touches.

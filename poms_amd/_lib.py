@@ -55,6 +55,8 @@ _SIGS = {
     "poms_op_create": [_vp, _i, _LP, _i, _i, C.POINTER(C.c_void_p), _i64, _i64, _pp],
     "poms_op_destroy": [_vp],
     "poms_op_set_chunk": [_vp, _i],
+    "poms_op_set_variant": [_vp, _i],
+    "poms_op_get_variant": [_vp, C.POINTER(_i)],
     "poms_op_apply": [_vp, _vp, _vp, _i64, _i64, _vp],
     "poms_op_residual": [_vp, _vp, _vp, _vp, _i64, _i64, _vp],
     "poms_op_jacobi_sweep": [_vp, _d, _vp, _vp, _vp, _i64, _i64, _i, _vp],

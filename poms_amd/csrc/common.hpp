@@ -40,6 +40,14 @@ struct AxisPass {
     int accumulate;  // prolongation: out += (1) or out = (0)
 };
 
+// Symmetric-Toeplitz interior of the band factors (v2 fast path): rows
+// [lo, hi) of an axis equal one symmetric row; t?[j] = row[P + j] = row[P - j].
+struct ToepConst {
+    double t1a[6], t1b[6];   // axis 1 (A1, B1)
+    double t0a[6], t0b[6];   // axis 0 (A0, M0), global rows
+    int lo1, hi1, lo0, hi0;
+};
+
 // Device pointers of one fused Kronecker launch.
 struct KronPtrs {
     const double* x;

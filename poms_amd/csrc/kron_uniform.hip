@@ -1,0 +1,365 @@
+// Fused Kronecker(-sum) operator, v2: symmetric-Toeplitz interior fast path.
+//
+// Same operator, epilogues and tile/march structure as kron_fused.hip (v1),
+// with the changes that matter on gfx950:
+//   * interior band rows of uniform-knot B-spline factors are identical and
+//     symmetric (rows [2p, n-2p)); their p+1 distinct values per factor are
+//     kernel arguments (SGPR operands of v_fma_f64) for the axis-1 pass; only
+//     workgroups whose rows touch the domain boundary read general axis-1
+//     rows from a per-tile LDS table.  v1 hoisted R rows x 14 coefficients out
+//     of the plane loop and spilled ~110 SGPRs into VGPR lanes (951
+//     v_readlane).  Axis-0 coefficients (one input plane's column, 2W values)
+//     are scalar-loaded per plane: short-lived SGPRs.
+//   * raw buffer loads/stores (hardware range check returns 0 past the end of
+//     the array) replace per-element predicates; a plane that does not exist
+//     gets a zero-sized descriptor.
+//   * XCD-aware block order: contiguous tile ranges (neighbours sharing
+//     halos) on one XCD's L2.
+// Preconditions (checked by the host): storage pads == P on every used axis.
+#include "common.hpp"
+
+namespace poms {
+
+typedef unsigned int u32x2 __attribute__((ext_vector_type(2)));
+
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t make_rsrc(const void* base, uint32_t bytes) {
+    return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(base), (short)0, (int)bytes, 0x00020000);
+}
+__device__ __forceinline__ double bload(__amdgpu_buffer_rsrc_t r, int off_bytes) {
+    u32x2 v = __builtin_amdgcn_raw_buffer_load_b64(r, off_bytes, 0, 0);
+    return __builtin_bit_cast(double, v);
+}
+__device__ __forceinline__ void bstore(__amdgpu_buffer_rsrc_t r, int off_bytes, double d) {
+    __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(u32x2, d), r, off_bytes, 0, 0);
+}
+
+// bytes of `planes_left` padded planes of s0 doubles, clamped to 2^31-1
+__device__ __forceinline__ uint32_t plane_bytes(int64_t planes_left, int64_t s0) {
+    if (planes_left <= 0) return 0u;
+    const int64_t b = planes_left * s0 * 8;
+    return b > 0x7fffffffLL ? 0x7fffffffu : (uint32_t)b;
+}
+
+template <int P, int R, int NW, bool IS3D, int FORM, int EPI>
+__global__ void __launch_bounds__(NW * 64)
+kron_v2_kernel(const double* __restrict__ x, double* __restrict__ y,
+               const double* __restrict__ bvec,
+               const double* __restrict__ a0t, const double* __restrict__ b0t,
+               const double* __restrict__ a1, const double* __restrict__ b1,
+               const double* __restrict__ a2, const double* __restrict__ b2,
+               double* __restrict__ partial, const KronGeom g, const ToepConst tc,
+               const double omega) {
+    constexpr int W = 2 * P + 1;
+    constexpr int NT = NW * 64;
+    constexpr int T2 = 64;
+    constexpr int T1 = NW * R;
+    constexpr int XR = T1 + 2 * P;
+    constexpr int XC = T2 + 2 * P;
+    constexpr int NX = XR * XC;
+    constexpr int NLD = (NX + NT - 1) / NT;
+    constexpr bool SUM = (FORM == FORM_SUM);
+    constexpr int NS = IS3D ? W : 1;
+
+    __shared__ double xs[NX];
+    __shared__ double as_[XR * T2];
+    __shared__ double bs_[SUM ? XR * T2 : 1];
+    __shared__ double c1a[T1 * W];               // general axis-1 rows of this tile
+    __shared__ double c1b[SUM ? T1 * W : 1];
+    __shared__ double red[NW];
+
+    const int tid = threadIdx.x;
+    const int lane = tid & 63;
+    const int wv = __builtin_amdgcn_readfirstlane(tid >> 6);
+
+    // XCD-aware, bijective block remap: consecutive logical tiles share an XCD.
+    const int nblk = gridDim.x;
+    int bid;
+    {
+        const int b = blockIdx.x, q = nblk >> 3, rr = nblk & 7, xcd = b & 7, k = b >> 3;
+        bid = (xcd < rr ? xcd * (q + 1) : rr * (q + 1) + (xcd - rr) * q) + k;
+    }
+    const int t2 = bid % g.tiles2;
+    bid /= g.tiles2;
+    const int t1 = bid % g.tiles1;
+    const int ch = bid / g.tiles1;
+    const int c0 = t2 * T2;
+    const int r0 = t1 * T1;
+    const int i2 = c0 + lane;
+    const bool col_ok = i2 < g.n2;
+
+    // axis-2: per-lane band rows (general), symmetric pair form when interior.
+    double ca2[W], cb2[W];
+    {
+        const int ic = col_ok ? i2 : g.n2 - 1;
+#pragma unroll
+        for (int k = 0; k < W; ++k) {
+            ca2[k] = a2[ic * W + k];
+            cb2[k] = SUM ? b2[ic * W + k] : 0.0;
+        }
+    }
+    // axis-1: fast iff every row of this tile is a Toeplitz row.
+    const bool fast1 = (r0 >= tc.lo1) && (r0 + T1 <= tc.hi1);
+    if (!fast1) {
+        for (int e = tid; e < T1 * W; e += NT) {
+            const int rl = e / W, k = e - rl * W;
+            const int row = min(r0 + rl, g.n1 - 1);
+            c1a[e] = a1[row * W + k];
+            if constexpr (SUM) c1b[e] = b1[row * W + k];
+        }
+    }
+
+    int z0 = 0, z1 = 1;
+    if constexpr (IS3D) {
+        z0 = g.z_begin + ch * g.chunk;
+        z1 = min(z0 + g.chunk, g.z_end);
+    }
+    const int nplanes = IS3D ? (z1 - z0) + 2 * P : 1;
+    const int nsp = g.n0 + 2 * g.pd0;  // stored planes
+
+    // tile-load byte offsets within a plane (may run past the plane: garbage
+    // there only feeds outputs that are never stored; past the array: zero)
+    int xoff[NLD];
+#pragma unroll
+    for (int l = 0; l < NLD; ++l) {
+        const int e = min(tid + l * NT, NX - 1);
+        const int rr = e / XC, cc = e - (e / XC) * XC;
+        xoff[l] = ((r0 + rr) * (int)g.s1 + (c0 + cc)) * 8;   // pads == P: tile origin at padded (r0, c0)
+    }
+    double xr[NLD];
+    auto load_plane = [&](int jj) {
+        const int sp = IS3D ? jj + g.pd0 : 0;
+        const bool ok = (sp >= 0) && (sp < nsp);
+        const __amdgpu_buffer_rsrc_t rs =
+            make_rsrc(x + (int64_t)(ok ? sp : 0) * g.s0, ok ? plane_bytes(nsp - sp, g.s0) : 0u);
+#pragma unroll
+        for (int l = 0; l < NLD; ++l) xr[l] = bload(rs, xoff[l]);
+    };
+
+    double acc[R][NS];
+#pragma unroll
+    for (int r = 0; r < R; ++r)
+#pragma unroll
+        for (int s = 0; s < NS; ++s) acc[r][s] = 0.0;
+    double nrm = 0.0;
+
+    const int obase_inplane = ((r0 + wv * R + g.pd1) * (int)g.s1 + (i2 + g.pd2)) * 8;
+
+    auto epilogue = [&](int zo, int r, double v) {
+        const int i1 = r0 + wv * R + r;
+        if (!(col_ok && i1 < g.n1)) return;
+        const int sp = zo + g.pd0;
+        const int off = obase_inplane + r * (int)g.s1 * 8;
+        const uint32_t nb = plane_bytes(nsp - sp, g.s0);
+        const __amdgpu_buffer_rsrc_t ys = make_rsrc(y + (int64_t)sp * g.s0, nb);
+        if constexpr (EPI == EPI_APPLY) {
+            bstore(ys, off, v);
+        } else if constexpr (EPI == EPI_RESID) {
+            const __amdgpu_buffer_rsrc_t bs = make_rsrc(bvec + (int64_t)sp * g.s0, nb);
+            bstore(ys, off, bload(bs, off) - v);
+        } else {
+            const __amdgpu_buffer_rsrc_t bs = make_rsrc(bvec + (int64_t)sp * g.s0, nb);
+            const __amdgpu_buffer_rsrc_t xsr = make_rsrc(x + (int64_t)sp * g.s0, nb);
+            const double d1a = fast1 ? tc.t1a[0] : c1a[(wv * R + r) * W + P];
+            const double d2a = ca2[P];
+            double diag;
+            if constexpr (IS3D) {
+                const int i0g = g.g0 + zo;
+                const double d0a = a0t[(i0g + P) * W + P];
+                if constexpr (SUM) {
+                    const double d0b = b0t[(i0g + P) * W + P];
+                    const double d1b = fast1 ? tc.t1b[0] : c1b[(wv * R + r) * W + P];
+                    diag = d0a * (d1a * d2a) + d0b * (d1b * d2a + d1a * cb2[P]);
+                } else {
+                    diag = d0a * d1a * d2a;
+                }
+            } else {
+                if constexpr (SUM) {
+                    const double d1b = fast1 ? tc.t1b[0] : c1b[(wv * R + r) * W + P];
+                    diag = d1a * d2a + d1b * cb2[P];
+                } else {
+                    diag = d1a * d2a;
+                }
+            }
+            const double dr = omega * (bload(bs, off) - v) / diag;
+            bstore(ys, off, bload(xsr, off) + dr);
+            nrm = fma(dr, dr, nrm);
+        }
+    };
+
+    load_plane(IS3D ? z0 - P : 0);
+    __syncthreads();  // c1a/c1b table visible
+    for (int tb = 0; tb < nplanes; tb += NS) {
+#pragma unroll
+        for (int q = 0; q < NS; ++q) {
+            const int t = tb + q;
+            if (t < nplanes) {
+#pragma unroll
+                for (int l = 0; l < NLD; ++l) {
+                    const int e = tid + l * NT;
+                    if (NX % NT == 0 || e < NX) xs[e] = xr[l];
+                }
+                __syncthreads();
+                if (IS3D && t + 1 < nplanes) load_plane(z0 - P + t + 1);
+
+                // ---- axis 2 (LDS -> LDS)
+#pragma unroll
+                for (int it = 0; it < (XR + NW - 1) / NW; ++it) {
+                    const int rr = wv + it * NW;
+                    if (rr < XR) {
+                        const double* xp = xs + rr * XC + lane;
+                        double sa, sb = 0.0;
+                        sa = ca2[0] * xp[0];
+                        if constexpr (SUM) sb = cb2[0] * xp[0];
+#pragma unroll
+                        for (int k = 1; k < W; ++k) {
+                            const double v = xp[k];
+                            sa = fma(ca2[k], v, sa);
+                            if constexpr (SUM) sb = fma(cb2[k], v, sb);
+                        }
+                        as_[rr * T2 + lane] = sa;
+                        if constexpr (SUM) bs_[rr * T2 + lane] = sb;
+                    }
+                }
+                __syncthreads();
+
+                // ---- axis 1 (streamed rows; Toeplitz constants or LDS table)
+                double cv[R], dv[R];
+#pragma unroll
+                for (int r = 0; r < R; ++r) { cv[r] = 0.0; dv[r] = 0.0; }
+                if (fast1) {
+#pragma unroll
+                    for (int qq = 0; qq < R + 2 * P; ++qq) {
+                        const int rr = wv * R + qq;
+                        const double va = as_[rr * T2 + lane];
+                        const double vb = SUM ? bs_[rr * T2 + lane] : 0.0;
+#pragma unroll
+                        for (int r = 0; r < R; ++r) {
+                            const int k = qq - r;
+                            if (k >= 0 && k < W) {
+                                const int j = k < P ? P - k : k - P;
+                                cv[r] = fma(tc.t1a[j], va, cv[r]);
+                                if constexpr (SUM) {
+                                    if constexpr (IS3D) dv[r] = fma(tc.t1b[j], va, fma(tc.t1a[j], vb, dv[r]));
+                                    else cv[r] = fma(tc.t1b[j], vb, cv[r]);
+                                }
+                            }
+                        }
+                    }
+                } else {
+#pragma unroll
+                    for (int qq = 0; qq < R + 2 * P; ++qq) {
+                        const int rr = wv * R + qq;
+                        const double va = as_[rr * T2 + lane];
+                        const double vb = SUM ? bs_[rr * T2 + lane] : 0.0;
+#pragma unroll
+                        for (int r = 0; r < R; ++r) {
+                            const int k = qq - r;
+                            if (k >= 0 && k < W) {
+                                const double ca = c1a[(wv * R + r) * W + k];
+                                cv[r] = fma(ca, va, cv[r]);
+                                if constexpr (SUM) {
+                                    const double cb = c1b[(wv * R + r) * W + k];
+                                    if constexpr (IS3D) dv[r] = fma(cb, va, fma(ca, vb, dv[r]));
+                                    else cv[r] = fma(cb, vb, cv[r]);
+                                }
+                            }
+                        }
+                    }
+                }
+
+                if constexpr (IS3D) {
+                    // ---- axis 0: scatter into rotating slots (per-plane scalar loads)
+                    const int jrow = (g.g0 + z0 - P + t + P) * W;
+#pragma unroll
+                    for (int s = 0; s < W; ++s) {
+                        const int slot = (q - P + s + NS) % NS;
+                        const double ka = a0t[jrow + s];
+                        const double kb = SUM ? b0t[jrow + s] : 0.0;
+#pragma unroll
+                        for (int r = 0; r < R; ++r) {
+                            acc[r][slot] = fma(ka, cv[r], acc[r][slot]);
+                            if constexpr (SUM) acc[r][slot] = fma(kb, dv[r], acc[r][slot]);
+                        }
+                    }
+                    const int done = (q + P + 1) % NS;
+                    if (t >= 2 * P) {
+                        const int zo = z0 - 2 * P + t;
+#pragma unroll
+                        for (int r = 0; r < R; ++r) epilogue(zo, r, acc[r][done]);
+                    }
+#pragma unroll
+                    for (int r = 0; r < R; ++r) acc[r][done] = 0.0;
+                } else {
+#pragma unroll
+                    for (int r = 0; r < R; ++r) epilogue(0, r, cv[r]);
+                }
+            }
+        }
+    }
+
+    if constexpr (EPI == EPI_JACOBI) {
+        if (partial != nullptr) {
+#pragma unroll
+            for (int off = 32; off > 0; off >>= 1) nrm += __shfl_xor(nrm, off, 64);
+            if (lane == 0) red[wv] = nrm;
+            __syncthreads();
+            if (tid == 0) {
+                double s = 0.0;
+                for (int w = 0; w < NW; ++w) s += red[w];
+                partial[blockIdx.x] = s;
+            }
+        }
+    }
+}
+
+// ---------------------------------------------------------------------------
+template <int P, int R, int NW, bool IS3D, int FORM, int EPI>
+static void v2_launch_t(const KronPtrs& p, const KronGeom& g, const ToepConst& tc, double omega,
+                        hipStream_t st) {
+    const int nblk = g.tiles2 * g.tiles1 * g.nchunks;
+    hipLaunchKernelGGL((kron_v2_kernel<P, R, NW, IS3D, FORM, EPI>), dim3(nblk), dim3(NW * 64), 0, st,
+                       p.x, p.y, p.b, p.a0t, p.b0t, p.a1, p.b1, p.a2, p.b2, p.partial, g, tc, omega);
+}
+
+template <int P, int R, int NW, bool IS3D, int FORM>
+static int v2_launch_e(int epi, const KronPtrs& p, const KronGeom& g, const ToepConst& tc,
+                       double omega, hipStream_t st) {
+    switch (epi) {
+        case EPI_APPLY: v2_launch_t<P, R, NW, IS3D, FORM, EPI_APPLY>(p, g, tc, omega, st); return 0;
+        case EPI_RESID: v2_launch_t<P, R, NW, IS3D, FORM, EPI_RESID>(p, g, tc, omega, st); return 0;
+        case EPI_JACOBI: v2_launch_t<P, R, NW, IS3D, FORM, EPI_JACOBI>(p, g, tc, omega, st); return 0;
+    }
+    return 1;
+}
+
+template <int P, int R, int NW>
+static int v2_launch_p(bool is3d, int form, int epi, const KronPtrs& p, const KronGeom& g,
+                       const ToepConst& tc, double omega, hipStream_t st) {
+    if (is3d)
+        return form == FORM_SUM ? v2_launch_e<P, R, NW, true, FORM_SUM>(epi, p, g, tc, omega, st)
+                                : v2_launch_e<P, R, NW, true, FORM_SINGLE>(epi, p, g, tc, omega, st);
+    return form == FORM_SUM ? v2_launch_e<P, R, NW, false, FORM_SUM>(epi, p, g, tc, omega, st)
+                            : v2_launch_e<P, R, NW, false, FORM_SINGLE>(epi, p, g, tc, omega, st);
+}
+
+// variant 1: 4 waves x 4 rows (16 x 64 tile); 2: 8 waves x 2 rows (16 x 64); 3: 8 waves x 4 rows (32 x 64)
+int kron_v2_launch(int variant, int pmax, bool is3d, int form, int epi, const KronPtrs& p,
+                   const KronGeom& g, const ToepConst& tc, double omega, hipStream_t st) {
+#define POMS_V2P(PP)                                                                        \
+    case PP:                                                                                \
+        return variant == 2   ? v2_launch_p<PP, 2, 8>(is3d, form, epi, p, g, tc, omega, st)   \
+               : variant == 3 ? v2_launch_p<PP, 4, 8>(is3d, form, epi, p, g, tc, omega, st)   \
+                              : v2_launch_p<PP, 4, 4>(is3d, form, epi, p, g, tc, omega, st);
+    switch (pmax) {
+        POMS_V2P(1)
+        POMS_V2P(2)
+        POMS_V2P(3)
+        POMS_V2P(4)
+        POMS_V2P(5)
+    }
+#undef POMS_V2P
+    set_error("pmax must be in 1..5");
+    return 1;
+}
+
+}  // namespace poms

@@ -13,6 +13,8 @@ void set_error(const std::string& msg) { g_err = msg; }
 
 int kron_launch(int pmax, bool is3d, int form, int epi, const KronPtrs& p, const KronGeom& g,
                 double omega, hipStream_t st);
+int kron_v2_launch(int variant, int pmax, bool is3d, int form, int epi, const KronPtrs& p,
+                   const KronGeom& g, const ToepConst& tc, double omega, hipStream_t st);
 int kron_tile_rows();
 int kron_tile_cols();
 int vec_launch(int op, const RowGeom& g, double a, double b, const double* x, const double* y,
@@ -46,7 +48,44 @@ struct poms_op {
     int64_t g0 = 0, n0g = 1;
     double *a0t = nullptr, *b0t = nullptr, *a1 = nullptr, *b1 = nullptr, *a2 = nullptr, *b2 = nullptr;
     int64_t last_partials = 0;
+    int variant = 0;
+    bool v2_ok = false;
+    ToepConst tc{};
 };
+
+// Largest row range [lo, hi) around the middle whose band rows equal one
+// symmetric row (bitwise), for the pair (fa, fb) (fb may be null).
+static void toeplitz_range(const double* fa, const double* fb, int64_t n, int P, int* lo, int* hi,
+                           double* ta, double* tb) {
+    const int W = 2 * P + 1;
+    *lo = *hi = 0;
+    for (int j = 0; j < 6; ++j) { ta[j] = 0.0; tb[j] = 0.0; }
+    if (n < 1) return;
+    const int64_t m = n / 2;
+    auto sym = [&](const double* f) {
+        if (!f) return true;
+        for (int j = 1; j <= P; ++j)
+            if (f[m * W + P + j] != f[m * W + P - j]) return false;
+        return true;
+    };
+    if (!sym(fa) || !sym(fb)) return;
+    auto same = [&](int64_t i) {
+        for (int k = 0; k < W; ++k) {
+            if (fa[i * W + k] != fa[m * W + k]) return false;
+            if (fb && fb[i * W + k] != fb[m * W + k]) return false;
+        }
+        return true;
+    };
+    int64_t a = m, b = m + 1;
+    while (a > 0 && same(a - 1)) --a;
+    while (b < n && same(b)) ++b;
+    *lo = (int)a;
+    *hi = (int)b;
+    for (int j = 0; j <= P; ++j) {
+        ta[j] = fa[m * W + P + j];
+        tb[j] = fb ? fb[m * W + P + j] : 0.0;
+    }
+}
 
 struct poms_transfer {
     poms_ctx* ctx = nullptr;
@@ -183,6 +222,12 @@ int poms_op_create(poms_ctx* ctx, int ndim, const poms_layout* layout, int form,
         rc |= upload(f[5], (size_t)layout->n[2] * W, &o->b2);
     }
     if (rc) { poms_op_destroy(o); return 1; }
+    // v2 preconditions: storage pads == pmax on the used axes
+    o->v2_ok = layout->pads[1] == pmax && layout->pads[2] == pmax && (!is3d || layout->pads[0] == pmax);
+    if (is3d)
+        toeplitz_range(f[0], sum ? f[1] : nullptr, n0_global, pmax, &o->tc.lo0, &o->tc.hi0, o->tc.t0a, o->tc.t0b);
+    toeplitz_range(f[2], sum ? f[3] : nullptr, layout->n[1], pmax, &o->tc.lo1, &o->tc.hi1, o->tc.t1a, o->tc.t1b);
+    o->variant = o->v2_ok ? 1 : 0;
     *op = o;
     return 0;
 }
@@ -192,6 +237,19 @@ int poms_op_destroy(poms_op* o) {
     for (double* p : {o->a0t, o->b0t, o->a1, o->b1, o->a2, o->b2})
         if (p) (void)hipFree(p);
     delete o;
+    return 0;
+}
+
+int poms_op_set_variant(poms_op* op, int variant) {
+    if (!op || variant < 0 || variant > 3) { set_error("poms_op_set_variant: bad argument"); return 1; }
+    if (variant > 0 && !op->v2_ok) { set_error("poms_op_set_variant: variant needs pads == pmax"); return 1; }
+    op->variant = variant;
+    return 0;
+}
+
+int poms_op_get_variant(poms_op* op, int* variant) {
+    if (!op || !variant) { set_error("poms_op_get_variant: null argument"); return 1; }
+    *variant = op->variant;
     return 0;
 }
 
@@ -210,7 +268,8 @@ static int op_geom(poms_op* o, int64_t zb, int64_t ze, KronGeom& g) {
     g.pd0 = r.pd0; g.pd1 = r.pd1; g.pd2 = r.pd2;
     g.g0 = (int)o->g0;
     g.tiles2 = (int)((o->L.n[2] + kron_tile_cols() - 1) / kron_tile_cols());
-    g.tiles1 = (int)((o->L.n[1] + kron_tile_rows() - 1) / kron_tile_rows());
+    const int trows = o->variant == 3 ? 32 : kron_tile_rows();
+    g.tiles1 = (int)((o->L.n[1] + trows - 1) / trows);
     if (!is3d) {
         g.z_begin = 0; g.z_end = 1; g.chunk = 1; g.nchunks = 1;
         return 0;
@@ -242,7 +301,10 @@ static int op_run(poms_op* o, int epi, double omega, const double* x, double* y,
     if (want_norm && nblk > kScratch) { set_error("too many blocks for norm scratch"); return 1; }
     KronPtrs p{x, y, b, o->a0t, o->b0t, o->a1, o->b1, o->a2, o->b2,
                want_norm ? o->ctx->scratch : nullptr};
-    if (kron_launch(o->pmax, o->ndim == 3, o->form, epi, p, g, omega, as_stream(stream))) return 1;
+    const int rc = o->variant == 0
+        ? kron_launch(o->pmax, o->ndim == 3, o->form, epi, p, g, omega, as_stream(stream))
+        : kron_v2_launch(o->variant, o->pmax, o->ndim == 3, o->form, epi, p, g, o->tc, omega, as_stream(stream));
+    if (rc) return 1;
     POMS_HIP_CHECK(hipGetLastError());
     o->last_partials = want_norm ? nblk : 0;
     return 0;

@@ -460,6 +460,16 @@ class KronOperator:
     def set_chunk(self, chunk: int) -> None:
         _lib.call("poms_op_set_chunk", self._h, int(chunk))
 
+    def set_variant(self, variant: int) -> None:
+        """0 = general kernel, 1/2 = Toeplitz-interior kernels (see poms_hip.h)."""
+        _lib.call("poms_op_set_variant", self._h, int(variant))
+
+    @property
+    def variant(self) -> int:
+        v = C.c_int()
+        _lib.call("poms_op_get_variant", self._h, C.byref(v))
+        return v.value
+
     def _check(self, *vs):
         for v in vs:
             if not isinstance(v, StencilVector) or v.space is not self.space:
