@@ -111,6 +111,11 @@ int poms_op_jacobi_sweep(poms_op* op, double omega, const double* b,
  * first damped-Jacobi sweep from x0 = 0 (A.0 = 0 exactly).                    */
 int poms_op_diag_scale(poms_op* op, double scale, const double* b, double* x,
                        int want_norm, void* stream);
+/* DIAGNOSTIC ONLY: run the s_memtime-stamped build of the kernel (3D p=3,
+ * variants 1/2) and write 8 per-phase cycle sums per wave into dbg (device,
+ * nwaves*8 uint64).  Stamps perturb the schedule: read shares, not times.    */
+int poms_op_profile_phases(poms_op* op, int jacobi, const double* b, const double* x,
+                           double* y, uint64_t* dbg, int64_t* nwaves, void* stream);
 /* Number of norm partials the last want_norm launch on this op produced. */
 int poms_op_last_partials(poms_op* op, int64_t* count);
 

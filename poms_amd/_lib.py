@@ -62,6 +62,7 @@ _SIGS = {
     "poms_op_jacobi_sweep": [_vp, _d, _vp, _vp, _vp, _i64, _i64, _i, _vp],
     "poms_op_diag_scale": [_vp, _d, _vp, _vp, _i, _vp],
     "poms_op_last_partials": [_vp, C.POINTER(_i64)],
+    "poms_op_profile_phases": [_vp, _i, _vp, _vp, _vp, _vp, C.POINTER(_i64), _vp],
     "poms_kron_dot_2d": [_vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _i64, _vp, _i64],
     "poms_vec_axpby": [_vp, _LP, _d, _vp, _d, _vp, _vp, _vp],
     "poms_vec_scale": [_vp, _LP, _d, _vp, _vp, _vp],

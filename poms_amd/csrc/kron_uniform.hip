@@ -40,7 +40,9 @@ __device__ __forceinline__ uint32_t plane_bytes(int64_t planes_left, int64_t s0)
     return b > 0x7fffffffLL ? 0x7fffffffu : (uint32_t)b;
 }
 
-template <int P, int R, int NW, bool IS3D, int FORM, int EPI>
+// STAMPS: diagnostic build only -- per-wave cycle shares of the plane-loop
+// phases (s_memtime), written to `dbg`; never used for timing claims.
+template <int P, int R, int NW, bool IS3D, int FORM, int EPI, bool STAMPS = false>
 __global__ void __launch_bounds__(NW * 64)
 kron_v2_kernel(const double* __restrict__ x, double* __restrict__ y,
                const double* __restrict__ bvec,
@@ -48,7 +50,7 @@ kron_v2_kernel(const double* __restrict__ x, double* __restrict__ y,
                const double* __restrict__ a1, const double* __restrict__ b1,
                const double* __restrict__ a2, const double* __restrict__ b2,
                double* __restrict__ partial, const KronGeom g, const ToepConst tc,
-               const double omega) {
+               const double omega, unsigned long long* __restrict__ dbg = nullptr) {
     constexpr int W = 2 * P + 1;
     constexpr int NT = NW * 64;
     constexpr int T2 = 64;
@@ -143,51 +145,86 @@ kron_v2_kernel(const double* __restrict__ x, double* __restrict__ y,
     double nrm = 0.0;
 
     const int obase_inplane = ((r0 + wv * R + g.pd1) * (int)g.s1 + (i2 + g.pd2)) * 8;
-
-    auto epilogue = [&](int zo, int r, double v) {
-        const int i1 = r0 + wv * R + r;
-        if (!(col_ok && i1 < g.n1)) return;
-        const int sp = zo + g.pd0;
-        const int off = obase_inplane + r * (int)g.s1 * 8;
-        const uint32_t nb = plane_bytes(nsp - sp, g.s0);
-        const __amdgpu_buffer_rsrc_t ys = make_rsrc(y + (int64_t)sp * g.s0, nb);
-        if constexpr (EPI == EPI_APPLY) {
-            bstore(ys, off, v);
-        } else if constexpr (EPI == EPI_RESID) {
+    const int rowstep = (int)g.s1 * 8;
+    double dX[R], dY[R];   // plane-invariant parts of diag(A) (JACOBI), set after the barrier below
+    // epilogue operands of the output plane, issued early (before the
+    // next-plane prefetch, so waiting for them never drains the prefetch)
+    double eb[R], ex[R];
+    auto epi_issue = [&](int zo) {
+        if constexpr (EPI != EPI_APPLY) {
+            const int sp = zo + g.pd0;
+            const uint32_t nb = plane_bytes(nsp - sp, g.s0);
             const __amdgpu_buffer_rsrc_t bs = make_rsrc(bvec + (int64_t)sp * g.s0, nb);
-            bstore(ys, off, bload(bs, off) - v);
-        } else {
-            const __amdgpu_buffer_rsrc_t bs = make_rsrc(bvec + (int64_t)sp * g.s0, nb);
-            const __amdgpu_buffer_rsrc_t xsr = make_rsrc(x + (int64_t)sp * g.s0, nb);
-            const double d1a = fast1 ? tc.t1a[0] : c1a[(wv * R + r) * W + P];
-            const double d2a = ca2[P];
-            double diag;
-            if constexpr (IS3D) {
-                const int i0g = g.g0 + zo;
-                const double d0a = a0t[(i0g + P) * W + P];
-                if constexpr (SUM) {
-                    const double d0b = b0t[(i0g + P) * W + P];
-                    const double d1b = fast1 ? tc.t1b[0] : c1b[(wv * R + r) * W + P];
-                    diag = d0a * (d1a * d2a) + d0b * (d1b * d2a + d1a * cb2[P]);
-                } else {
-                    diag = d0a * d1a * d2a;
-                }
-            } else {
-                if constexpr (SUM) {
-                    const double d1b = fast1 ? tc.t1b[0] : c1b[(wv * R + r) * W + P];
-                    diag = d1a * d2a + d1b * cb2[P];
-                } else {
-                    diag = d1a * d2a;
-                }
+#pragma unroll
+            for (int r = 0; r < R; ++r) eb[r] = bload(bs, obase_inplane + r * rowstep);
+            if constexpr (EPI == EPI_JACOBI) {
+                const __amdgpu_buffer_rsrc_t xsr = make_rsrc(x + (int64_t)sp * g.s0, nb);
+#pragma unroll
+                for (int r = 0; r < R; ++r) ex[r] = bload(xsr, obase_inplane + r * rowstep);
             }
-            const double dr = omega * (bload(bs, off) - v) / diag;
-            bstore(ys, off, bload(xsr, off) + dr);
-            nrm = fma(dr, dr, nrm);
+        }
+    };
+    auto epi_finish = [&](int zo, const double* v) {
+        const int sp = zo + g.pd0;
+        const __amdgpu_buffer_rsrc_t ys = make_rsrc(y + (int64_t)sp * g.s0, plane_bytes(nsp - sp, g.s0));
+        double d0a = 1.0, d0b = 0.0;
+        if constexpr (EPI == EPI_JACOBI && IS3D) {
+            const int i0g = g.g0 + zo;
+            d0a = a0t[(i0g + P) * W + P];
+            if constexpr (SUM) d0b = b0t[(i0g + P) * W + P];
+        }
+#pragma unroll
+        for (int r = 0; r < R; ++r) {
+            double outv;
+            if constexpr (EPI == EPI_APPLY) {
+                outv = v[r];
+            } else if constexpr (EPI == EPI_RESID) {
+                outv = eb[r] - v[r];
+            } else {
+                const double diag = IS3D ? fma(d0a, dX[r], d0b * dY[r]) : dX[r];
+                // 1/diag: v_rcp_f64 + two Newton steps (<= 1 ulp)
+                double rc = __builtin_amdgcn_rcp(diag);
+                double e = fma(-diag, rc, 1.0);
+                rc = fma(rc, e, rc);
+                e = fma(-diag, rc, 1.0);
+                rc = fma(rc, e, rc);
+                const double dr = omega * (eb[r] - v[r]) * rc;
+                outv = ex[r] + dr;
+                const bool ok = col_ok && (r0 + wv * R + r < g.n1);
+                nrm = ok ? fma(dr, dr, nrm) : nrm;
+            }
+            if (col_ok && (r0 + wv * R + r < g.n1)) bstore(ys, obase_inplane + r * rowstep, outv);
         }
     };
 
+    unsigned long long tph[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    unsigned long long tlast = 0;
+#define POMS_STAMP(i)                                                      \
+    if constexpr (STAMPS) {                                                \
+        __builtin_amdgcn_sched_barrier(0);                                 \
+        const unsigned long long tnow = __builtin_amdgcn_s_memtime();     \
+        tph[i] += tnow - tlast;                                            \
+        tlast = tnow;                                                      \
+        __builtin_amdgcn_sched_barrier(0);                                 \
+    }
     load_plane(IS3D ? z0 - P : 0);
     __syncthreads();  // c1a/c1b table visible
+    // plane-invariant parts of diag(A) for this thread's points (JACOBI)
+    if constexpr (EPI == EPI_JACOBI) {
+#pragma unroll
+        for (int r = 0; r < R; ++r) {
+            const double d1a = fast1 ? tc.t1a[0] : c1a[(wv * R + r) * W + P];
+            const double d1b = SUM ? (fast1 ? tc.t1b[0] : c1b[(wv * R + r) * W + P]) : 0.0;
+            if constexpr (IS3D) {
+                dX[r] = d1a * ca2[P];
+                dY[r] = SUM ? (d1b * ca2[P] + d1a * cb2[P]) : 0.0;
+            } else {
+                dX[r] = SUM ? (d1a * ca2[P] + d1b * cb2[P]) : d1a * ca2[P];
+                dY[r] = 0.0;
+            }
+        }
+    }
+    if constexpr (STAMPS) tlast = __builtin_amdgcn_s_memtime();
     for (int tb = 0; tb < nplanes; tb += NS) {
 #pragma unroll
         for (int q = 0; q < NS; ++q) {
@@ -198,8 +235,12 @@ kron_v2_kernel(const double* __restrict__ x, double* __restrict__ y,
                     const int e = tid + l * NT;
                     if (NX % NT == 0 || e < NX) xs[e] = xr[l];
                 }
+                POMS_STAMP(0)
                 __syncthreads();
+                POMS_STAMP(1)
+                if (!IS3D || t >= 2 * P) epi_issue(IS3D ? z0 - 2 * P + t : 0);
                 if (IS3D && t + 1 < nplanes) load_plane(z0 - P + t + 1);
+                POMS_STAMP(2)
 
                 // ---- axis 2 (LDS -> LDS)
 #pragma unroll
@@ -220,7 +261,9 @@ kron_v2_kernel(const double* __restrict__ x, double* __restrict__ y,
                         if constexpr (SUM) bs_[rr * T2 + lane] = sb;
                     }
                 }
+                POMS_STAMP(3)
                 __syncthreads();
+                POMS_STAMP(4)
 
                 // ---- axis 1 (streamed rows; Toeplitz constants or LDS table)
                 double cv[R], dv[R];
@@ -267,6 +310,7 @@ kron_v2_kernel(const double* __restrict__ x, double* __restrict__ y,
                     }
                 }
 
+                POMS_STAMP(5)
                 if constexpr (IS3D) {
                     // ---- axis 0: scatter into rotating slots (per-plane scalar loads)
                     const int jrow = (g.g0 + z0 - P + t + P) * W;
@@ -282,21 +326,28 @@ kron_v2_kernel(const double* __restrict__ x, double* __restrict__ y,
                         }
                     }
                     const int done = (q + P + 1) % NS;
+                    POMS_STAMP(6)
                     if (t >= 2 * P) {
-                        const int zo = z0 - 2 * P + t;
+                        double vv[R];
 #pragma unroll
-                        for (int r = 0; r < R; ++r) epilogue(zo, r, acc[r][done]);
+                        for (int r = 0; r < R; ++r) vv[r] = acc[r][done];
+                        epi_finish(z0 - 2 * P + t, vv);
                     }
+                    POMS_STAMP(7)
 #pragma unroll
                     for (int r = 0; r < R; ++r) acc[r][done] = 0.0;
                 } else {
-#pragma unroll
-                    for (int r = 0; r < R; ++r) epilogue(0, r, cv[r]);
+                    epi_finish(0, cv);
                 }
             }
         }
     }
 
+#undef POMS_STAMP
+    if constexpr (STAMPS) {
+        if (lane == 0 && dbg != nullptr)
+            for (int i = 0; i < 8; ++i) dbg[((size_t)blockIdx.x * NW + wv) * 8 + i] = tph[i];
+    }
     if constexpr (EPI == EPI_JACOBI) {
         if (partial != nullptr) {
 #pragma unroll
@@ -340,6 +391,24 @@ static int v2_launch_p(bool is3d, int form, int epi, const KronPtrs& p, const Kr
                                 : v2_launch_e<P, R, NW, true, FORM_SINGLE>(epi, p, g, tc, omega, st);
     return form == FORM_SUM ? v2_launch_e<P, R, NW, false, FORM_SUM>(epi, p, g, tc, omega, st)
                             : v2_launch_e<P, R, NW, false, FORM_SINGLE>(epi, p, g, tc, omega, st);
+}
+
+// Diagnostic launch (STAMPS build): P=3, 3D, FORM_SUM, APPLY or JACOBI,
+// variant 1 or 2; dbg receives nblk*NW*8 cycle counters.
+int kron_v2_stamps(int variant, int epi, const KronPtrs& p, const KronGeom& g, const ToepConst& tc,
+                   double omega, unsigned long long* dbg, hipStream_t st) {
+    const int nblk = g.tiles2 * g.tiles1 * g.nchunks;
+#define POMS_ST(R_, NW_, E_)                                                                       \
+    hipLaunchKernelGGL((kron_v2_kernel<3, R_, NW_, true, FORM_SUM, E_, true>), dim3(nblk),           \
+                       dim3(NW_ * 64), 0, st, p.x, p.y, p.b, p.a0t, p.b0t, p.a1, p.b1, p.a2, p.b2,    \
+                       p.partial, g, tc, omega, dbg)
+    if (variant == 2) {
+        if (epi == EPI_JACOBI) POMS_ST(2, 8, EPI_JACOBI); else POMS_ST(2, 8, EPI_APPLY);
+    } else {
+        if (epi == EPI_JACOBI) POMS_ST(4, 4, EPI_JACOBI); else POMS_ST(4, 4, EPI_APPLY);
+    }
+#undef POMS_ST
+    return 0;
 }
 
 // variant 1: 4 waves x 4 rows (16 x 64 tile); 2: 8 waves x 2 rows (16 x 64); 3: 8 waves x 4 rows (32 x 64)

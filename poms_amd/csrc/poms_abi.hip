@@ -15,6 +15,8 @@ int kron_launch(int pmax, bool is3d, int form, int epi, const KronPtrs& p, const
                 double omega, hipStream_t st);
 int kron_v2_launch(int variant, int pmax, bool is3d, int form, int epi, const KronPtrs& p,
                    const KronGeom& g, const ToepConst& tc, double omega, hipStream_t st);
+int kron_v2_stamps(int variant, int epi, const KronPtrs& p, const KronGeom& g, const ToepConst& tc,
+                   double omega, unsigned long long* dbg, hipStream_t st);
 int kron_tile_rows();
 int kron_tile_cols();
 int vec_launch(int op, const RowGeom& g, double a, double b, const double* x, const double* y,
@@ -335,6 +337,24 @@ int poms_op_diag_scale(poms_op* o, double scale, const double* b, double* x, int
                       as_stream(stream), &nb);
     POMS_HIP_CHECK(hipGetLastError());
     o->last_partials = want_norm ? nb : 0;
+    return 0;
+}
+
+int poms_op_profile_phases(poms_op* o, int jacobi, const double* b, const double* x, double* y,
+                           uint64_t* dbg, int64_t* nwaves, void* stream) {
+    if (!o || !x || !y || !dbg || !nwaves || (jacobi && !b)) { set_error("profile: null argument"); return 1; }
+    if (o->ndim != 3 || o->form != FORM_SUM || o->pmax != 3 || (o->variant != 1 && o->variant != 2)) {
+        set_error("profile: diagnostic build exists for 3D FORM_SUM p=3, variants 1/2");
+        return 1;
+    }
+    KronGeom g;
+    if (op_geom(o, 0, o->L.n[0], g)) return 1;
+    const int64_t nblk = (int64_t)g.tiles2 * g.tiles1 * g.nchunks;
+    *nwaves = nblk * (o->variant == 2 ? 8 : 4);
+    KronPtrs p{x, y, b, o->a0t, o->b0t, o->a1, o->b1, o->a2, o->b2, nullptr};
+    kron_v2_stamps(o->variant, jacobi ? EPI_JACOBI : EPI_APPLY, p, g, o->tc, 2.0 / 3.0,
+                   reinterpret_cast<unsigned long long*>(dbg), as_stream(stream));
+    POMS_HIP_CHECK(hipGetLastError());
     return 0;
 }
 
