@@ -82,9 +82,10 @@ int poms_op_destroy(poms_op* op);
 /* Planes per workgroup along axis 0 (3D); 0 = automatic. */
 int poms_op_set_chunk(poms_op* op, int chunk);
 /* Kernel variant: 0 = general (any band rows, any pads), 1 = Toeplitz-interior
- * fast path, 4 waves x 4 rows, 2 = same with 8 waves x 2 rows.  Variants 1/2
- * need storage pads == pmax on every used axis; the default is 1 when that
- * holds, else 0.  All variants compute the same operator.                     */
+ * fast path, 4 waves x 4 rows, 2 = same with 8 waves x 2 rows, 3 = 8 waves x
+ * 4 rows, 4 = DPP axis-2 pass with one barrier per plane.  Variants 1-4 need
+ * storage pads == pmax on every used axis; the default is the fastest
+ * measured one when that holds, else 0.  All variants compute the same operator. */
 int poms_op_set_variant(poms_op* op, int variant);
 int poms_op_get_variant(poms_op* op, int* variant);
 

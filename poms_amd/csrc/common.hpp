@@ -71,6 +71,28 @@ __device__ inline double block_sum_256(double v, double* red4) {
     return s;
 }
 
+// ---- raw buffer access (hardware range check: loads past num_records return
+// 0, stores past it are dropped) ------------------------------------------------
+typedef unsigned int u32x2 __attribute__((ext_vector_type(2)));
+
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t make_rsrc(const void* base, uint32_t bytes) {
+    return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(base), (short)0, (int)bytes, 0x00020000);
+}
+__device__ __forceinline__ double bload(__amdgpu_buffer_rsrc_t r, int off_bytes) {
+    u32x2 v = __builtin_amdgcn_raw_buffer_load_b64(r, off_bytes, 0, 0);
+    return __builtin_bit_cast(double, v);
+}
+__device__ __forceinline__ void bstore(__amdgpu_buffer_rsrc_t r, int off_bytes, double d) {
+    __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(u32x2, d), r, off_bytes, 0, 0);
+}
+
+// bytes of `planes_left` padded planes of s0 doubles, clamped to 2^31-1
+__device__ __forceinline__ uint32_t plane_bytes(int64_t planes_left, int64_t s0) {
+    if (planes_left <= 0) return 0u;
+    const int64_t b = planes_left * s0 * 8;
+    return b > 0x7fffffffLL ? 0x7fffffffu : (uint32_t)b;
+}
+
 }  // namespace poms
 
 #define POMS_HIP_CHECK(expr)                                                   \

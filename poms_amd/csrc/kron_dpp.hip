@@ -1,0 +1,368 @@
+// Fused Kronecker(-sum) operator, v3: axis-2 pass in registers via DPP lane
+// shifts, one barrier per plane.
+//
+// Same operator / epilogues / axis-0 march as v1 and v2.  What changes:
+//   * lanes of a wave are 64 consecutive columns of the tile INCLUDING the
+//     2P halo columns (58 output columns per tile at P = 3); each wave loads
+//     whole 512-B rows of x straight into VGPRs (coalesced, prefetched one
+//     plane ahead) and forms the 2P shifted neighbours with v_mov_b32_dpp
+//     wave_shr:1 / wave_shl:1 -- no x tile in LDS, no LDS reads, no barrier
+//     for the axis-2 pass;
+//   * the (a, b) = (M2 x, K2 x) rows go to a DOUBLE-BUFFERED 16-B-pair LDS
+//     tile; the axis-1 pass reads it after the plane's single barrier, so the
+//     next plane's axis-2 writes never race with this plane's axis-1 reads;
+//   * axis-1 Toeplitz constants / LDS table and per-plane axis-0 scalar loads
+//     as in v2; epilogue operands issued before the prefetch; stores of
+//     invalid points dropped by the buffer range check (no branches around
+//     memory operations: exact vmcnt counting).
+// Preconditions: storage pads == P on every used axis (checked by the host).
+#include "common.hpp"
+
+namespace poms {
+
+__device__ __forceinline__ double dpp_shr1(double v) {  // lane l <- lane l-1 (lane 0 <- 0)
+    const int2 w = __builtin_bit_cast(int2, v);
+    const int lo = __builtin_amdgcn_update_dpp(0, w.x, 0x138, 0xf, 0xf, true);
+    const int hi = __builtin_amdgcn_update_dpp(0, w.y, 0x138, 0xf, 0xf, true);
+    return __builtin_bit_cast(double, make_int2(lo, hi));
+}
+__device__ __forceinline__ double dpp_shl1(double v) {  // lane l <- lane l+1 (lane 63 <- 0)
+    const int2 w = __builtin_bit_cast(int2, v);
+    const int lo = __builtin_amdgcn_update_dpp(0, w.x, 0x130, 0xf, 0xf, true);
+    const int hi = __builtin_amdgcn_update_dpp(0, w.y, 0x130, 0xf, 0xf, true);
+    return __builtin_bit_cast(double, make_int2(lo, hi));
+}
+
+template <int P, int R, int NW, bool IS3D, int FORM, int EPI>
+__global__ void __launch_bounds__(NW * 64, ((P <= 3 ? 2 : 1) * NW * 64) / 256)  // 2 WGs/CU for P <= 3
+kron_v3_kernel(const double* __restrict__ x, double* __restrict__ y,
+               const double* __restrict__ bvec,
+               const double* __restrict__ a0t, const double* __restrict__ b0t,
+               const double* __restrict__ a1, const double* __restrict__ b1,
+               const double* __restrict__ a2, const double* __restrict__ b2,
+               double* __restrict__ partial, const KronGeom g, const ToepConst tc,
+               const double omega) {
+    constexpr int W = 2 * P + 1;
+    constexpr int NT = NW * 64;
+    constexpr int TO = 64 - 2 * P;          // output columns per tile
+    constexpr int T1 = NW * R;
+    constexpr int XR = T1 + 2 * P;
+    constexpr int NRW = (XR + NW - 1) / NW;  // axis-2 rows per wave
+    constexpr int XRP = NRW * NW;            // padded row count of the LDS tile
+    constexpr bool SUM = (FORM == FORM_SUM);
+    constexpr int NS = IS3D ? W : 1;
+    typedef double d2 __attribute__((ext_vector_type(2)));
+
+    __shared__ d2 ab_[SUM ? 2 * XRP * 64 : 1];
+    __shared__ double as_[SUM ? 1 : 2 * XRP * 64];
+    __shared__ double c1a[T1 * W];
+    __shared__ double c1b[SUM ? T1 * W : 1];
+    __shared__ double red[NW];
+
+    const int tid = threadIdx.x;
+    const int lane = tid & 63;
+    const int wv = __builtin_amdgcn_readfirstlane(tid >> 6);
+
+    const int nblk = gridDim.x;
+    int bid;
+    {
+        const int b = blockIdx.x, q = nblk >> 3, rr = nblk & 7, xcd = b & 7, k = b >> 3;
+        bid = (xcd < rr ? xcd * (q + 1) : rr * (q + 1) + (xcd - rr) * q) + k;
+    }
+    const int t2 = bid % g.tiles2;
+    bid /= g.tiles2;
+    const int t1 = bid % g.tiles1;
+    const int ch = bid / g.tiles1;
+    const int c0 = t2 * TO;             // first output column of the tile
+    const int r0 = t1 * T1;
+    const int i2 = c0 - P + lane;       // this lane's column (may be a halo column)
+    const bool col_ok = lane >= P && lane < 64 - P && i2 < g.n2;
+
+    double ca2[W], cb2[W];
+    {
+        const int ic = min(max(i2, 0), g.n2 - 1);
+#pragma unroll
+        for (int k = 0; k < W; ++k) {
+            ca2[k] = a2[ic * W + k];
+            cb2[k] = SUM ? b2[ic * W + k] : 0.0;
+        }
+    }
+    const bool fast1 = (r0 >= tc.lo1) && (r0 + T1 <= tc.hi1);
+    if (!fast1) {
+        for (int e = tid; e < T1 * W; e += NT) {
+            const int rl = e / W, k = e - rl * W;
+            const int row = min(r0 + rl, g.n1 - 1);
+            c1a[e] = a1[row * W + k];
+            if constexpr (SUM) c1b[e] = b1[row * W + k];
+        }
+    }
+
+    int z0 = 0, z1 = 1;
+    if constexpr (IS3D) {
+        z0 = g.z_begin + ch * g.chunk;
+        z1 = min(z0 + g.chunk, g.z_end);
+    }
+    const int nplanes = IS3D ? (z1 - z0) + 2 * P : 1;
+    const int nsp = g.n0 + 2 * g.pd0;
+
+    // this wave's axis-2 rows: rr = wv + j*NW; storage (row, col) = (r0 + rr, c0 + lane)
+    int xoff[NRW];
+#pragma unroll
+    for (int j = 0; j < NRW; ++j) {
+        const int rr = wv + j * NW;
+        xoff[j] = rr < XR ? ((r0 + rr) * (int)g.s1 + (c0 + lane)) * 8 : 0x7ffffff0;
+    }
+    double xr[NRW];
+    auto load_plane = [&](int jj) {
+        const int sp = IS3D ? jj + g.pd0 : 0;
+        const bool ok = (sp >= 0) && (sp < nsp);
+        const __amdgpu_buffer_rsrc_t rs =
+            make_rsrc(x + (int64_t)(ok ? sp : 0) * g.s0, ok ? plane_bytes(nsp - sp, g.s0) : 0u);
+#pragma unroll
+        for (int j = 0; j < NRW; ++j) xr[j] = bload(rs, xoff[j]);
+    };
+
+    double acc[R][NS];
+#pragma unroll
+    for (int r = 0; r < R; ++r)
+#pragma unroll
+        for (int s = 0; s < NS; ++s) acc[r][s] = 0.0;
+    double nrm = 0.0;
+
+    const int obase = ((r0 + wv * R + g.pd1) * (int)g.s1 + (i2 + g.pd2)) * 8;
+    const int rowstep = (int)g.s1 * 8;
+    double eb[R], ex[R];
+    // plane-invariant factors of diag(A) for row r of this thread (recomputed
+    // per plane: cheaper than keeping 2R doubles live)
+    auto diag_parts = [&](int r, double& dX, double& dY) {
+        const double d1a = fast1 ? tc.t1a[0] : c1a[(wv * R + r) * W + P];
+        const double d1b = SUM ? (fast1 ? tc.t1b[0] : c1b[(wv * R + r) * W + P]) : 0.0;
+        if constexpr (IS3D) {
+            dX = d1a * ca2[P];
+            dY = SUM ? (d1b * ca2[P] + d1a * cb2[P]) : 0.0;
+        } else {
+            dX = SUM ? (d1a * ca2[P] + d1b * cb2[P]) : d1a * ca2[P];
+            dY = 0.0;
+        }
+    };
+    auto epi_issue = [&](int zo) {
+        if constexpr (EPI != EPI_APPLY) {
+            const int sp = zo + g.pd0;
+            const uint32_t nb = plane_bytes(nsp - sp, g.s0);
+            const __amdgpu_buffer_rsrc_t bs = make_rsrc(bvec + (int64_t)sp * g.s0, nb);
+#pragma unroll
+            for (int r = 0; r < R; ++r) eb[r] = bload(bs, obase + r * rowstep);
+            if constexpr (EPI == EPI_JACOBI) {
+                const __amdgpu_buffer_rsrc_t xsr = make_rsrc(x + (int64_t)sp * g.s0, nb);
+#pragma unroll
+                for (int r = 0; r < R; ++r) ex[r] = bload(xsr, obase + r * rowstep);
+            }
+        }
+    };
+    auto epi_finish = [&](int zo, const double* v, bool en) {
+        const int sp = zo + g.pd0;
+        const __amdgpu_buffer_rsrc_t ys = make_rsrc(y + (int64_t)sp * g.s0, plane_bytes(nsp - sp, g.s0));
+        double d0a = 1.0, d0b = 0.0;
+        if constexpr (EPI == EPI_JACOBI && IS3D) {
+            const int i0g = g.g0 + zo;
+            d0a = a0t[(i0g + P) * W + P];
+            if constexpr (SUM) d0b = b0t[(i0g + P) * W + P];
+        }
+#pragma unroll
+        for (int r = 0; r < R; ++r) {
+            const bool ok = en && col_ok && (r0 + wv * R + r < g.n1);
+            double outv;
+            if constexpr (EPI == EPI_APPLY) {
+                outv = v[r];
+            } else if constexpr (EPI == EPI_RESID) {
+                outv = eb[r] - v[r];
+            } else {
+                double dX, dY;
+                diag_parts(r, dX, dY);
+                const double diag = IS3D ? fma(d0a, dX, d0b * dY) : dX;
+                double rc = __builtin_amdgcn_rcp(diag);
+                double e = fma(-diag, rc, 1.0);
+                rc = fma(rc, e, rc);
+                e = fma(-diag, rc, 1.0);
+                rc = fma(rc, e, rc);
+                const double dr = omega * (eb[r] - v[r]) * rc;
+                outv = ex[r] + dr;
+                nrm = ok ? fma(dr, dr, nrm) : nrm;
+            }
+            bstore(ys, ok ? obase + r * rowstep : 0x7ffffff0, outv);
+        }
+    };
+
+    load_plane(IS3D ? z0 - P : 0);
+    __syncthreads();  // c1a/c1b visible
+
+    for (int tb = 0; tb < nplanes; tb += NS) {
+#pragma unroll
+        for (int q = 0; q < NS; ++q) {
+            const int t = tb + q;
+            if (t < nplanes) {
+                const int buf = (t & 1) * XRP * 64;
+                // ---- axis 2 in registers: DPP shifts of whole rows
+#pragma unroll
+                for (int j = 0; j < NRW; ++j) {
+                    double sh[W];
+                    sh[P] = xr[j];
+#pragma unroll
+                    for (int d = 1; d <= P; ++d) {
+                        sh[P - d] = dpp_shr1(sh[P - d + 1]);  // column i2 - d
+                        sh[P + d] = dpp_shl1(sh[P + d - 1]);  // column i2 + d
+                    }
+                    double sa = ca2[0] * sh[0];
+                    double sb = SUM ? cb2[0] * sh[0] : 0.0;
+#pragma unroll
+                    for (int k = 1; k < W; ++k) {
+                        sa = fma(ca2[k], sh[k], sa);
+                        if constexpr (SUM) sb = fma(cb2[k], sh[k], sb);
+                    }
+                    const int rr = wv + j * NW;
+                    if constexpr (SUM) {
+                        d2 pr;
+                        pr.x = sa;
+                        pr.y = sb;
+                        ab_[buf + rr * 64 + lane] = pr;
+                    } else {
+                        as_[buf + rr * 64 + lane] = sa;
+                    }
+                }
+                // ---- loads for the rest of the iteration / the next plane
+                epi_issue(IS3D ? max(z0 - 2 * P + t, z0) : 0);
+                if constexpr (IS3D) load_plane(t + 1 < nplanes ? z0 - P + t + 1 : -(1 << 20));
+                __syncthreads();
+
+                // ---- axis 1 from the LDS tile
+                double cv[R], dv[R];
+#pragma unroll
+                for (int r = 0; r < R; ++r) { cv[r] = 0.0; dv[r] = 0.0; }
+                auto axis1 = [&](auto coef) {
+#pragma unroll
+                    for (int qq = 0; qq < R + 2 * P; ++qq) {
+                        const int rr = wv * R + qq;
+                        double va, vb = 0.0;
+                        if constexpr (SUM) {
+                            const d2 pr = ab_[buf + rr * 64 + lane];
+                            va = pr.x;
+                            vb = pr.y;
+                        } else {
+                            va = as_[buf + rr * 64 + lane];
+                        }
+#pragma unroll
+                        for (int r = 0; r < R; ++r) {
+                            const int k = qq - r;
+                            if (k >= 0 && k < W) {
+                                double ca, cb;
+                                coef(r, k, ca, cb);
+                                cv[r] = fma(ca, va, cv[r]);
+                                if constexpr (SUM) {
+                                    if constexpr (IS3D) dv[r] = fma(cb, va, fma(ca, vb, dv[r]));
+                                    else cv[r] = fma(cb, vb, cv[r]);
+                                }
+                            }
+                        }
+                    }
+                };
+                if (fast1) {
+                    axis1([&](int, int k, double& ca, double& cb) {
+                        const int jj = k < P ? P - k : k - P;
+                        ca = tc.t1a[jj];
+                        cb = SUM ? tc.t1b[jj] : 0.0;
+                    });
+                } else {
+                    axis1([&](int r, int k, double& ca, double& cb) {
+                        ca = c1a[(wv * R + r) * W + k];
+                        cb = SUM ? c1b[(wv * R + r) * W + k] : 0.0;
+                    });
+                }
+
+                if constexpr (IS3D) {
+                    // ---- axis 0: scatter into rotating slots
+                    const int jrow = (g.g0 + z0 - P + t + P) * W;
+#pragma unroll
+                    for (int s = 0; s < W; ++s) {
+                        const int slot = (q - P + s + NS) % NS;
+                        const double ka = a0t[jrow + s];
+                        const double kb = SUM ? b0t[jrow + s] : 0.0;
+#pragma unroll
+                        for (int r = 0; r < R; ++r) {
+                            acc[r][slot] = fma(ka, cv[r], acc[r][slot]);
+                            if constexpr (SUM) acc[r][slot] = fma(kb, dv[r], acc[r][slot]);
+                        }
+                    }
+                    const int done = (q + P + 1) % NS;
+                    double vv[R];
+#pragma unroll
+                    for (int r = 0; r < R; ++r) vv[r] = acc[r][done];
+                    epi_finish(max(z0 - 2 * P + t, z0), vv, t >= 2 * P);
+#pragma unroll
+                    for (int r = 0; r < R; ++r) acc[r][done] = 0.0;
+                } else {
+                    epi_finish(0, cv, true);
+                }
+            }
+        }
+    }
+
+    if constexpr (EPI == EPI_JACOBI) {
+        if (partial != nullptr) {
+#pragma unroll
+            for (int off = 32; off > 0; off >>= 1) nrm += __shfl_xor(nrm, off, 64);
+            if (lane == 0) red[wv] = nrm;
+            __syncthreads();
+            if (tid == 0) {
+                double s = 0.0;
+                for (int w = 0; w < NW; ++w) s += red[w];
+                partial[blockIdx.x] = s;
+            }
+        }
+    }
+}
+
+template <int P, int R, int NW, bool IS3D, int FORM, int EPI>
+static void v3_launch_t(const KronPtrs& p, const KronGeom& g, const ToepConst& tc, double omega,
+                        hipStream_t st) {
+    const int nblk = g.tiles2 * g.tiles1 * g.nchunks;
+    hipLaunchKernelGGL((kron_v3_kernel<P, R, NW, IS3D, FORM, EPI>), dim3(nblk), dim3(NW * 64), 0, st,
+                       p.x, p.y, p.b, p.a0t, p.b0t, p.a1, p.b1, p.a2, p.b2, p.partial, g, tc, omega);
+}
+
+template <int P, int R, int NW, bool IS3D, int FORM>
+static int v3_launch_e(int epi, const KronPtrs& p, const KronGeom& g, const ToepConst& tc,
+                       double omega, hipStream_t st) {
+    switch (epi) {
+        case EPI_APPLY: v3_launch_t<P, R, NW, IS3D, FORM, EPI_APPLY>(p, g, tc, omega, st); return 0;
+        case EPI_RESID: v3_launch_t<P, R, NW, IS3D, FORM, EPI_RESID>(p, g, tc, omega, st); return 0;
+        case EPI_JACOBI: v3_launch_t<P, R, NW, IS3D, FORM, EPI_JACOBI>(p, g, tc, omega, st); return 0;
+    }
+    return 1;
+}
+
+template <int P, int R, int NW>
+static int v3_launch_p(bool is3d, int form, int epi, const KronPtrs& p, const KronGeom& g,
+                       const ToepConst& tc, double omega, hipStream_t st) {
+    if (is3d)
+        return form == FORM_SUM ? v3_launch_e<P, R, NW, true, FORM_SUM>(epi, p, g, tc, omega, st)
+                                : v3_launch_e<P, R, NW, true, FORM_SINGLE>(epi, p, g, tc, omega, st);
+    return form == FORM_SUM ? v3_launch_e<P, R, NW, false, FORM_SUM>(epi, p, g, tc, omega, st)
+                            : v3_launch_e<P, R, NW, false, FORM_SINGLE>(epi, p, g, tc, omega, st);
+}
+
+// variant 4: 8 waves x 2 rows (16 x (64-2P) tile)
+int kron_v3_launch(int variant, int pmax, bool is3d, int form, int epi, const KronPtrs& p,
+                   const KronGeom& g, const ToepConst& tc, double omega, hipStream_t st) {
+    (void)variant;
+    switch (pmax) {
+        case 1: return v3_launch_p<1, 2, 8>(is3d, form, epi, p, g, tc, omega, st);
+        case 2: return v3_launch_p<2, 2, 8>(is3d, form, epi, p, g, tc, omega, st);
+        case 3: return v3_launch_p<3, 2, 8>(is3d, form, epi, p, g, tc, omega, st);
+        case 4: return v3_launch_p<4, 2, 8>(is3d, form, epi, p, g, tc, omega, st);
+        case 5: return v3_launch_p<5, 2, 8>(is3d, form, epi, p, g, tc, omega, st);
+    }
+    set_error("pmax must be in 1..5");
+    return 1;
+}
+
+}  // namespace poms

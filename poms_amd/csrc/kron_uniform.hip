@@ -20,26 +20,6 @@
 
 namespace poms {
 
-typedef unsigned int u32x2 __attribute__((ext_vector_type(2)));
-
-__device__ __forceinline__ __amdgpu_buffer_rsrc_t make_rsrc(const void* base, uint32_t bytes) {
-    return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(base), (short)0, (int)bytes, 0x00020000);
-}
-__device__ __forceinline__ double bload(__amdgpu_buffer_rsrc_t r, int off_bytes) {
-    u32x2 v = __builtin_amdgcn_raw_buffer_load_b64(r, off_bytes, 0, 0);
-    return __builtin_bit_cast(double, v);
-}
-__device__ __forceinline__ void bstore(__amdgpu_buffer_rsrc_t r, int off_bytes, double d) {
-    __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(u32x2, d), r, off_bytes, 0, 0);
-}
-
-// bytes of `planes_left` padded planes of s0 doubles, clamped to 2^31-1
-__device__ __forceinline__ uint32_t plane_bytes(int64_t planes_left, int64_t s0) {
-    if (planes_left <= 0) return 0u;
-    const int64_t b = planes_left * s0 * 8;
-    return b > 0x7fffffffLL ? 0x7fffffffu : (uint32_t)b;
-}
-
 // STAMPS: diagnostic build only -- per-wave cycle shares of the plane-loop
 // phases (s_memtime), written to `dbg`; never used for timing claims.
 template <int P, int R, int NW, bool IS3D, int FORM, int EPI, bool STAMPS = false>
@@ -62,9 +42,11 @@ kron_v2_kernel(const double* __restrict__ x, double* __restrict__ y,
     constexpr bool SUM = (FORM == FORM_SUM);
     constexpr int NS = IS3D ? W : 1;
 
-    __shared__ double xs[NX];
-    __shared__ double as_[XR * T2];
-    __shared__ double bs_[SUM ? XR * T2 : 1];
+    __shared__ double xs[NLD * NT];             // padded: every thread stores NLD values
+    typedef double d2 __attribute__((ext_vector_type(2)));
+    // axis-2 results: (a, b) interleaved as 16-byte pairs (one b128 write / read)
+    __shared__ d2 ab_[SUM ? XR * T2 : 1];
+    __shared__ double as_[SUM ? 1 : XR * T2];
     __shared__ double c1a[T1 * W];               // general axis-1 rows of this tile
     __shared__ double c1b[SUM ? T1 * W : 1];
     __shared__ double red[NW];
@@ -164,7 +146,7 @@ kron_v2_kernel(const double* __restrict__ x, double* __restrict__ y,
             }
         }
     };
-    auto epi_finish = [&](int zo, const double* v) {
+    auto epi_finish = [&](int zo, const double* v, bool en) {
         const int sp = zo + g.pd0;
         const __amdgpu_buffer_rsrc_t ys = make_rsrc(y + (int64_t)sp * g.s0, plane_bytes(nsp - sp, g.s0));
         double d0a = 1.0, d0b = 0.0;
@@ -190,10 +172,13 @@ kron_v2_kernel(const double* __restrict__ x, double* __restrict__ y,
                 rc = fma(rc, e, rc);
                 const double dr = omega * (eb[r] - v[r]) * rc;
                 outv = ex[r] + dr;
-                const bool ok = col_ok && (r0 + wv * R + r < g.n1);
+                const bool ok = en && col_ok && (r0 + wv * R + r < g.n1);
                 nrm = ok ? fma(dr, dr, nrm) : nrm;
             }
-            if (col_ok && (r0 + wv * R + r < g.n1)) bstore(ys, obase_inplane + r * rowstep, outv);
+            // invalid points: out-of-range offset, the store is dropped by the
+            // buffer range check (no branch, no exec-mask region)
+            const bool ok = en && col_ok && (r0 + wv * R + r < g.n1);
+            bstore(ys, ok ? obase_inplane + r * rowstep : 0x7ffffff0, outv);
         }
     };
 
@@ -231,15 +216,13 @@ kron_v2_kernel(const double* __restrict__ x, double* __restrict__ y,
             const int t = tb + q;
             if (t < nplanes) {
 #pragma unroll
-                for (int l = 0; l < NLD; ++l) {
-                    const int e = tid + l * NT;
-                    if (NX % NT == 0 || e < NX) xs[e] = xr[l];
-                }
+                for (int l = 0; l < NLD; ++l) xs[tid + l * NT] = xr[l];
                 POMS_STAMP(0)
                 __syncthreads();
                 POMS_STAMP(1)
-                if (!IS3D || t >= 2 * P) epi_issue(IS3D ? z0 - 2 * P + t : 0);
-                if (IS3D && t + 1 < nplanes) load_plane(z0 - P + t + 1);
+                // unconditional memory ops (no branch around loads: exact vmcnt counts)
+                epi_issue(IS3D ? max(z0 - 2 * P + t, z0) : 0);
+                if constexpr (IS3D) load_plane(t + 1 < nplanes ? z0 - P + t + 1 : -(1 << 20));
                 POMS_STAMP(2)
 
                 // ---- axis 2 (LDS -> LDS)
@@ -257,8 +240,14 @@ kron_v2_kernel(const double* __restrict__ x, double* __restrict__ y,
                             sa = fma(ca2[k], v, sa);
                             if constexpr (SUM) sb = fma(cb2[k], v, sb);
                         }
-                        as_[rr * T2 + lane] = sa;
-                        if constexpr (SUM) bs_[rr * T2 + lane] = sb;
+                        if constexpr (SUM) {
+                            d2 pr;
+                            pr.x = sa;
+                            pr.y = sb;
+                            ab_[rr * T2 + lane] = pr;
+                        } else {
+                            as_[rr * T2 + lane] = sa;
+                        }
                     }
                 }
                 POMS_STAMP(3)
@@ -273,8 +262,14 @@ kron_v2_kernel(const double* __restrict__ x, double* __restrict__ y,
 #pragma unroll
                     for (int qq = 0; qq < R + 2 * P; ++qq) {
                         const int rr = wv * R + qq;
-                        const double va = as_[rr * T2 + lane];
-                        const double vb = SUM ? bs_[rr * T2 + lane] : 0.0;
+                        double va, vb = 0.0;
+                        if constexpr (SUM) {
+                            const d2 pr = ab_[rr * T2 + lane];
+                            va = pr.x;
+                            vb = pr.y;
+                        } else {
+                            va = as_[rr * T2 + lane];
+                        }
 #pragma unroll
                         for (int r = 0; r < R; ++r) {
                             const int k = qq - r;
@@ -292,8 +287,14 @@ kron_v2_kernel(const double* __restrict__ x, double* __restrict__ y,
 #pragma unroll
                     for (int qq = 0; qq < R + 2 * P; ++qq) {
                         const int rr = wv * R + qq;
-                        const double va = as_[rr * T2 + lane];
-                        const double vb = SUM ? bs_[rr * T2 + lane] : 0.0;
+                        double va, vb = 0.0;
+                        if constexpr (SUM) {
+                            const d2 pr = ab_[rr * T2 + lane];
+                            va = pr.x;
+                            vb = pr.y;
+                        } else {
+                            va = as_[rr * T2 + lane];
+                        }
 #pragma unroll
                         for (int r = 0; r < R; ++r) {
                             const int k = qq - r;
@@ -327,17 +328,17 @@ kron_v2_kernel(const double* __restrict__ x, double* __restrict__ y,
                     }
                     const int done = (q + P + 1) % NS;
                     POMS_STAMP(6)
-                    if (t >= 2 * P) {
+                    {
                         double vv[R];
 #pragma unroll
                         for (int r = 0; r < R; ++r) vv[r] = acc[r][done];
-                        epi_finish(z0 - 2 * P + t, vv);
+                        epi_finish(max(z0 - 2 * P + t, z0), vv, t >= 2 * P);
                     }
                     POMS_STAMP(7)
 #pragma unroll
                     for (int r = 0; r < R; ++r) acc[r][done] = 0.0;
                 } else {
-                    epi_finish(0, cv);
+                    epi_finish(0, cv, true);
                 }
             }
         }

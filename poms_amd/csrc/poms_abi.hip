@@ -15,6 +15,8 @@ int kron_launch(int pmax, bool is3d, int form, int epi, const KronPtrs& p, const
                 double omega, hipStream_t st);
 int kron_v2_launch(int variant, int pmax, bool is3d, int form, int epi, const KronPtrs& p,
                    const KronGeom& g, const ToepConst& tc, double omega, hipStream_t st);
+int kron_v3_launch(int variant, int pmax, bool is3d, int form, int epi, const KronPtrs& p,
+                   const KronGeom& g, const ToepConst& tc, double omega, hipStream_t st);
 int kron_v2_stamps(int variant, int epi, const KronPtrs& p, const KronGeom& g, const ToepConst& tc,
                    double omega, unsigned long long* dbg, hipStream_t st);
 int kron_tile_rows();
@@ -229,7 +231,7 @@ int poms_op_create(poms_ctx* ctx, int ndim, const poms_layout* layout, int form,
     if (is3d)
         toeplitz_range(f[0], sum ? f[1] : nullptr, n0_global, pmax, &o->tc.lo0, &o->tc.hi0, o->tc.t0a, o->tc.t0b);
     toeplitz_range(f[2], sum ? f[3] : nullptr, layout->n[1], pmax, &o->tc.lo1, &o->tc.hi1, o->tc.t1a, o->tc.t1b);
-    o->variant = o->v2_ok ? 1 : 0;
+    o->variant = o->v2_ok ? 4 : 0;
     *op = o;
     return 0;
 }
@@ -243,7 +245,7 @@ int poms_op_destroy(poms_op* o) {
 }
 
 int poms_op_set_variant(poms_op* op, int variant) {
-    if (!op || variant < 0 || variant > 3) { set_error("poms_op_set_variant: bad argument"); return 1; }
+    if (!op || variant < 0 || variant > 4) { set_error("poms_op_set_variant: bad argument"); return 1; }
     if (variant > 0 && !op->v2_ok) { set_error("poms_op_set_variant: variant needs pads == pmax"); return 1; }
     op->variant = variant;
     return 0;
@@ -272,6 +274,7 @@ static int op_geom(poms_op* o, int64_t zb, int64_t ze, KronGeom& g) {
     g.tiles2 = (int)((o->L.n[2] + kron_tile_cols() - 1) / kron_tile_cols());
     const int trows = o->variant == 3 ? 32 : kron_tile_rows();
     g.tiles1 = (int)((o->L.n[1] + trows - 1) / trows);
+    if (o->variant == 4) g.tiles2 = (int)((o->L.n[2] + (64 - 2 * o->pmax) - 1) / (64 - 2 * o->pmax));
     if (!is3d) {
         g.z_begin = 0; g.z_end = 1; g.chunk = 1; g.nchunks = 1;
         return 0;
@@ -305,6 +308,8 @@ static int op_run(poms_op* o, int epi, double omega, const double* x, double* y,
                want_norm ? o->ctx->scratch : nullptr};
     const int rc = o->variant == 0
         ? kron_launch(o->pmax, o->ndim == 3, o->form, epi, p, g, omega, as_stream(stream))
+        : o->variant == 4
+        ? kron_v3_launch(o->variant, o->pmax, o->ndim == 3, o->form, epi, p, g, o->tc, omega, as_stream(stream))
         : kron_v2_launch(o->variant, o->pmax, o->ndim == 3, o->form, epi, p, g, o->tc, omega, as_stream(stream));
     if (rc) return 1;
     POMS_HIP_CHECK(hipGetLastError());

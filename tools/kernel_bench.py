@@ -56,7 +56,8 @@ def main():
                 if var is not None:
                     A.set_variant(var)
                 for kind in kinds:
-                    fn = {"apply": lambda: A.dot(x, out=y),
+                    fn = {"dot": lambda: x.dot(b),
+                          "apply": lambda: A.dot(x, out=y),
                           "residual": lambda: A.residual(b, x, out=y),
                           "jacobi": lambda: A.jacobi_sweep(b, x, y, 2.0 / 3.0, want_norm=False)}[kind]
                     for _ in range(2):
@@ -72,7 +73,7 @@ def main():
     out = []
     for (ch, var, kind), ts in res.items():
         med = statistics.median(ts)
-        bpd = 16 if kind == "apply" else 24
+        bpd = 16 if kind in ("apply", "dot") else 24
         row = {"chunk": ch, "variant": var, "kind": kind, "median_us": med, "min_us": min(ts),
                "GBps": bpd * dof / med / 1e3, "GDOFps": dof / med / 1e3}
         out.append(row)
