@@ -48,12 +48,17 @@ kron_v3_kernel(const double* __restrict__ x, double* __restrict__ y,
     constexpr int T1 = NW * R;
     constexpr int XR = T1 + 2 * P;
     constexpr int NRW = (XR + NW - 1) / NW;  // axis-2 rows per wave
-    constexpr int XRP = NRW * NW;            // padded row count of the LDS tile
+    constexpr int XRP = XR;                  // rows of the LDS (a, b) tile
     constexpr bool SUM = (FORM == FORM_SUM);
     constexpr int NS = IS3D ? W : 1;
     typedef double d2 __attribute__((ext_vector_type(2)));
 
+    constexpr bool XRING = (EPI == EPI_JACOBI) && IS3D;
+    constexpr int NRING = P + 1;            // x planes kept for the Jacobi update
     __shared__ d2 ab_[SUM ? 2 * XRP * 64 : 1];
+    // x of the tile's output rows for the last P+1 planes (the Jacobi epilogue's
+    // x_in): re-reading it from HBM P planes later costs 8 B/DOF (L2-evicted)
+    __shared__ double xring[XRING ? NRING * T1 * 64 : 1];
     __shared__ double as_[SUM ? 1 : 2 * XRP * 64];
     __shared__ double c1a[T1 * W];
     __shared__ double c1b[SUM ? T1 * W : 1];
@@ -152,7 +157,7 @@ kron_v3_kernel(const double* __restrict__ x, double* __restrict__ y,
             const __amdgpu_buffer_rsrc_t bs = make_rsrc(bvec + (int64_t)sp * g.s0, nb);
 #pragma unroll
             for (int r = 0; r < R; ++r) eb[r] = bload(bs, obase + r * rowstep);
-            if constexpr (EPI == EPI_JACOBI) {
+            if constexpr (EPI == EPI_JACOBI && !XRING) {
                 const __amdgpu_buffer_rsrc_t xsr = make_rsrc(x + (int64_t)sp * g.s0, nb);
 #pragma unroll
                 for (int r = 0; r < R; ++r) ex[r] = bload(xsr, obase + r * rowstep);
@@ -220,17 +225,32 @@ kron_v3_kernel(const double* __restrict__ x, double* __restrict__ y,
                         if constexpr (SUM) sb = fma(cb2[k], sh[k], sb);
                     }
                     const int rr = wv + j * NW;
-                    if constexpr (SUM) {
-                        d2 pr;
-                        pr.x = sa;
-                        pr.y = sb;
-                        ab_[buf + rr * 64 + lane] = pr;
-                    } else {
-                        as_[buf + rr * 64 + lane] = sa;
+                    if constexpr (XRING) {
+                        const int orow = rr - P;   // output row of this tile row, if any
+                        if (orow >= 0 && orow < T1)
+                            xring[(((t + NRING) % NRING) * T1 + orow) * 64 + lane] = xr[j];
+                    }
+                    if (XR % NW == 0 || rr < XR) {
+                        if constexpr (SUM) {
+                            d2 pr;
+                            pr.x = sa;
+                            pr.y = sb;
+                            ab_[buf + rr * 64 + lane] = pr;
+                        } else {
+                            as_[buf + rr * 64 + lane] = sa;
+                        }
                     }
                 }
                 // ---- loads for the rest of the iteration / the next plane
                 epi_issue(IS3D ? max(z0 - 2 * P + t, z0) : 0);
+                if constexpr (XRING) {
+                    // x_in of this iteration's output plane (input plane t-P): read
+                    // BEFORE the barrier -- its slot is rewritten by iteration t+1's
+                    // axis-2 pass, which runs after this barrier.
+                    const int slot = (t - P + NRING) % NRING;
+#pragma unroll
+                    for (int r = 0; r < R; ++r) ex[r] = xring[(slot * T1 + wv * R + r) * 64 + lane];
+                }
                 if constexpr (IS3D) load_plane(t + 1 < nplanes ? z0 - P + t + 1 : -(1 << 20));
                 __syncthreads();
 

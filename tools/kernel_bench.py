@@ -64,10 +64,18 @@ def main():
                         fn()
                     torch.cuda.synchronize()
                     A.timer = []
+                    ev = []
                     for _ in range(a.reps):
+                        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                        e0.record()
                         fn()
+                        e1.record()
+                        ev.append((e0, e1))
                     torch.cuda.synchronize()
-                    ts = [e0.elapsed_time(e1) * 1e3 for _, e0, e1 in A.timer]
+                    if A.timer:   # per-launch kernel events (operator kinds)
+                        ts = [e0.elapsed_time(e1) * 1e3 for _, e0, e1 in A.timer]
+                    else:         # whole call (dot includes its reduction + host read)
+                        ts = [e0.elapsed_time(e1) * 1e3 for e0, e1 in ev]
                     A.timer = None
                     res.setdefault((ch, var, kind), []).extend(ts)
     out = []
