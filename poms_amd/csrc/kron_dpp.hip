@@ -34,7 +34,7 @@ __device__ __forceinline__ double dpp_shl1(double v) {  // lane l <- lane l+1 (l
 }
 
 template <int P, int R, int NW, bool IS3D, int FORM, int EPI>
-__global__ void __launch_bounds__(NW * 64, ((P <= 3 ? 2 : 1) * NW * 64) / 256)  // 2 WGs/CU for P <= 3
+__global__ void __launch_bounds__(NW * 64, ((P <= 3 && NW <= 8 ? 2 : 1) * NW * 64) / 256)  // 16 waves/CU for P <= 3
 kron_v3_kernel(const double* __restrict__ x, double* __restrict__ y,
                const double* __restrict__ bvec,
                const double* __restrict__ a0t, const double* __restrict__ b0t,
@@ -370,10 +370,18 @@ static int v3_launch_p(bool is3d, int form, int epi, const KronPtrs& p, const Kr
                             : v3_launch_e<P, R, NW, false, FORM_SINGLE>(epi, p, g, tc, omega, st);
 }
 
-// variant 4: 8 waves x 2 rows (16 x (64-2P) tile)
+// variant 4: 8 waves x 2 rows (16 x (64-2P) tile, 2 WGs/CU);
+// variant 5: 16 waves x 2 rows (32 x (64-2P) tile, 1 WG/CU, less halo recompute)
 int kron_v3_launch(int variant, int pmax, bool is3d, int form, int epi, const KronPtrs& p,
                    const KronGeom& g, const ToepConst& tc, double omega, hipStream_t st) {
-    (void)variant;
+    if (variant == 5) {
+        switch (pmax) {
+            case 1: return v3_launch_p<1, 2, 16>(is3d, form, epi, p, g, tc, omega, st);
+            case 2: return v3_launch_p<2, 2, 16>(is3d, form, epi, p, g, tc, omega, st);
+            case 3: return v3_launch_p<3, 2, 16>(is3d, form, epi, p, g, tc, omega, st);
+            default: break;  // P >= 4: the 32-row tile exceeds the LDS budget
+        }
+    }
     switch (pmax) {
         case 1: return v3_launch_p<1, 2, 8>(is3d, form, epi, p, g, tc, omega, st);
         case 2: return v3_launch_p<2, 2, 8>(is3d, form, epi, p, g, tc, omega, st);

@@ -245,8 +245,9 @@ int poms_op_destroy(poms_op* o) {
 }
 
 int poms_op_set_variant(poms_op* op, int variant) {
-    if (!op || variant < 0 || variant > 4) { set_error("poms_op_set_variant: bad argument"); return 1; }
+    if (!op || variant < 0 || variant > 5) { set_error("poms_op_set_variant: bad argument"); return 1; }
     if (variant > 0 && !op->v2_ok) { set_error("poms_op_set_variant: variant needs pads == pmax"); return 1; }
+    if (variant == 5 && op->pmax > 3) variant = 4;  // 32-row tile does not fit LDS at p >= 4
     op->variant = variant;
     return 0;
 }
@@ -272,9 +273,9 @@ static int op_geom(poms_op* o, int64_t zb, int64_t ze, KronGeom& g) {
     g.pd0 = r.pd0; g.pd1 = r.pd1; g.pd2 = r.pd2;
     g.g0 = (int)o->g0;
     g.tiles2 = (int)((o->L.n[2] + kron_tile_cols() - 1) / kron_tile_cols());
-    const int trows = o->variant == 3 ? 32 : kron_tile_rows();
+    const int trows = (o->variant == 3 || o->variant == 5) ? 32 : kron_tile_rows();
     g.tiles1 = (int)((o->L.n[1] + trows - 1) / trows);
-    if (o->variant == 4) g.tiles2 = (int)((o->L.n[2] + (64 - 2 * o->pmax) - 1) / (64 - 2 * o->pmax));
+    if (o->variant >= 4) g.tiles2 = (int)((o->L.n[2] + (64 - 2 * o->pmax) - 1) / (64 - 2 * o->pmax));
     if (!is3d) {
         g.z_begin = 0; g.z_end = 1; g.chunk = 1; g.nchunks = 1;
         return 0;
@@ -308,7 +309,7 @@ static int op_run(poms_op* o, int epi, double omega, const double* x, double* y,
                want_norm ? o->ctx->scratch : nullptr};
     const int rc = o->variant == 0
         ? kron_launch(o->pmax, o->ndim == 3, o->form, epi, p, g, omega, as_stream(stream))
-        : o->variant == 4
+        : o->variant >= 4
         ? kron_v3_launch(o->variant, o->pmax, o->ndim == 3, o->form, epi, p, g, o->tc, omega, as_stream(stream))
         : kron_v2_launch(o->variant, o->pmax, o->ndim == 3, o->form, epi, p, g, o->tc, omega, as_stream(stream));
     if (rc) return 1;
