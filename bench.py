@@ -43,7 +43,8 @@ def parse():
     ap.add_argument("--coarse", type=int, default=8)
     ap.add_argument("--chunk", type=int, default=0)
     ap.add_argument("--kron-reps", type=int, default=20)
-    ap.add_argument("--cpu-cells", type=int, default=96)
+    ap.add_argument("--cpu-cells", type=int, default=160)
+    ap.add_argument("--cpu-cycles", type=int, default=3)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--pmc-json", type=str, default="",
                     help="rocprofv3 PMC summary (bytes per launch) to fill roofline.traffic")
@@ -140,11 +141,11 @@ def main():
         try:
             from oracle import cpu_baseline as cb
             threads = min(16, os.cpu_count() or 1)
-            r = cb.time_vcycle(N=args.cpu_cells, p=args.p, Nc=args.coarse, cycles=1, threads=threads)
+            r = cb.time_vcycle(N=args.cpu_cells, p=args.p, Nc=args.coarse, cycles=args.cpu_cycles, threads=threads)
             cpu = {"value": r["dof_per_s"], "unit": "DOF/s", "cores": r["threads"], "kind": "port",
-                   "sample": (f"one full two-level V-cycle (same schedule) at {args.cpu_cells}^3 cells p={args.p} "
-                              f"({r['dof']} DOF), C/OpenMP restatement of the reference loop nests "
-                              f"(oracle/kron_cpu.c), {r['seconds_per_cycle']:.2f} s")}
+                   "sample": (f"{args.cpu_cycles} full two-level V-cycles (same schedule) at {args.cpu_cells}^3 "
+                              f"cells p={args.p} ({r['dof']} DOF), C/OpenMP restatement of the reference loop "
+                              f"nests (oracle/kron_cpu.c), {r['seconds_per_cycle']:.2f} s per cycle")}
         except Exception as e:  # baseline is informative only
             cpu = {"value": None, "unit": "DOF/s", "cores": 0, "kind": "port", "sample": f"failed: {e!r}"}
 
@@ -170,7 +171,7 @@ def main():
                 "parallelism": f"slab{world}",
             },
             "roofline": {
-                "kernel": "kron_fused_kernel<P=3,3D,SUM,JACOBI> (Kron apply + damped-Jacobi update)",
+                "kernel": f"kron_v3_kernel<P={args.p},3D,SUM,JACOBI> (variant {A.variant}: Kron apply + damped-Jacobi update)",
                 "bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBPS, "unit": "GB/s",
                 "frac": achieved / HBM_PEAK_GBPS, "traffic": traffic,
                 "algorithmic_bytes_per_launch": bytes_sweep, "avg_launch_us": sweep_s * 1e6,
