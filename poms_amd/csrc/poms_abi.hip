@@ -52,6 +52,7 @@ struct poms_op {
     int64_t g0 = 0, n0g = 1;
     double *a0t = nullptr, *b0t = nullptr, *a1 = nullptr, *b1 = nullptr, *a2 = nullptr, *b2 = nullptr;
     int64_t last_partials = 0;
+    double *dg2a = nullptr, *dg2b = nullptr;  // contiguous axis-2 band diagonals
     int variant = 0;
     bool v2_ok = false;
     ToepConst tc{};
@@ -225,6 +226,15 @@ int poms_op_create(poms_ctx* ctx, int ndim, const poms_layout* layout, int form,
         rc |= upload(f[3], (size_t)layout->n[1] * W, &o->b1);
         rc |= upload(f[5], (size_t)layout->n[2] * W, &o->b2);
     }
+    {
+        std::vector<double> da(layout->n[2]), db(layout->n[2], 0.0);
+        for (int64_t c = 0; c < layout->n[2]; ++c) {
+            da[c] = f[4][c * W + pmax];
+            if (sum) db[c] = f[5][c * W + pmax];
+        }
+        rc |= upload(da.data(), da.size(), &o->dg2a);
+        rc |= upload(db.data(), db.size(), &o->dg2b);
+    }
     if (rc) { poms_op_destroy(o); return 1; }
     // v2 preconditions: storage pads == pmax on the used axes
     o->v2_ok = layout->pads[1] == pmax && layout->pads[2] == pmax && (!is3d || layout->pads[0] == pmax);
@@ -238,7 +248,7 @@ int poms_op_create(poms_ctx* ctx, int ndim, const poms_layout* layout, int form,
 
 int poms_op_destroy(poms_op* o) {
     if (!o) return 0;
-    for (double* p : {o->a0t, o->b0t, o->a1, o->b1, o->a2, o->b2})
+    for (double* p : {o->a0t, o->b0t, o->a1, o->b1, o->a2, o->b2, o->dg2a, o->dg2b})
         if (p) (void)hipFree(p);
     delete o;
     return 0;
@@ -339,7 +349,7 @@ int poms_op_diag_scale(poms_op* o, double scale, const double* b, double* x, int
     const RowGeom g = row_geom(&o->L);
     int nb = 0;
     diag_scale_launch(o->ndim == 3, o->form, g, o->pmax, (int)o->g0, scale, b, x, o->a0t, o->b0t,
-                      o->a1, o->b1, o->a2, o->b2, want_norm ? o->ctx->scratch : nullptr,
+                      o->a1, o->b1, o->dg2a, o->dg2b, want_norm ? o->ctx->scratch : nullptr,
                       as_stream(stream), &nb);
     POMS_HIP_CHECK(hipGetLastError());
     o->last_partials = want_norm ? nb : 0;

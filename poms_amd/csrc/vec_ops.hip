@@ -62,15 +62,17 @@ reduce_partials_kernel(const double* __restrict__ partial, int count, double* __
     if (threadIdx.x == 0) out[0] = t;
 }
 
-// x = scale * b / diag(A), optional ||x||^2 partials.  diag from the 1D band
-// diagonals exactly as in kron_fused_kernel's JACOBI epilogue.
+// x = scale * b / diag(A), optional ||x||^2 partials.  diag(A) from the 1D
+// band diagonals exactly as in the fused kernels' JACOBI epilogue; the
+// axis-2 diagonals come as contiguous arrays (dg2a, dg2b) so the loads are
+// coalesced, and 1/diag is v_rcp_f64 + two Newton steps.
 template <bool IS3D, int FORM>
 __global__ void __launch_bounds__(256)
 diag_scale_kernel(const RowGeom g, const int P, const int g0, const double scale,
                   const double* __restrict__ bvec, double* __restrict__ xout,
                   const double* __restrict__ a0t, const double* __restrict__ b0t,
                   const double* __restrict__ a1, const double* __restrict__ b1,
-                  const double* __restrict__ a2, const double* __restrict__ b2,
+                  const double* __restrict__ dg2a, const double* __restrict__ dg2b,
                   double* __restrict__ partial) {
     __shared__ double red[4];
     const int W = 2 * P + 1;
@@ -90,16 +92,21 @@ diag_scale_kernel(const RowGeom g, const int P, const int g0, const double scale
             if constexpr (FORM == FORM_SUM) d0b = b0t[(g0 + i0 + P) * W + P];
         }
         for (int c = lane; c < g.n2; c += 64) {
-            const double d2a = a2[c * W + P];
+            const double d2a = dg2a[c];
             double diag;
             if constexpr (FORM == FORM_SUM) {
-                const double d2b = b2[c * W + P];
+                const double d2b = dg2b[c];
                 if constexpr (IS3D) diag = d0a * (d1a * d2a) + d0b * (d1b * d2a + d1a * d2b);
                 else diag = d1a * d2a + d1b * d2b;
             } else {
                 diag = d0a * d1a * d2a;
             }
-            const double v = scale * bvec[base + c] / diag;
+            double rc = __builtin_amdgcn_rcp(diag);
+            double e = fma(-diag, rc, 1.0);
+            rc = fma(rc, e, rc);
+            e = fma(-diag, rc, 1.0);
+            rc = fma(rc, e, rc);
+            const double v = scale * bvec[base + c] * rc;
             xout[base + c] = v;
             s = fma(v, v, s);
         }
@@ -164,6 +171,7 @@ int diag_scale_launch(bool is3d, int form, const RowGeom& g, int P, int g0, doub
                       const double* b, double* x, const double* a0t, const double* b0t,
                       const double* a1, const double* b1, const double* a2, const double* b2,
                       double* partial, hipStream_t st, int* nblk_out) {
+    // a2 / b2 here are the contiguous axis-2 diagonals (poms_op keeps them)
     const int nb = row_blocks(g);
     if (nblk_out) *nblk_out = nb;
 #define POMS_DS(I3, F)                                                                          \
