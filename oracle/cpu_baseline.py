@@ -163,6 +163,8 @@ def time_vcycle(N: int = 96, p: int = 3, Nc: int = 8, cycles: int = 1, threads: 
     nf, nc = len(Tf) - p - 1, len(Tc) - p - 1
     Ts = knots_to_insert(Tf, nf, p, Tc, nc, p)
     P1 = matrix_multi_stages(Ts, nc, p, Tc)
+    if P1.shape[0] != nf:
+        raise ValueError(f"coarse knots ({Nc} cells) are not nested in the fine ones ({N} cells)")
     M, K = assemble_1d(Tf, p)
     A = CpuLaplace3D(M, K, p)
     Md, Kd = band_to_dense(M), band_to_dense(K)
