@@ -1,0 +1,98 @@
+"""The HIP path against the reference's own outputs (tests/golden/*.npz, made by
+tests/golden/make_golden.py from the reference's Python)."""
+import numpy as np
+import pytest
+
+from poms_amd.splines import assemble_1d, make_open_knots
+
+pytestmark = pytest.mark.gpu
+
+
+def load(golden_dir, name):
+    z = np.load(golden_dir / name, allow_pickle=False)
+    out = {}
+    for k in z.files:
+        case, field = k.split("__", 1)
+        out.setdefault(case, {})[field] = z[k]
+    return out
+
+
+def rel(a, b):
+    return float(np.linalg.norm((a - b).ravel()) / max(np.linalg.norm(b.ravel()), 1e-300))
+
+
+def test_kron_dot_pyccel_2d_golden(gpu, golden_dir):
+    """poms_kron_dot_2d with the pyccel kernel's arguments == `pyccel/pyccel_functions.py:4-21` outputs."""
+    from poms_amd.kron_product import kron_dot_pyccel_2d
+    for name, c in load(golden_dir, "kron_dot_2d.npz").items():
+        X = np.ascontiguousarray(c["X"])
+        Y = np.zeros_like(X)
+        kron_dot_pyccel_2d(c["starts"], c["ends"], c["pads"], X, np.zeros_like(X), Y,
+                           np.ascontiguousarray(c["A"]), np.ascontiguousarray(c["B"]))
+        p1, p2 = (int(v) for v in c["pads"])
+        s, e = c["starts"], c["ends"]
+        n1, n2 = int(e[0] - s[0] + 1), int(e[1] - s[1] + 1)
+        got, want = Y[p1:p1 + n1, p2:p2 + n2], c["Y"][p1:p1 + n1, p2:p2 + n2]
+        assert rel(got, want) <= 1e-13, name
+        # pointwise, scaled by the output's max (cancellation)
+        assert np.max(np.abs(got - want)) <= 1e-13 * max(np.max(np.abs(want)), 1e-300), name
+
+
+def _space_op(p, ne):
+    from poms_amd.stencil import KronOperator, StencilVectorSpace
+    M, K = assemble_1d(make_open_knots(p, ne + p), p)
+    n = ne + p
+    V = StencilVectorSpace([n, n], [p, p])
+    return V, KronOperator.laplace(V, [M, M], [K, K])
+
+
+def _pcg_bound(p, ne, c):
+    from oracle import poms_oracle as orc
+    M, K = assemble_1d(make_open_knots(p, ne + p), p)
+    n = ne + p
+    apply = lambda v: orc.kron_sum_apply(v.reshape(n, n), [M, M], [K, K]).reshape(-1)
+    D = orc.kron_sum_diag([M, M], [K, K]).reshape(-1)
+    xo, _ = orc.pcg(apply, lambda r: orc.damped_jacobi(apply, D, r), c["b"], tol=1e-6, maxiter=10)
+    return max(1e-9, 20 * rel(xo, c["pcg_mgjac"]))
+
+
+@pytest.mark.parametrize("p,ne", [(1, 4), (1, 16), (3, 8)])
+def test_solvers_golden(gpu, golden_dir, p, ne):
+    """damped_jacobi / pcg / jacobi on device == `sources/solvers.py` run by the reference."""
+    from poms_amd.solvers import damped_jacobi, jacobi, pcg
+    sol = load(golden_dir, "solvers_2d.npz")
+    V, A = _space_op(p, ne)
+    n = ne + p
+    for rhs in ("manuf", "ones"):
+        c = sol[f"p{p}_ne{ne}_{rhs}"]
+        b = V.zeros().from_numpy(c["b"].reshape(n, n))
+        for m in (1, 3, 10):
+            x = damped_jacobi(A, b, tol=0.0, maxiter=m)
+            assert rel(x.to_local_numpy().reshape(-1), c[f"djac_m{m}_tol0"]) <= 1e-12, (rhs, m)
+        x = damped_jacobi(A, b)
+        assert rel(x.to_local_numpy().reshape(-1), c["djac_default"]) <= 1e-12
+        assert rel(jacobi(A, b).to_local_numpy().reshape(-1), c["jacobi"]) <= 1e-14
+        for m in (1, 2, 5):
+            x, info = pcg(A, damped_jacobi, b, tol=0.0, maxiter=m)
+            assert info["niter"] == int(c[f"pcg_m{m}_tol0_info"][0])
+            assert rel(x.to_local_numpy().reshape(-1), c[f"pcg_m{m}_tol0"]) <= 1e-10, (rhs, m)
+        x, info = pcg(A, damped_jacobi, b, tol=1e-6, maxiter=10)
+        ref = c["pcg_mgjac_info"]
+        assert info["niter"] == int(ref[0]) and info["success"] == bool(ref[1])
+        # 10 PCG iterations amplify 1-ulp operator differences; the bound is
+        # the spread between the reference and the CPU oracle on our 1D factors
+        assert rel(x.to_local_numpy().reshape(-1), c["pcg_mgjac"]) <= _pcg_bound(p, ne, c)
+
+
+def test_vcycle_golden(gpu, golden_dir):
+    """TwoLevelVCycle on the reference driver's knots == `sources/mg_jac.py` run as a script."""
+    from poms_amd.mg import TwoLevelVCycle
+    for name, c in load(golden_dir, "vcycle_mg_jac.npz").items():
+        p = int(c["p"])
+        mg = TwoLevelVCycle(p, 0, 0, ndim=2, knots_fine=c["Tf"], knots_coarse=c["Tc"])
+        np.testing.assert_array_equal(mg.T, c["T"])
+        assert np.max(np.abs(mg.P1 - c["P1"])) <= 1e-15
+        bf = mg.rhs_ones()
+        xf2, ipre, ipos = mg.cycle(bf)
+        assert ipre["niter"] == int(c["info_pre"][0]) and ipos["niter"] == int(c["info_pos"][0]), name
+        assert rel(xf2.to_local_numpy().reshape(-1), c["xf2"]) <= 1e-8, name
