@@ -81,11 +81,15 @@ int poms_op_create(poms_ctx* ctx, int ndim, const poms_layout* layout, int form,
 int poms_op_destroy(poms_op* op);
 /* Planes per workgroup along axis 0 (3D); 0 = automatic. */
 int poms_op_set_chunk(poms_op* op, int chunk);
-/* Kernel variant: 0 = general (any band rows, any pads), 1 = Toeplitz-interior
- * fast path, 4 waves x 4 rows, 2 = same with 8 waves x 2 rows, 3 = 8 waves x
- * 4 rows, 4 = DPP axis-2 pass with one barrier per plane.  Variants 1-4 need
- * storage pads == pmax on every used axis; the default is the fastest
- * measured one when that holds, else 0.  All variants compute the same operator. */
+/* Kernel variant.  All variants compute the same operator:
+ *   0 = general (any band rows, any pads);
+ *   1-3 = v2 Toeplitz-interior kernels (4x4, 8x2, 8x4 waves x rows);
+ *   4 = v3: axis-2 pass by DPP lane shifts, (a, b) tile in LDS, one barrier per plane;
+ *   5 = v3 with 16 waves (32-row tile, p <= 3);   6 = v3 with x prefetched two planes ahead;
+ *   7 = v4: axis-1-first, x planes DMA'd into an LDS ring (buffer_load ... lds),
+ *       two columns per lane, symmetric Toeplitz pair sums;
+ *   8 = auto (default when pads == pmax): the fastest measured kernel per epilogue.
+ * Variants 1-8 need storage pads == pmax on every used axis.                  */
 int poms_op_set_variant(poms_op* op, int variant);
 int poms_op_get_variant(poms_op* op, int* variant);
 

@@ -45,7 +45,8 @@ struct AxisPass {
 struct ToepConst {
     double t1a[6], t1b[6];   // axis 1 (A1, B1)
     double t0a[6], t0b[6];   // axis 0 (A0, M0), global rows
-    int lo1, hi1, lo0, hi0;
+    double t2a[6], t2b[6];   // axis 2 (M2, K2)
+    int lo1, hi1, lo0, hi0, lo2, hi2;
 };
 
 // Device pointers of one fused Kronecker launch.
@@ -84,6 +85,19 @@ __device__ __forceinline__ double bload(__amdgpu_buffer_rsrc_t r, int off_bytes)
 }
 __device__ __forceinline__ void bstore(__amdgpu_buffer_rsrc_t r, int off_bytes, double d) {
     __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(u32x2, d), r, off_bytes, 0, 0);
+}
+// store with an explicit cache-policy field (gfx950 aux: bit0 sc0, bit1 nt, bit4 sc1)
+template <int AUX>
+__device__ __forceinline__ void bstore_p(__amdgpu_buffer_rsrc_t r, int off_bytes, double d) {
+    __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(u32x2, d), r, off_bytes, 0, AUX);
+}
+typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+template <int AUX>
+__device__ __forceinline__ void bstore2_p(__amdgpu_buffer_rsrc_t r, int off_bytes, double d0, double d1) {
+    u32x4 v;
+    const u32x2 a = __builtin_bit_cast(u32x2, d0), b = __builtin_bit_cast(u32x2, d1);
+    v.x = a.x; v.y = a.y; v.z = b.x; v.w = b.y;
+    __builtin_amdgcn_raw_buffer_store_b128(v, r, off_bytes, 0, AUX);
 }
 
 // bytes of `planes_left` padded planes of s0 doubles, clamped to 2^31-1

@@ -33,7 +33,7 @@ __device__ __forceinline__ double dpp_shl1(double v) {  // lane l <- lane l+1 (l
     return __builtin_bit_cast(double, make_int2(lo, hi));
 }
 
-template <int P, int R, int NW, bool IS3D, int FORM, int EPI>
+template <int P, int R, int NW, bool IS3D, int FORM, int EPI, int PF, int MODE = 0>
 __global__ void __launch_bounds__(NW * 64, ((P <= 3 && NW <= 8 ? 2 : 1) * NW * 64) / 256)  // 16 waves/CU for P <= 3
 kron_v3_kernel(const double* __restrict__ x, double* __restrict__ y,
                const double* __restrict__ bvec,
@@ -117,14 +117,14 @@ kron_v3_kernel(const double* __restrict__ x, double* __restrict__ y,
         const int rr = wv + j * NW;
         xoff[j] = rr < XR ? ((r0 + rr) * (int)g.s1 + (c0 + lane)) * 8 : 0x7ffffff0;
     }
-    double xr[NRW];
-    auto load_plane = [&](int jj) {
+    double xr[PF][NRW];
+    auto load_plane = [&](int jj, int xb) {
         const int sp = IS3D ? jj + g.pd0 : 0;
         const bool ok = (sp >= 0) && (sp < nsp);
         const __amdgpu_buffer_rsrc_t rs =
             make_rsrc(x + (int64_t)(ok ? sp : 0) * g.s0, ok ? plane_bytes(nsp - sp, g.s0) : 0u);
 #pragma unroll
-        for (int j = 0; j < NRW; ++j) xr[j] = bload(rs, xoff[j]);
+        for (int j = 0; j < NRW; ++j) xr[xb][j] = MODE == 2 ? (double)(jj * 7 + j) * 1e-3 + (double)lane : bload(rs, xoff[j]);
     };
 
     double acc[R][NS];
@@ -136,7 +136,7 @@ kron_v3_kernel(const double* __restrict__ x, double* __restrict__ y,
 
     const int obase = ((r0 + wv * R + g.pd1) * (int)g.s1 + (i2 + g.pd2)) * 8;
     const int rowstep = (int)g.s1 * 8;
-    double eb[R], ex[R];
+    double ebb[PF][R], ex[R];
     // plane-invariant factors of diag(A) for row r of this thread (recomputed
     // per plane: cheaper than keeping 2R doubles live)
     auto diag_parts = [&](int r, double& dX, double& dY) {
@@ -150,7 +150,8 @@ kron_v3_kernel(const double* __restrict__ x, double* __restrict__ y,
             dY = 0.0;
         }
     };
-    auto epi_issue = [&](int zo) {
+    auto epi_issue = [&](int zo, int eb_i) {
+        double* eb = ebb[eb_i];
         if constexpr (EPI != EPI_APPLY) {
             const int sp = zo + g.pd0;
             const uint32_t nb = plane_bytes(nsp - sp, g.s0);
@@ -164,7 +165,8 @@ kron_v3_kernel(const double* __restrict__ x, double* __restrict__ y,
             }
         }
     };
-    auto epi_finish = [&](int zo, const double* v, bool en) {
+    auto epi_finish = [&](int zo, const double* v, bool en, int eb_i) {
+        const double* eb = ebb[eb_i];
         const int sp = zo + g.pd0;
         const __amdgpu_buffer_rsrc_t ys = make_rsrc(y + (int64_t)sp * g.s0, plane_bytes(nsp - sp, g.s0));
         double d0a = 1.0, d0b = 0.0;
@@ -194,24 +196,35 @@ kron_v3_kernel(const double* __restrict__ x, double* __restrict__ y,
                 outv = ex[r] + dr;
                 nrm = ok ? fma(dr, dr, nrm) : nrm;
             }
-            bstore(ys, ok ? obase + r * rowstep : 0x7ffffff0, outv);
+            if constexpr (MODE == 2) {
+                if (outv == 12345.678) bstore(ys, ok ? obase + r * rowstep : 0x7ffffff0, outv);
+            } else {
+                bstore(ys, ok ? obase + r * rowstep : 0x7ffffff0, outv);
+            }
         }
     };
 
-    load_plane(IS3D ? z0 - P : 0);
+    auto zo_of = [&](int t) { return IS3D ? max(z0 - 2 * P + t, z0) : 0; };
+    load_plane(IS3D ? z0 - P : 0, 0);
+    if constexpr (PF == 2) {
+        load_plane(IS3D ? (1 < nplanes ? z0 - P + 1 : -(1 << 20)) : 0, 1);
+        epi_issue(zo_of(0), 0);
+    }
     __syncthreads();  // c1a/c1b visible
 
-    for (int tb = 0; tb < nplanes; tb += NS) {
+    for (int tb = 0; tb < nplanes; tb += NS * PF) {
 #pragma unroll
-        for (int q = 0; q < NS; ++q) {
-            const int t = tb + q;
+        for (int q2 = 0; q2 < NS * PF; ++q2) {
+            const int t = tb + q2;
+            const int q = q2 % NS;
+            const int xb = q2 % PF;
             if (t < nplanes) {
                 const int buf = (t & 1) * XRP * 64;
                 // ---- axis 2 in registers: DPP shifts of whole rows
 #pragma unroll
                 for (int j = 0; j < NRW; ++j) {
                     double sh[W];
-                    sh[P] = xr[j];
+                    sh[P] = xr[xb][j];
 #pragma unroll
                     for (int d = 1; d <= P; ++d) {
                         sh[P - d] = dpp_shr1(sh[P - d + 1]);  // column i2 - d
@@ -219,16 +232,18 @@ kron_v3_kernel(const double* __restrict__ x, double* __restrict__ y,
                     }
                     double sa = ca2[0] * sh[0];
                     double sb = SUM ? cb2[0] * sh[0] : 0.0;
+                    if constexpr (MODE == 1) { sa = xr[xb][j]; sb = sa; } else {
 #pragma unroll
                     for (int k = 1; k < W; ++k) {
                         sa = fma(ca2[k], sh[k], sa);
                         if constexpr (SUM) sb = fma(cb2[k], sh[k], sb);
                     }
+                    }
                     const int rr = wv + j * NW;
                     if constexpr (XRING) {
                         const int orow = rr - P;   // output row of this tile row, if any
                         if (orow >= 0 && orow < T1)
-                            xring[(((t + NRING) % NRING) * T1 + orow) * 64 + lane] = xr[j];
+                            xring[(((t + NRING) % NRING) * T1 + orow) * 64 + lane] = xr[xb][j];
                     }
                     if (XR % NW == 0 || rr < XR) {
                         if constexpr (SUM) {
@@ -242,7 +257,8 @@ kron_v3_kernel(const double* __restrict__ x, double* __restrict__ y,
                     }
                 }
                 // ---- loads for the rest of the iteration / the next plane
-                epi_issue(IS3D ? max(z0 - 2 * P + t, z0) : 0);
+                if constexpr (PF == 1) epi_issue(zo_of(t), 0);
+                else epi_issue(zo_of(t + 1), (q2 + 1) % PF);
                 if constexpr (XRING) {
                     // x_in of this iteration's output plane (input plane t-P): read
                     // BEFORE the barrier -- its slot is rewritten by iteration t+1's
@@ -251,7 +267,7 @@ kron_v3_kernel(const double* __restrict__ x, double* __restrict__ y,
 #pragma unroll
                     for (int r = 0; r < R; ++r) ex[r] = xring[(slot * T1 + wv * R + r) * 64 + lane];
                 }
-                if constexpr (IS3D) load_plane(t + 1 < nplanes ? z0 - P + t + 1 : -(1 << 20));
+                if constexpr (IS3D) load_plane(t + PF < nplanes ? z0 - P + t + PF : -(1 << 20), xb);
                 __syncthreads();
 
                 // ---- axis 1 from the LDS tile
@@ -285,7 +301,10 @@ kron_v3_kernel(const double* __restrict__ x, double* __restrict__ y,
                         }
                     }
                 };
-                if (fast1) {
+                if constexpr (MODE == 1) {
+                    const d2 pr = ab_[buf + (wv * R + P) * 64 + lane];
+                    for (int r = 0; r < R; ++r) { cv[r] = pr.x; dv[r] = pr.y; }
+                } else if (fast1) {
                     axis1([&](int, int k, double& ca, double& cb) {
                         const int jj = k < P ? P - k : k - P;
                         ca = tc.t1a[jj];
@@ -298,7 +317,12 @@ kron_v3_kernel(const double* __restrict__ x, double* __restrict__ y,
                     });
                 }
 
-                if constexpr (IS3D) {
+                if constexpr (IS3D && MODE == 1) {
+                    double vv[R];
+#pragma unroll
+                    for (int r = 0; r < R; ++r) vv[r] = cv[r] + dv[r];
+                    epi_finish(zo_of(t), vv, t >= 2 * P, PF == 1 ? 0 : xb);
+                } else if constexpr (IS3D) {
                     // ---- axis 0: scatter into rotating slots
                     const int jrow = (g.g0 + z0 - P + t + P) * W;
 #pragma unroll
@@ -316,11 +340,11 @@ kron_v3_kernel(const double* __restrict__ x, double* __restrict__ y,
                     double vv[R];
 #pragma unroll
                     for (int r = 0; r < R; ++r) vv[r] = acc[r][done];
-                    epi_finish(max(z0 - 2 * P + t, z0), vv, t >= 2 * P);
+                    epi_finish(zo_of(t), vv, t >= 2 * P, PF == 1 ? 0 : xb);
 #pragma unroll
                     for (int r = 0; r < R; ++r) acc[r][done] = 0.0;
                 } else {
-                    epi_finish(0, cv, true);
+                    epi_finish(0, cv, true, 0);
                 }
             }
         }
@@ -341,39 +365,54 @@ kron_v3_kernel(const double* __restrict__ x, double* __restrict__ y,
     }
 }
 
-template <int P, int R, int NW, bool IS3D, int FORM, int EPI>
+template <int P, int R, int NW, bool IS3D, int FORM, int EPI, int PF, int MODE = 0>
 static void v3_launch_t(const KronPtrs& p, const KronGeom& g, const ToepConst& tc, double omega,
                         hipStream_t st) {
     const int nblk = g.tiles2 * g.tiles1 * g.nchunks;
-    hipLaunchKernelGGL((kron_v3_kernel<P, R, NW, IS3D, FORM, EPI>), dim3(nblk), dim3(NW * 64), 0, st,
+    hipLaunchKernelGGL((kron_v3_kernel<P, R, NW, IS3D, FORM, EPI, PF, MODE>), dim3(nblk), dim3(NW * 64), 0, st,
                        p.x, p.y, p.b, p.a0t, p.b0t, p.a1, p.b1, p.a2, p.b2, p.partial, g, tc, omega);
 }
 
-template <int P, int R, int NW, bool IS3D, int FORM>
+template <int P, int R, int NW, bool IS3D, int FORM, int PF>
 static int v3_launch_e(int epi, const KronPtrs& p, const KronGeom& g, const ToepConst& tc,
                        double omega, hipStream_t st) {
     switch (epi) {
-        case EPI_APPLY: v3_launch_t<P, R, NW, IS3D, FORM, EPI_APPLY>(p, g, tc, omega, st); return 0;
-        case EPI_RESID: v3_launch_t<P, R, NW, IS3D, FORM, EPI_RESID>(p, g, tc, omega, st); return 0;
-        case EPI_JACOBI: v3_launch_t<P, R, NW, IS3D, FORM, EPI_JACOBI>(p, g, tc, omega, st); return 0;
+        case EPI_APPLY: v3_launch_t<P, R, NW, IS3D, FORM, EPI_APPLY, PF>(p, g, tc, omega, st); return 0;
+        case EPI_RESID: v3_launch_t<P, R, NW, IS3D, FORM, EPI_RESID, PF>(p, g, tc, omega, st); return 0;
+        case EPI_JACOBI: v3_launch_t<P, R, NW, IS3D, FORM, EPI_JACOBI, PF>(p, g, tc, omega, st); return 0;
     }
     return 1;
 }
 
-template <int P, int R, int NW>
+template <int P, int R, int NW, int PF = 1>
 static int v3_launch_p(bool is3d, int form, int epi, const KronPtrs& p, const KronGeom& g,
                        const ToepConst& tc, double omega, hipStream_t st) {
     if (is3d)
-        return form == FORM_SUM ? v3_launch_e<P, R, NW, true, FORM_SUM>(epi, p, g, tc, omega, st)
-                                : v3_launch_e<P, R, NW, true, FORM_SINGLE>(epi, p, g, tc, omega, st);
-    return form == FORM_SUM ? v3_launch_e<P, R, NW, false, FORM_SUM>(epi, p, g, tc, omega, st)
-                            : v3_launch_e<P, R, NW, false, FORM_SINGLE>(epi, p, g, tc, omega, st);
+        return form == FORM_SUM ? v3_launch_e<P, R, NW, true, FORM_SUM, PF>(epi, p, g, tc, omega, st)
+                                : v3_launch_e<P, R, NW, true, FORM_SINGLE, PF>(epi, p, g, tc, omega, st);
+    return form == FORM_SUM ? v3_launch_e<P, R, NW, false, FORM_SUM, PF>(epi, p, g, tc, omega, st)
+                            : v3_launch_e<P, R, NW, false, FORM_SINGLE, PF>(epi, p, g, tc, omega, st);
 }
 
 // variant 4: 8 waves x 2 rows (16 x (64-2P) tile, 2 WGs/CU);
 // variant 5: 16 waves x 2 rows (32 x (64-2P) tile, 1 WG/CU, less halo recompute)
 int kron_v3_launch(int variant, int pmax, bool is3d, int form, int epi, const KronPtrs& p,
                    const KronGeom& g, const ToepConst& tc, double omega, hipStream_t st) {
+    if (variant == 90 || variant == 91) {   // DIAGNOSTIC: memory-only / compute-only apply, 3D SUM P=3
+        if (pmax != 3 || !is3d || form != FORM_SUM || epi != EPI_APPLY) { set_error("diag variant: 3D SUM P=3 apply only"); return 1; }
+        if (variant == 90) v3_launch_t<3, 2, 8, true, FORM_SUM, EPI_APPLY, 1, 1>(p, g, tc, omega, st);
+        else v3_launch_t<3, 2, 8, true, FORM_SUM, EPI_APPLY, 1, 2>(p, g, tc, omega, st);
+        return 0;
+    }
+    if (variant == 6) {
+        switch (pmax) {
+            case 1: return v3_launch_p<1, 2, 8, 2>(is3d, form, epi, p, g, tc, omega, st);
+            case 2: return v3_launch_p<2, 2, 8, 2>(is3d, form, epi, p, g, tc, omega, st);
+            case 3: return v3_launch_p<3, 2, 8, 2>(is3d, form, epi, p, g, tc, omega, st);
+            case 4: return v3_launch_p<4, 2, 8, 2>(is3d, form, epi, p, g, tc, omega, st);
+            case 5: return v3_launch_p<5, 2, 8, 2>(is3d, form, epi, p, g, tc, omega, st);
+        }
+    }
     if (variant == 5) {
         switch (pmax) {
             case 1: return v3_launch_p<1, 2, 16>(is3d, form, epi, p, g, tc, omega, st);

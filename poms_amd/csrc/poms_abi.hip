@@ -17,6 +17,8 @@ int kron_v2_launch(int variant, int pmax, bool is3d, int form, int epi, const Kr
                    const KronGeom& g, const ToepConst& tc, double omega, hipStream_t st);
 int kron_v3_launch(int variant, int pmax, bool is3d, int form, int epi, const KronPtrs& p,
                    const KronGeom& g, const ToepConst& tc, double omega, hipStream_t st);
+int kron_v4_launch(int pmax, bool is3d, int form, int epi, const KronPtrs& p, const KronGeom& g,
+                   const ToepConst& tc, double omega, hipStream_t st, int diag_mode);
 int kron_v2_stamps(int variant, int epi, const KronPtrs& p, const KronGeom& g, const ToepConst& tc,
                    double omega, unsigned long long* dbg, hipStream_t st);
 int kron_tile_rows();
@@ -241,7 +243,8 @@ int poms_op_create(poms_ctx* ctx, int ndim, const poms_layout* layout, int form,
     if (is3d)
         toeplitz_range(f[0], sum ? f[1] : nullptr, n0_global, pmax, &o->tc.lo0, &o->tc.hi0, o->tc.t0a, o->tc.t0b);
     toeplitz_range(f[2], sum ? f[3] : nullptr, layout->n[1], pmax, &o->tc.lo1, &o->tc.hi1, o->tc.t1a, o->tc.t1b);
-    o->variant = o->v2_ok ? 4 : 0;
+    toeplitz_range(f[4], sum ? f[5] : nullptr, layout->n[2], pmax, &o->tc.lo2, &o->tc.hi2, o->tc.t2a, o->tc.t2b);
+    o->variant = o->v2_ok ? 8 : 0;
     *op = o;
     return 0;
 }
@@ -255,7 +258,7 @@ int poms_op_destroy(poms_op* o) {
 }
 
 int poms_op_set_variant(poms_op* op, int variant) {
-    if (!op || variant < 0 || variant > 5) { set_error("poms_op_set_variant: bad argument"); return 1; }
+    if (!op || variant < 0 || (variant > 8 && (variant < 90 || variant > 97))) { set_error("poms_op_set_variant: bad argument"); return 1; }
     if (variant > 0 && !op->v2_ok) { set_error("poms_op_set_variant: variant needs pads == pmax"); return 1; }
     if (variant == 5 && op->pmax > 3) variant = 4;  // 32-row tile does not fit LDS at p >= 4
     op->variant = variant;
@@ -317,11 +320,18 @@ static int op_run(poms_op* o, int epi, double omega, const double* x, double* y,
     if (want_norm && nblk > kScratch) { set_error("too many blocks for norm scratch"); return 1; }
     KronPtrs p{x, y, b, o->a0t, o->b0t, o->a1, o->b1, o->a2, o->b2,
                want_norm ? o->ctx->scratch : nullptr};
-    const int rc = o->variant == 0
+    // variant 8 (default when pads == pmax): the fastest measured kernel per
+    // epilogue -- v4 (7) for apply / residual at p <= 3, v3 (4) otherwise
+    int v = o->variant;
+    if (v == 8) v = (epi != EPI_JACOBI && o->pmax <= 3) ? 7 : 4;
+    const int rc = v == 0
         ? kron_launch(o->pmax, o->ndim == 3, o->form, epi, p, g, omega, as_stream(stream))
-        : o->variant >= 4
-        ? kron_v3_launch(o->variant, o->pmax, o->ndim == 3, o->form, epi, p, g, o->tc, omega, as_stream(stream))
-        : kron_v2_launch(o->variant, o->pmax, o->ndim == 3, o->form, epi, p, g, o->tc, omega, as_stream(stream));
+        : (v == 7 || (v >= 92 && v <= 97))
+        ? kron_v4_launch(o->pmax, o->ndim == 3, o->form, epi, p, g, o->tc, omega, as_stream(stream),
+                         v == 7 ? 0 : v - 91)
+        : v >= 4
+        ? kron_v3_launch(v, o->pmax, o->ndim == 3, o->form, epi, p, g, o->tc, omega, as_stream(stream))
+        : kron_v2_launch(v, o->pmax, o->ndim == 3, o->form, epi, p, g, o->tc, omega, as_stream(stream));
     if (rc) return 1;
     POMS_HIP_CHECK(hipGetLastError());
     o->last_partials = want_norm ? nblk : 0;

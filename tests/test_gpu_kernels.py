@@ -49,7 +49,7 @@ CASES = [
 ]
 
 
-VARIANTS = [0, 1, 2, 3, 4, 5]
+VARIANTS = [0, 1, 2, 3, 4, 5, 6, 7, 8]
 
 
 @pytest.mark.parametrize("ndim,cells,p", CASES)
