@@ -88,7 +88,8 @@ int poms_op_set_chunk(poms_op* op, int chunk);
  *   5 = v3 with 16 waves (32-row tile, p <= 3);   6 = v3 with x prefetched two planes ahead;
  *   7 = v4: axis-1-first, x planes DMA'd into an LDS ring (buffer_load ... lds),
  *       two columns per lane, symmetric Toeplitz pair sums;
- *   8 = auto (default when pads == pmax): the fastest measured kernel per epilogue.
+ *   8 = auto (default when pads == pmax): the fastest measured kernel per epilogue;
+ *   9 = v3 addressing each array through one buffer resource (arrays < 2 GiB).
  * Variants 1-8 need storage pads == pmax on every used axis.                  */
 int poms_op_set_variant(poms_op* op, int variant);
 int poms_op_get_variant(poms_op* op, int* variant);
@@ -111,6 +112,16 @@ int poms_op_residual(poms_op* op, const double* b, const double* x, double* r,
 int poms_op_jacobi_sweep(poms_op* op, double omega, const double* b,
                          const double* x_in, double* x_out, int64_t z_begin,
                          int64_t z_end, int want_norm, void* stream);
+/* The same sweep, also accumulating x_out . b per block: the dr.dr partials
+ * (if want_norm) go to scratch[0, count), the x_out . b partials to
+ * scratch[count, 2 count) with count from poms_op_last_partials; reduce them
+ * with poms_reduce_partials_at.  With b = r this is pcg's `sr = s.dot(r)`
+ * (`sources/solvers.py:91,120`) fused into the last smoothing sweep.
+ * Kernel variants 4-9 only (poms_op_fused_dot_supported).                    */
+int poms_op_jacobi_sweep_dot(poms_op* op, double omega, const double* b,
+                             const double* x_in, double* x_out, int64_t z_begin,
+                             int64_t z_end, int want_norm, void* stream);
+int poms_op_fused_dot_supported(poms_op* op, int* yes);
 /* x = scale * b / diag(A) on the interior.  With scale = 1 this is
  * `jacobi(A, b)` (`sources/solvers.py:139-163`); with scale = omega it is the
  * first damped-Jacobi sweep from x0 = 0 (A.0 = 0 exactly).                    */
@@ -155,6 +166,9 @@ int poms_pcg_update(poms_ctx* ctx, const poms_layout* L, double alpha, double* x
                     void* stream);
 /* Reduce `count` partials from the context scratch into out_dev[0]. */
 int poms_reduce_partials(poms_ctx* ctx, int64_t count, double* out_dev, void* stream);
+/* Same, starting at scratch[offset]. */
+int poms_reduce_partials_at(poms_ctx* ctx, int64_t offset, int64_t count, double* out_dev,
+                            void* stream);
 
 /* ---- inter-grid transfer (knot insertion) --------------------------------- */
 /* P_d are HOST dense row-major (nf_global_d x nc_d) prolongation factors

@@ -60,6 +60,8 @@ _SIGS = {
     "poms_op_apply": [_vp, _vp, _vp, _i64, _i64, _vp],
     "poms_op_residual": [_vp, _vp, _vp, _vp, _i64, _i64, _vp],
     "poms_op_jacobi_sweep": [_vp, _d, _vp, _vp, _vp, _i64, _i64, _i, _vp],
+    "poms_op_jacobi_sweep_dot": [_vp, _d, _vp, _vp, _vp, _i64, _i64, _i, _vp],
+    "poms_op_fused_dot_supported": [_vp, C.POINTER(_i)],
     "poms_op_diag_scale": [_vp, _d, _vp, _vp, _i, _vp],
     "poms_op_last_partials": [_vp, C.POINTER(_i64)],
     "poms_op_profile_phases": [_vp, _i, _vp, _vp, _vp, _vp, C.POINTER(_i64), _vp],
@@ -70,6 +72,7 @@ _SIGS = {
     "poms_vec_dot": [_vp, _LP, _vp, _vp, _vp, _vp],
     "poms_pcg_update": [_vp, _LP, _d, _vp, _vp, _vp, _vp, _vp, _vp],
     "poms_reduce_partials": [_vp, _i64, _vp, _vp],
+    "poms_reduce_partials_at": [_vp, _i64, _i64, _vp, _vp],
     "poms_transfer_create": [_vp, _i, _LP, _i64, _vp, _vp, C.POINTER(C.c_void_p), _pp],
     "poms_transfer_destroy": [_vp],
     "poms_restrict": [_vp, _vp, _vp, _vp],

@@ -55,7 +55,8 @@ struct KronPtrs {
     double* y;
     const double* b;
     const double *a0t, *b0t, *a1, *b1, *a2, *b2;
-    double* partial;
+    double* partial;    // Jacobi: per-block sums of dr.dr (or null)
+    double* partial2;   // Jacobi: per-block sums of x_out.b (or null)
 };
 
 void set_error(const std::string& msg);
@@ -85,6 +86,14 @@ __device__ __forceinline__ double bload(__amdgpu_buffer_rsrc_t r, int off_bytes)
 }
 __device__ __forceinline__ void bstore(__amdgpu_buffer_rsrc_t r, int off_bytes, double d) {
     __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(u32x2, d), r, off_bytes, 0, 0);
+}
+// loads / stores with a scalar (per-plane) offset on a whole-array resource
+__device__ __forceinline__ double bload_s(__amdgpu_buffer_rsrc_t r, int voff, unsigned soff) {
+    u32x2 v = __builtin_amdgcn_raw_buffer_load_b64(r, voff, (int)soff, 0);
+    return __builtin_bit_cast(double, v);
+}
+__device__ __forceinline__ void bstore_s(__amdgpu_buffer_rsrc_t r, int voff, unsigned soff, double d) {
+    __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(u32x2, d), r, voff, (int)soff, 0);
 }
 // store with an explicit cache-policy field (gfx950 aux: bit0 sc0, bit1 nt, bit4 sc1)
 template <int AUX>

@@ -33,15 +33,15 @@ __device__ __forceinline__ double dpp_shl1(double v) {  // lane l <- lane l+1 (l
     return __builtin_bit_cast(double, make_int2(lo, hi));
 }
 
-template <int P, int R, int NW, bool IS3D, int FORM, int EPI, int PF, int MODE = 0>
+template <int P, int R, int NW, bool IS3D, int FORM, int EPI, int PF, int MODE = 0, bool FLAT = false>
 __global__ void __launch_bounds__(NW * 64, ((P <= 3 && NW <= 8 ? 2 : 1) * NW * 64) / 256)  // 16 waves/CU for P <= 3
 kron_v3_kernel(const double* __restrict__ x, double* __restrict__ y,
                const double* __restrict__ bvec,
                const double* __restrict__ a0t, const double* __restrict__ b0t,
                const double* __restrict__ a1, const double* __restrict__ b1,
                const double* __restrict__ a2, const double* __restrict__ b2,
-               double* __restrict__ partial, const KronGeom g, const ToepConst tc,
-               const double omega) {
+               double* __restrict__ partial, double* __restrict__ partial2, const KronGeom g,
+               const ToepConst tc, const double omega) {
     constexpr int W = 2 * P + 1;
     constexpr int NT = NW * 64;
     constexpr int TO = 64 - 2 * P;          // output columns per tile
@@ -118,9 +118,22 @@ kron_v3_kernel(const double* __restrict__ x, double* __restrict__ y,
         xoff[j] = rr < XR ? ((r0 + rr) * (int)g.s1 + (c0 + lane)) * 8 : 0x7ffffff0;
     }
     double xr[PF][NRW];
+    // FLAT: one resource per array for the whole launch (array < 2 GiB, checked by the
+    // host); planes are addressed by the scalar offset -- no per-plane descriptor math
+    const uint32_t arr_bytes = FLAT ? (uint32_t)((int64_t)nsp * g.s0 * 8) : 0u;
+    const __amdgpu_buffer_rsrc_t rx_all = make_rsrc(x, arr_bytes);
+    const __amdgpu_buffer_rsrc_t rb_all = make_rsrc(bvec, EPI != EPI_APPLY ? arr_bytes : 0u);
+    const __amdgpu_buffer_rsrc_t ry_all = make_rsrc(y, arr_bytes);
+    const uint32_t plane8 = (uint32_t)(g.s0 * 8);
     auto load_plane = [&](int jj, int xb) {
         const int sp = IS3D ? jj + g.pd0 : 0;
         const bool ok = (sp >= 0) && (sp < nsp);
+        if constexpr (FLAT) {
+            const uint32_t so = ok ? (uint32_t)sp * plane8 : 0x80000000u;
+#pragma unroll
+            for (int j = 0; j < NRW; ++j) xr[xb][j] = bload_s(rx_all, xoff[j], so);
+            return;
+        }
         const __amdgpu_buffer_rsrc_t rs =
             make_rsrc(x + (int64_t)(ok ? sp : 0) * g.s0, ok ? plane_bytes(nsp - sp, g.s0) : 0u);
 #pragma unroll
@@ -132,7 +145,7 @@ kron_v3_kernel(const double* __restrict__ x, double* __restrict__ y,
     for (int r = 0; r < R; ++r)
 #pragma unroll
         for (int s = 0; s < NS; ++s) acc[r][s] = 0.0;
-    double nrm = 0.0;
+    double nrm = 0.0, dotp = 0.0;
 
     const int obase = ((r0 + wv * R + g.pd1) * (int)g.s1 + (i2 + g.pd2)) * 8;
     const int rowstep = (int)g.s1 * 8;
@@ -152,7 +165,15 @@ kron_v3_kernel(const double* __restrict__ x, double* __restrict__ y,
     };
     auto epi_issue = [&](int zo, int eb_i) {
         double* eb = ebb[eb_i];
-        if constexpr (EPI != EPI_APPLY) {
+        if constexpr (EPI != EPI_APPLY && FLAT) {
+            const uint32_t so = (uint32_t)(zo + g.pd0) * plane8;
+#pragma unroll
+            for (int r = 0; r < R; ++r) eb[r] = bload_s(rb_all, obase + r * rowstep, so);
+            if constexpr (EPI == EPI_JACOBI && !XRING) {
+#pragma unroll
+                for (int r = 0; r < R; ++r) ex[r] = bload_s(rx_all, obase + r * rowstep, so);
+            }
+        } else if constexpr (EPI != EPI_APPLY) {
             const int sp = zo + g.pd0;
             const uint32_t nb = plane_bytes(nsp - sp, g.s0);
             const __amdgpu_buffer_rsrc_t bs = make_rsrc(bvec + (int64_t)sp * g.s0, nb);
@@ -195,9 +216,12 @@ kron_v3_kernel(const double* __restrict__ x, double* __restrict__ y,
                 const double dr = omega * (eb[r] - v[r]) * rc;
                 outv = ex[r] + dr;
                 nrm = ok ? fma(dr, dr, nrm) : nrm;
+                dotp = ok ? fma(outv, eb[r], dotp) : dotp;   // x_out . b (pcg's s.r)
             }
             if constexpr (MODE == 2) {
                 if (outv == 12345.678) bstore(ys, ok ? obase + r * rowstep : 0x7ffffff0, outv);
+            } else if constexpr (FLAT) {
+                bstore_s(ry_all, ok ? obase + r * rowstep : 0x7ffffff0, (uint32_t)sp * plane8, outv);
             } else {
                 bstore(ys, ok ? obase + r * rowstep : 0x7ffffff0, outv);
             }
@@ -362,36 +386,48 @@ kron_v3_kernel(const double* __restrict__ x, double* __restrict__ y,
                 partial[blockIdx.x] = s;
             }
         }
+        if (partial2 != nullptr) {
+#pragma unroll
+            for (int off = 32; off > 0; off >>= 1) dotp += __shfl_xor(dotp, off, 64);
+            __syncthreads();
+            if (lane == 0) red[wv] = dotp;
+            __syncthreads();
+            if (tid == 0) {
+                double s = 0.0;
+                for (int w = 0; w < NW; ++w) s += red[w];
+                partial2[blockIdx.x] = s;
+            }
+        }
     }
 }
 
-template <int P, int R, int NW, bool IS3D, int FORM, int EPI, int PF, int MODE = 0>
+template <int P, int R, int NW, bool IS3D, int FORM, int EPI, int PF, int MODE = 0, bool FLAT = false>
 static void v3_launch_t(const KronPtrs& p, const KronGeom& g, const ToepConst& tc, double omega,
                         hipStream_t st) {
     const int nblk = g.tiles2 * g.tiles1 * g.nchunks;
-    hipLaunchKernelGGL((kron_v3_kernel<P, R, NW, IS3D, FORM, EPI, PF, MODE>), dim3(nblk), dim3(NW * 64), 0, st,
-                       p.x, p.y, p.b, p.a0t, p.b0t, p.a1, p.b1, p.a2, p.b2, p.partial, g, tc, omega);
+    hipLaunchKernelGGL((kron_v3_kernel<P, R, NW, IS3D, FORM, EPI, PF, MODE, FLAT>), dim3(nblk), dim3(NW * 64), 0, st,
+                       p.x, p.y, p.b, p.a0t, p.b0t, p.a1, p.b1, p.a2, p.b2, p.partial, p.partial2, g, tc, omega);
 }
 
-template <int P, int R, int NW, bool IS3D, int FORM, int PF>
+template <int P, int R, int NW, bool IS3D, int FORM, int PF, bool FLAT = false>
 static int v3_launch_e(int epi, const KronPtrs& p, const KronGeom& g, const ToepConst& tc,
                        double omega, hipStream_t st) {
     switch (epi) {
-        case EPI_APPLY: v3_launch_t<P, R, NW, IS3D, FORM, EPI_APPLY, PF>(p, g, tc, omega, st); return 0;
-        case EPI_RESID: v3_launch_t<P, R, NW, IS3D, FORM, EPI_RESID, PF>(p, g, tc, omega, st); return 0;
-        case EPI_JACOBI: v3_launch_t<P, R, NW, IS3D, FORM, EPI_JACOBI, PF>(p, g, tc, omega, st); return 0;
+        case EPI_APPLY: v3_launch_t<P, R, NW, IS3D, FORM, EPI_APPLY, PF, 0, FLAT>(p, g, tc, omega, st); return 0;
+        case EPI_RESID: v3_launch_t<P, R, NW, IS3D, FORM, EPI_RESID, PF, 0, FLAT>(p, g, tc, omega, st); return 0;
+        case EPI_JACOBI: v3_launch_t<P, R, NW, IS3D, FORM, EPI_JACOBI, PF, 0, FLAT>(p, g, tc, omega, st); return 0;
     }
     return 1;
 }
 
-template <int P, int R, int NW, int PF = 1>
+template <int P, int R, int NW, int PF = 1, bool FLAT = false>
 static int v3_launch_p(bool is3d, int form, int epi, const KronPtrs& p, const KronGeom& g,
                        const ToepConst& tc, double omega, hipStream_t st) {
     if (is3d)
-        return form == FORM_SUM ? v3_launch_e<P, R, NW, true, FORM_SUM, PF>(epi, p, g, tc, omega, st)
-                                : v3_launch_e<P, R, NW, true, FORM_SINGLE, PF>(epi, p, g, tc, omega, st);
-    return form == FORM_SUM ? v3_launch_e<P, R, NW, false, FORM_SUM, PF>(epi, p, g, tc, omega, st)
-                            : v3_launch_e<P, R, NW, false, FORM_SINGLE, PF>(epi, p, g, tc, omega, st);
+        return form == FORM_SUM ? v3_launch_e<P, R, NW, true, FORM_SUM, PF, FLAT>(epi, p, g, tc, omega, st)
+                                : v3_launch_e<P, R, NW, true, FORM_SINGLE, PF, FLAT>(epi, p, g, tc, omega, st);
+    return form == FORM_SUM ? v3_launch_e<P, R, NW, false, FORM_SUM, PF, FLAT>(epi, p, g, tc, omega, st)
+                            : v3_launch_e<P, R, NW, false, FORM_SINGLE, PF, FLAT>(epi, p, g, tc, omega, st);
 }
 
 // variant 4: 8 waves x 2 rows (16 x (64-2P) tile, 2 WGs/CU);
@@ -403,6 +439,18 @@ int kron_v3_launch(int variant, int pmax, bool is3d, int form, int epi, const Kr
         if (variant == 90) v3_launch_t<3, 2, 8, true, FORM_SUM, EPI_APPLY, 1, 1>(p, g, tc, omega, st);
         else v3_launch_t<3, 2, 8, true, FORM_SUM, EPI_APPLY, 1, 2>(p, g, tc, omega, st);
         return 0;
+    }
+    if (variant == 9) {   // v3 with whole-array buffer resources (arrays < 2 GiB)
+        const int64_t bytes = (int64_t)(g.n0 + 2 * g.pd0) * g.s0 * 8;
+        if (bytes < 0x7fffffffLL) {
+            switch (pmax) {
+                case 1: return v3_launch_p<1, 2, 8, 1, true>(is3d, form, epi, p, g, tc, omega, st);
+                case 2: return v3_launch_p<2, 2, 8, 1, true>(is3d, form, epi, p, g, tc, omega, st);
+                case 3: return v3_launch_p<3, 2, 8, 1, true>(is3d, form, epi, p, g, tc, omega, st);
+                case 4: return v3_launch_p<4, 2, 8, 1, true>(is3d, form, epi, p, g, tc, omega, st);
+                case 5: return v3_launch_p<5, 2, 8, 1, true>(is3d, form, epi, p, g, tc, omega, st);
+            }
+        }
     }
     if (variant == 6) {
         switch (pmax) {

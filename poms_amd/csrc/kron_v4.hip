@@ -52,15 +52,15 @@ __device__ __forceinline__ void wait_vm() {
     __builtin_amdgcn_s_waitcnt((N & 15) | (7 << 4) | (15 << 8) | ((N >> 4) << 14));
 }
 
-template <int P, int NW, bool IS3D, int FORM, int EPI, int MODE = 0, bool EXDPP = true>
-__global__ void __launch_bounds__(NW * 64, (2 * NW * 64) / 256)
+template <int P, int NW, bool IS3D, int FORM, int EPI, int MODE = 0, bool EXDPP = true, int MINW = (2 * NW * 64) / 256, int DFORCE = 0>
+__global__ void __launch_bounds__(NW * 64, MINW)
 kron_v4_kernel(const double* __restrict__ x, double* __restrict__ y,
                const double* __restrict__ bvec,
                const double* __restrict__ a0t, const double* __restrict__ b0t,
                const double* __restrict__ a1, const double* __restrict__ b1,
                const double* __restrict__ a2, const double* __restrict__ b2,
-               double* __restrict__ partial, const KronGeom g, const ToepConst tc,
-               const double omega) {
+               double* __restrict__ partial, double* __restrict__ partial2, const KronGeom g,
+               const ToepConst tc, const double omega) {
     constexpr int W = 2 * P + 1;
     constexpr int NT = NW * 64;
     constexpr int TO = 64 - 2 * P;      // output columns per tile
@@ -73,7 +73,7 @@ kron_v4_kernel(const double* __restrict__ x, double* __restrict__ y,
     constexpr bool XIN = (EPI == EPI_JACOBI) && IS3D;
     // x ring depth: apply 4 (3 planes in flight); with a b ring the b DMA of the
     // next plane anchors the wait, so 3 is all the depth that can be used
-    constexpr int D = IS3D ? (HASB ? 3 : 4) : 1;
+    constexpr int D = IS3D ? (DFORCE ? DFORCE : (HASB ? 3 : 4)) : 1;
     constexpr int PFX = D - 1;                      // x prefetch distance (planes)
     constexpr int DB = IS3D ? 2 : 1;               // b ring depth
     constexpr int BSLOT = (XIN ? 2 : 1) * T1 * 64; // b rows (+ x_in rows)
@@ -154,7 +154,7 @@ kron_v4_kernel(const double* __restrict__ x, double* __restrict__ y,
 
     // ---- LDS-DMA issue (counts per wave: x 1 or 2 (waves < P), b 1) ----
     auto dma_x = [&](int m, int slot) {
-        if constexpr (MODE == 2) return;
+        if constexpr (MODE == 2 || MODE == 7) return;
         const int sp = IS3D ? m + g.pd0 : 0;
         const bool ok = (sp >= 0) && (sp < nsp);
         const __amdgpu_buffer_rsrc_t rs =
@@ -170,7 +170,7 @@ kron_v4_kernel(const double* __restrict__ x, double* __restrict__ y,
         }
     };
     auto dma_b = [&](int zo, int slot) {
-        if constexpr (MODE == 2) return;
+        if constexpr (MODE == 2 || MODE == 7) return;
         const int sp = zo + g.pd0;
         const bool ok = (sp >= 0) && (sp < nsp);
         const __amdgpu_buffer_rsrc_t rs =
@@ -190,7 +190,7 @@ kron_v4_kernel(const double* __restrict__ x, double* __restrict__ y,
     double acc[NS][2];
 #pragma unroll
     for (int s = 0; s < NS; ++s) { acc[s][0] = 0.0; acc[s][1] = 0.0; }
-    double nrm = 0.0;
+    double nrm = 0.0, dotp = 0.0;
 
     const int exo = EX_OFF + wv * 128;   // this wave's exchange slot
 
@@ -208,7 +208,7 @@ kron_v4_kernel(const double* __restrict__ x, double* __restrict__ y,
             if (t < nplanes) {
                 // ---- x(t) and b(t) landed (own DMA), then everyone's
                 // issue order per iteration: b(t+1) [x_in(t+1)], x(t+PFX), 2 stores
-                if constexpr (MODE == 2) {
+                if constexpr (MODE == 2 || MODE == 7) {
                 } else if constexpr (!IS3D) {
                     wait_vm<0>();
                 } else if constexpr (HASB) {
@@ -222,7 +222,7 @@ kron_v4_kernel(const double* __restrict__ x, double* __restrict__ y,
                     else if (wv < P) wait_vm<(PFX - 1) * (2 + 2) + 2>();
                     else wait_vm<(PFX - 1) * (1 + 2) + 2>();
                 }
-                if constexpr (MODE != 4) __builtin_amdgcn_s_barrier();
+                if constexpr (MODE != 4 && MODE != 7) __builtin_amdgcn_s_barrier();
                 // ---- prefetch (dummies past the end keep the counts fixed)
                 if constexpr (IS3D) {
                     if constexpr (HASB) dma_b(zo_of(t + 1), (t + 1) & 1);
@@ -470,6 +470,8 @@ kron_v4_kernel(const double* __restrict__ x, double* __restrict__ y,
                         outv[1] = xin1 + dr1;
                         nrm = (en && row_ok && col_ok[0]) ? fma(dr0, dr0, nrm) : nrm;
                         nrm = (en && row_ok && col_ok[1]) ? fma(dr1, dr1, nrm) : nrm;
+                        dotp = (en && row_ok && col_ok[0]) ? fma(outv[0], bv.x, dotp) : dotp;
+                        dotp = (en && row_ok && col_ok[1]) ? fma(outv[1], bv.y, dotp) : dotp;
                     }
                 }
                 const __amdgpu_buffer_rsrc_t ys = make_rsrc(y + (int64_t)sp * g.s0, plane_bytes(nsp - sp, g.s0));
@@ -477,7 +479,7 @@ kron_v4_kernel(const double* __restrict__ x, double* __restrict__ y,
 #pragma unroll
                 for (int e = 0; e < 2; ++e) {
                     const bool ok = en && row_ok && col_ok[e];
-                    if constexpr (MODE == 2) {
+                    if constexpr (MODE == 2 || MODE == 7) {
                         if (outv[e] == 12345.678) bstore(ys, ok ? obase + 8 * e : 0x7ffffff0, outv[e]);
                     } else {
                         bstore(ys, ok ? obase + 8 * e : 0x7ffffff0, outv[e]);
@@ -500,6 +502,18 @@ kron_v4_kernel(const double* __restrict__ x, double* __restrict__ y,
                 partial[blockIdx.x] = s;
             }
         }
+        if (partial2 != nullptr) {
+#pragma unroll
+            for (int off = 32; off > 0; off >>= 1) dotp += __shfl_xor(dotp, off, 64);
+            __syncthreads();
+            if (lane == 0) lds[RED_OFF + wv] = dotp;
+            __syncthreads();
+            if (tid == 0) {
+                double s = 0.0;
+                for (int w = 0; w < NW; ++w) s += lds[RED_OFF + w];
+                partial2[blockIdx.x] = s;
+            }
+        }
     }
 }
 
@@ -508,7 +522,7 @@ static void v4_launch_t(const KronPtrs& p, const KronGeom& g, const ToepConst& t
                         hipStream_t st) {
     const int nblk = g.tiles2 * g.tiles1 * g.nchunks;
     hipLaunchKernelGGL((kron_v4_kernel<P, NW, IS3D, FORM, EPI>), dim3(nblk), dim3(NW * 64), 0, st,
-                       p.x, p.y, p.b, p.a0t, p.b0t, p.a1, p.b1, p.a2, p.b2, p.partial, g, tc, omega);
+                       p.x, p.y, p.b, p.a0t, p.b0t, p.a1, p.b1, p.a2, p.b2, p.partial, p.partial2, g, tc, omega);
 }
 
 template <int P, bool IS3D, int FORM>
@@ -541,22 +555,31 @@ int kron_v4_launch(int pmax, bool is3d, int form, int epi, const KronPtrs& p, co
         const int nblk = g.tiles2 * g.tiles1 * g.nchunks;
         if (diag_mode == 1)
             hipLaunchKernelGGL((kron_v4_kernel<3, 8, true, FORM_SUM, EPI_APPLY, 1>), dim3(nblk), dim3(512), 0, st,
-                               p.x, p.y, p.b, p.a0t, p.b0t, p.a1, p.b1, p.a2, p.b2, p.partial, g, tc, omega);
+                               p.x, p.y, p.b, p.a0t, p.b0t, p.a1, p.b1, p.a2, p.b2, p.partial, p.partial2, g, tc, omega);
         else if (diag_mode == 3)
             hipLaunchKernelGGL((kron_v4_kernel<3, 8, true, FORM_SUM, EPI_APPLY, 3>), dim3(nblk), dim3(512), 0, st,
-                               p.x, p.y, p.b, p.a0t, p.b0t, p.a1, p.b1, p.a2, p.b2, p.partial, g, tc, omega);
+                               p.x, p.y, p.b, p.a0t, p.b0t, p.a1, p.b1, p.a2, p.b2, p.partial, p.partial2, g, tc, omega);
         else if (diag_mode == 4)
             hipLaunchKernelGGL((kron_v4_kernel<3, 8, true, FORM_SUM, EPI_APPLY, 4>), dim3(nblk), dim3(512), 0, st,
-                               p.x, p.y, p.b, p.a0t, p.b0t, p.a1, p.b1, p.a2, p.b2, p.partial, g, tc, omega);
+                               p.x, p.y, p.b, p.a0t, p.b0t, p.a1, p.b1, p.a2, p.b2, p.partial, p.partial2, g, tc, omega);
         else if (diag_mode == 5)
             hipLaunchKernelGGL((kron_v4_kernel<3, 8, true, FORM_SUM, EPI_APPLY, 5>), dim3(nblk), dim3(512), 0, st,
-                               p.x, p.y, p.b, p.a0t, p.b0t, p.a1, p.b1, p.a2, p.b2, p.partial, g, tc, omega);
+                               p.x, p.y, p.b, p.a0t, p.b0t, p.a1, p.b1, p.a2, p.b2, p.partial, p.partial2, g, tc, omega);
+        else if (diag_mode == 8)   // 3 workgroups per CU: 6 waves/SIMD, 3-deep ring
+            hipLaunchKernelGGL((kron_v4_kernel<3, 8, true, FORM_SUM, EPI_APPLY, 0, true, 6, 3>), dim3(nblk), dim3(512), 0, st,
+                               p.x, p.y, p.b, p.a0t, p.b0t, p.a1, p.b1, p.a2, p.b2, p.partial, p.partial2, g, tc, omega);
+        else if (diag_mode == 9)   // 5 waves/SIMD
+            hipLaunchKernelGGL((kron_v4_kernel<3, 8, true, FORM_SUM, EPI_APPLY, 0, true, 5, 3>), dim3(nblk), dim3(512), 0, st,
+                               p.x, p.y, p.b, p.a0t, p.b0t, p.a1, p.b1, p.a2, p.b2, p.partial, p.partial2, g, tc, omega);
+        else if (diag_mode == 7)
+            hipLaunchKernelGGL((kron_v4_kernel<3, 8, true, FORM_SUM, EPI_APPLY, 7>), dim3(nblk), dim3(512), 0, st,
+                               p.x, p.y, p.b, p.a0t, p.b0t, p.a1, p.b1, p.a2, p.b2, p.partial, p.partial2, g, tc, omega);
         else if (diag_mode == 6)
             hipLaunchKernelGGL((kron_v4_kernel<3, 8, true, FORM_SUM, EPI_APPLY, 6>), dim3(nblk), dim3(512), 0, st,
-                               p.x, p.y, p.b, p.a0t, p.b0t, p.a1, p.b1, p.a2, p.b2, p.partial, g, tc, omega);
+                               p.x, p.y, p.b, p.a0t, p.b0t, p.a1, p.b1, p.a2, p.b2, p.partial, p.partial2, g, tc, omega);
         else
             hipLaunchKernelGGL((kron_v4_kernel<3, 8, true, FORM_SUM, EPI_APPLY, 2>), dim3(nblk), dim3(512), 0, st,
-                               p.x, p.y, p.b, p.a0t, p.b0t, p.a1, p.b1, p.a2, p.b2, p.partial, g, tc, omega);
+                               p.x, p.y, p.b, p.a0t, p.b0t, p.a1, p.b1, p.a2, p.b2, p.partial, p.partial2, g, tc, omega);
         return 0;
     }
     switch (pmax) {

@@ -258,7 +258,7 @@ int poms_op_destroy(poms_op* o) {
 }
 
 int poms_op_set_variant(poms_op* op, int variant) {
-    if (!op || variant < 0 || (variant > 8 && (variant < 90 || variant > 97))) { set_error("poms_op_set_variant: bad argument"); return 1; }
+    if (!op || variant < 0 || (variant > 9 && (variant < 90 || variant > 100))) { set_error("poms_op_set_variant: bad argument"); return 1; }
     if (variant > 0 && !op->v2_ok) { set_error("poms_op_set_variant: variant needs pads == pmax"); return 1; }
     if (variant == 5 && op->pmax > 3) variant = 4;  // 32-row tile does not fit LDS at p >= 4
     op->variant = variant;
@@ -309,24 +309,32 @@ static int op_geom(poms_op* o, int64_t zb, int64_t ze, KronGeom& g) {
     return 0;
 }
 
+// variants whose Jacobi epilogue also accumulates x_out . b (v3 and v4 kernels)
+static bool fused_dot_ok(const poms_op* o) { return o->variant >= 4 && o->variant <= 9; }
+
 static int op_run(poms_op* o, int epi, double omega, const double* x, double* y, const double* b,
-                  int64_t zb, int64_t ze, int want_norm, void* stream) {
+                  int64_t zb, int64_t ze, int want_norm, void* stream, int want_dot = 0) {
     if (!o || !x || !y) { set_error("null operator or vector"); return 1; }
     if (epi != EPI_APPLY && !b) { set_error("null right-hand side"); return 1; }
+    if (want_dot && (epi != EPI_JACOBI || !fused_dot_ok(o))) {
+        set_error("fused x_out.b needs a Jacobi sweep on kernel variants 4-9");
+        return 1;
+    }
     KronGeom g;
     if (op_geom(o, zb, ze, g)) return 1;
     const int64_t nblk = (int64_t)g.tiles2 * g.tiles1 * g.nchunks;
     if (nblk == 0) { o->last_partials = 0; return 0; }
-    if (want_norm && nblk > kScratch) { set_error("too many blocks for norm scratch"); return 1; }
+    if ((want_norm || want_dot) && 2 * nblk > kScratch) { set_error("too many blocks for the partial-sum scratch"); return 1; }
     KronPtrs p{x, y, b, o->a0t, o->b0t, o->a1, o->b1, o->a2, o->b2,
-               want_norm ? o->ctx->scratch : nullptr};
+               want_norm ? o->ctx->scratch : nullptr, want_dot ? o->ctx->scratch + nblk : nullptr};
     // variant 8 (default when pads == pmax): the fastest measured kernel per
-    // epilogue -- v4 (7) for apply / residual at p <= 3, v3 (4) otherwise
+    // epilogue -- v4 (7) for apply / residual at p <= 3, v3 with whole-array
+    // buffer resources (9; falls back to 4 for arrays >= 2 GiB) otherwise
     int v = o->variant;
-    if (v == 8) v = (epi != EPI_JACOBI && o->pmax <= 3) ? 7 : 4;
+    if (v == 8) v = (epi != EPI_JACOBI && o->pmax <= 3) ? 7 : 9;
     const int rc = v == 0
         ? kron_launch(o->pmax, o->ndim == 3, o->form, epi, p, g, omega, as_stream(stream))
-        : (v == 7 || (v >= 92 && v <= 97))
+        : (v == 7 || (v >= 92 && v <= 100))
         ? kron_v4_launch(o->pmax, o->ndim == 3, o->form, epi, p, g, o->tc, omega, as_stream(stream),
                          v == 7 ? 0 : v - 91)
         : v >= 4
@@ -334,7 +342,7 @@ static int op_run(poms_op* o, int epi, double omega, const double* x, double* y,
         : kron_v2_launch(v, o->pmax, o->ndim == 3, o->form, epi, p, g, o->tc, omega, as_stream(stream));
     if (rc) return 1;
     POMS_HIP_CHECK(hipGetLastError());
-    o->last_partials = want_norm ? nblk : 0;
+    o->last_partials = (want_norm || want_dot) ? nblk : 0;
     return 0;
 }
 
@@ -351,6 +359,18 @@ int poms_op_jacobi_sweep(poms_op* op, double omega, const double* b, const doubl
                          double* x_out, int64_t zb, int64_t ze, int want_norm, void* stream) {
     if (x_in == x_out) { set_error("jacobi sweep: x_out must not alias x_in"); return 1; }
     return op_run(op, EPI_JACOBI, omega, x_in, x_out, b, zb, ze, want_norm, stream);
+}
+
+int poms_op_jacobi_sweep_dot(poms_op* op, double omega, const double* b, const double* x_in,
+                             double* x_out, int64_t zb, int64_t ze, int want_norm, void* stream) {
+    if (x_in == x_out) { set_error("jacobi sweep: x_out must not alias x_in"); return 1; }
+    return op_run(op, EPI_JACOBI, omega, x_in, x_out, b, zb, ze, want_norm, stream, 1);
+}
+
+int poms_op_fused_dot_supported(poms_op* op, int* yes) {
+    if (!op || !yes) { set_error("poms_op_fused_dot_supported: null argument"); return 1; }
+    *yes = fused_dot_ok(op) ? 1 : 0;
+    return 0;
 }
 
 int poms_op_diag_scale(poms_op* o, double scale, const double* b, double* x, int want_norm,
@@ -377,7 +397,7 @@ int poms_op_profile_phases(poms_op* o, int jacobi, const double* b, const double
     if (op_geom(o, 0, o->L.n[0], g)) return 1;
     const int64_t nblk = (int64_t)g.tiles2 * g.tiles1 * g.nchunks;
     *nwaves = nblk * (o->variant == 2 ? 8 : 4);
-    KronPtrs p{x, y, b, o->a0t, o->b0t, o->a1, o->b1, o->a2, o->b2, nullptr};
+    KronPtrs p{x, y, b, o->a0t, o->b0t, o->a1, o->b1, o->a2, o->b2, nullptr, nullptr};
     kron_v2_stamps(o->variant, jacobi ? EPI_JACOBI : EPI_APPLY, p, g, o->tc, 2.0 / 3.0,
                    reinterpret_cast<unsigned long long*>(dbg), as_stream(stream));
     POMS_HIP_CHECK(hipGetLastError());
@@ -488,8 +508,15 @@ int poms_pcg_update(poms_ctx* ctx, const poms_layout* L, double alpha, double* x
 }
 
 int poms_reduce_partials(poms_ctx* ctx, int64_t count, double* out_dev, void* stream) {
-    if (!ctx || !out_dev || count < 0 || count > kScratch) { set_error("reduce: bad argument"); return 1; }
-    reduce_launch(ctx->scratch, (int)count, out_dev, as_stream(stream));
+    return poms_reduce_partials_at(ctx, 0, count, out_dev, stream);
+}
+
+int poms_reduce_partials_at(poms_ctx* ctx, int64_t offset, int64_t count, double* out_dev, void* stream) {
+    if (!ctx || !out_dev || count < 0 || offset < 0 || offset + count > kScratch) {
+        set_error("reduce: bad argument");
+        return 1;
+    }
+    reduce_launch(ctx->scratch + offset, (int)count, out_dev, as_stream(stream));
     POMS_HIP_CHECK(hipGetLastError());
     return 0;
 }

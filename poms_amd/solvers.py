@@ -18,7 +18,9 @@ Differences that do not change results:
   fused HIP kernel; the first sweep from ``x0 = None`` uses ``A.0 = 0``
   exactly and launches the diagonal scaling alone;
 * with ``tol == 0`` the norms that can never stop the iteration are not
-  computed (no host synchronisation).
+  computed (no host synchronisation);
+* inside ``pcg`` with this module's ``damped_jacobi`` as ``psolve``, ``s.dot(r)``
+  is accumulated by the final smoothing sweep (``poms_op_jacobi_sweep_dot``).
 
 Inputs must be :mod:`poms_amd.stencil` device objects; there is no CPU path.
 """
@@ -61,9 +63,8 @@ def pcg(A, psolve, b, x0=None, tol=1e-6, maxiter=100, verbose=False):
         r = A.residual(b, x)
 
     nrmr0 = sqrt(r.dot(r))
-    s = psolve(A, r)
+    s, sr = _psolve_dot(A, psolve, r)
     p = s
-    sr = s.dot(r)
     q = V.empty()
 
     if verbose:
@@ -79,9 +80,8 @@ def pcg(A, psolve, b, x0=None, tol=1e-6, maxiter=100, verbose=False):
         if nrmr < tol * nrmr0:
             k -= 1
             break
-        s = psolve(A, r)
         srold = sr
-        sr = s.dot(r)
+        s, sr = _psolve_dot(A, psolve, r)
         beta = sr / srold
         if p is s:
             raise RuntimeError("psolve returned its input buffer")
@@ -93,6 +93,18 @@ def pcg(A, psolve, b, x0=None, tol=1e-6, maxiter=100, verbose=False):
         print("+---------+---------------------+")
     info = {"niter": k, "success": nrmr < tol * nrmr0, "res_norm": sqrt(nrmr)}
     return x, info
+
+
+def _psolve_dot(A, psolve, r):
+    """``s = psolve(A, r)`` and ``s.dot(r)``; for this module's damped_jacobi the dot is
+    accumulated by the last smoothing sweep itself (same values, one pass less)."""
+    if psolve is damped_jacobi and A.fused_dot_supported:
+        s, sr = _damped_jacobi(A, r, want_dot=True)
+        if sr is not None:
+            return s, sr
+        return s, s.dot(r)
+    s = psolve(A, r)
+    return s, s.dot(r)
 
 
 def _pcg_update(V, alpha, x, p, r, q) -> float:
@@ -117,6 +129,12 @@ def jacobi(A, b):
 
 def damped_jacobi(A, b, x0=None, tol=1e-6, maxiter=10, verbose=False):
     """Weighted Jacobi, omega = 2/3 (`sources/solvers.py:167-235`); returns x."""
+    return _damped_jacobi(A, b, x0, tol, maxiter, verbose)[0]
+
+
+def _damped_jacobi(A, b, x0=None, tol=1e-6, maxiter=10, verbose=False, want_dot=False):
+    """damped_jacobi; with ``want_dot`` also returns ``x.b`` accumulated by the final
+    sweep (None when the last sweep was not a full sweep)."""
     _check(A, b)
     V = b.space
     omega = OMEGA
@@ -129,14 +147,14 @@ def damped_jacobi(A, b, x0=None, tol=1e-6, maxiter=10, verbose=False):
     k0 = 1
     if x0 is None:
         if maxiter < 1:
-            return V.zeros()
+            return V.zeros(), None
         # k = 1 from x = 0:  r = b - A.0 = b,  dr = omega b / diag,  x = dr
         x = V.empty()
         nrmr = A.diag_scale(b, x, omega, want_norm=need)
         if need and nrmr < tol_sqr:
             if verbose:
                 print("+---------+---------------------+")
-            return x
+            return x, None
         if verbose:
             print(template.format(1, sqrt(nrmr)))
         k0 = 2
@@ -144,10 +162,14 @@ def damped_jacobi(A, b, x0=None, tol=1e-6, maxiter=10, verbose=False):
         assert x0.shape == (A.shape[0],)
         x = x0.copy()
 
+    dot = None
     if maxiter >= k0:
         xn = V.empty()
         for k in range(k0, maxiter + 1):
-            nrmr = A.jacobi_sweep(b, x, xn, omega, want_norm=need)
+            if want_dot and k == maxiter:   # the last sweep also forms x_out . b
+                nrmr, dot = A.jacobi_sweep(b, x, xn, omega, want_norm=need, want_dot=True)
+            else:
+                nrmr = A.jacobi_sweep(b, x, xn, omega, want_norm=need)
             x, xn = xn, x
             if need and nrmr < tol_sqr:
                 break
@@ -155,4 +177,4 @@ def damped_jacobi(A, b, x0=None, tol=1e-6, maxiter=10, verbose=False):
                 print(template.format(k, sqrt(nrmr)))
     if verbose:
         print("+---------+---------------------+")
-    return x
+    return x, dot

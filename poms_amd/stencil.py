@@ -475,7 +475,7 @@ class KronOperator:
             if not isinstance(v, StencilVector) or v.space is not self.space:
                 raise TypeError("vector does not belong to this operator's space")
 
-    def _launch(self, fn, x: StencilVector, *args, want_norm=False, norm_buf=None, kind="apply"):
+    def _launch(self, fn, x: StencilVector, *args, want_norm=False, norm_buf=None, kind="apply", want_dot=False):
         """Run one kernel over all local planes; overlap the RCCL ghost exchange
         with the interior planes when x's ghosts are stale."""
         V = self.space
@@ -504,10 +504,14 @@ class KronOperator:
                 self.timer.append((kind, e0, e1))
             else:
                 fn(*args, zb, ze, st)
-            if want_norm:
+            if want_norm or want_dot:
                 cnt = C.c_int64()
                 _lib.call("poms_op_last_partials", self._h, C.byref(cnt))
-                _lib.call("poms_reduce_partials", V.ctx, cnt.value, rt.ptr(norm_buf[idx:idx + 1]), st)
+                if want_norm:
+                    _lib.call("poms_reduce_partials", V.ctx, cnt.value, rt.ptr(norm_buf[idx:idx + 1]), st)
+                if want_dot:   # x_out . b partials follow the norm partials (slots 4..)
+                    _lib.call("poms_reduce_partials_at", V.ctx, cnt.value, cnt.value,
+                              rt.ptr(norm_buf[4 + idx:5 + idx]), st)
                 total += 1
         if handle is not None:
             V.dist.finish_exchange(handle)
@@ -543,21 +547,36 @@ class KronOperator:
         r._mark_written()
         return r
 
+    @property
+    def fused_dot_supported(self) -> bool:
+        v = C.c_int()
+        _lib.call("poms_op_fused_dot_supported", self._h, C.byref(v))
+        return bool(v.value)
+
     def jacobi_sweep(self, b: StencilVector, x_in: StencilVector, x_out: StencilVector,
-                     omega: float, want_norm: bool = False):
-        """x_out = x_in + omega (b - A x_in)/diag(A); returns global ||dr||^2 or None."""
+                     omega: float, want_norm: bool = False, want_dot: bool = False):
+        """x_out = x_in + omega (b - A x_in)/diag(A).
+
+        Returns the global ``||dr||^2`` (or None); with ``want_dot`` returns
+        ``(||dr||^2 or None, x_out . b)``, the dot fused into the sweep.
+        """
         self._check(b, x_in, x_out)
         if x_in is x_out:
             raise ValueError("x_out must not alias x_in")
         V = self.space
         nb = V.scalar_buffer()
+        name = "poms_op_jacobi_sweep_dot" if want_dot else "poms_op_jacobi_sweep"
 
         def fn(zb, ze, st):
-            _lib.call("poms_op_jacobi_sweep", self._h, float(omega), rt.ptr(b._data), rt.ptr(x_in._data),
+            _lib.call(name, self._h, float(omega), rt.ptr(b._data), rt.ptr(x_in._data),
                       rt.ptr(x_out._data), zb, ze, int(want_norm), st)
 
-        n = self._launch(fn, x_in, want_norm=want_norm, norm_buf=nb, kind="jacobi")
+        n = self._launch(fn, x_in, want_norm=want_norm, norm_buf=nb, kind="jacobi", want_dot=want_dot)
         x_out._mark_written()
+        if want_dot:
+            host = nb.cpu()   # one read for both reductions
+            nrm = V.global_dot(float(host[:n].sum())) if want_norm else None
+            return nrm, V.global_dot(float(host[4:4 + n].sum()))
         if not want_norm:
             return None
         return V.global_dot(float(nb[:n].sum().item()))

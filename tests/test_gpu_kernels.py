@@ -49,7 +49,7 @@ CASES = [
 ]
 
 
-VARIANTS = [0, 1, 2, 3, 4, 5, 6, 7, 8]
+VARIANTS = [0, 1, 2, 3, 4, 5, 6, 7, 8, 9]
 
 
 @pytest.mark.parametrize("ndim,cells,p", CASES)
@@ -178,3 +178,29 @@ def test_diag_scale_and_first_sweep(gpu):
     ref = (2.0 / 3.0) * b / orc.kron_sum_diag(M, K)
     assert rel(out.to_local_numpy(), ref) <= 1e-15
     assert abs(nrm - float(np.vdot(ref, ref))) <= 1e-12 * float(np.vdot(ref, ref))
+
+
+@pytest.mark.parametrize("variant", [4, 7, 8, 9])
+@pytest.mark.parametrize("ndim,cells,p", [(3, (25, 18, 70), 3), (2, (64, 64), 3), (3, (14, 12, 66), 5)])
+def test_jacobi_sweep_fused_dot(gpu, variant, ndim, cells, p):
+    """poms_op_jacobi_sweep_dot: same x_out as the plain sweep, x_out.b == StencilVector.dot."""
+    from poms_amd.stencil import KronOperator
+    rng = np.random.default_rng(3)
+    F = [assemble_1d(uniform_knots(p, N), p) for N in cells]
+    n = [N + p for N in cells]
+    V = _space(n, [p] * ndim)
+    A = KronOperator.laplace(V, [f[0] for f in F], [f[1] for f in F])
+    A.set_variant(variant)
+    assert A.fused_dot_supported
+    x, b = V.zeros().from_numpy(rng.standard_normal(n)), V.zeros().from_numpy(rng.standard_normal(n))
+    y1, y2 = V.zeros(), V.zeros()
+    nrm1 = A.jacobi_sweep(b, x, y1, 2.0 / 3.0, want_norm=True)
+    nrm2, dot = A.jacobi_sweep(b, x, y2, 2.0 / 3.0, want_norm=True, want_dot=True)
+    np.testing.assert_array_equal(y1.to_local_numpy(), y2.to_local_numpy())
+    assert abs(nrm1 - nrm2) <= 1e-14 * abs(nrm1)
+    want = float(np.vdot(y1.to_local_numpy(), b.to_local_numpy()))
+    assert abs(dot - want) <= 1e-12 * (abs(want) + np.linalg.norm(y1.to_local_numpy()) * np.linalg.norm(b.to_local_numpy()))
+    _, dot_only = A.jacobi_sweep(b, x, y2, 2.0 / 3.0, want_norm=False, want_dot=True)
+    assert abs(dot_only - dot) <= 1e-14 * abs(dot) + 1e-300
+    A.set_variant(0)
+    assert not A.fused_dot_supported
