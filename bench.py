@@ -46,8 +46,9 @@ def parse():
     ap.add_argument("--cpu-cells", type=int, default=160)
     ap.add_argument("--cpu-cycles", type=int, default=3)
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--pmc-json", type=str, default="",
-                    help="rocprofv3 PMC summary (bytes per launch) to fill roofline.traffic")
+    ap.add_argument("--pmc-json", type=str, default=str(ROOT / "profiles" / "r01" / "pmc_traffic_jacobi.json"),
+                    help="tools/pmc_traffic.py summary of a separate rocprofv3 --pmc pass "
+                         "(FETCH_SIZE x2 + WRITE_SIZE per launch) used for roofline.traffic")
     return ap.parse_args()
 
 
@@ -99,13 +100,16 @@ def main():
         dt = float(t.item())
     sec_per_cycle = dt / args.steps
 
-    # per-launch kernel durations inside the timed region (events on the launch stream)
-    per_kind = {}
-    for kind, e0, e1 in timer:
-        per_kind.setdefault(kind, []).append(e0.elapsed_time(e1) * 1e-3)
-    jac = per_kind.get("jacobi", [])
-    n_launch_per_sweep = 1 if world == 1 else 3
-    sweep_s = sum(jac) / max(1, len(jac) // n_launch_per_sweep)
+    # per-launch kernel durations inside the timed region (events on the launch stream);
+    # one operator call is 1 launch, or 3 when the halo exchange overlaps the interior planes
+    def per_call(entries, want):
+        calls = {}
+        for kind, e0, e1, call in entries:
+            if kind == want:
+                calls[call] = calls.get(call, 0.0) + e0.elapsed_time(e1) * 1e-3
+        return sum(calls.values()) / max(1, len(calls)), len(calls)
+
+    sweep_s, n_sweeps = per_call(timer, "jacobi")
     bytes_sweep = 24.0 * local_dof
     achieved = bytes_sweep / sweep_s / 1e9 if sweep_s > 0 else 0.0
 
@@ -122,9 +126,8 @@ def main():
     for _ in range(args.kron_reps):
         A.dot(xv, out=yk)
     barrier()
-    kt = [e0.elapsed_time(e1) * 1e-3 for _, e0, e1 in A.timer]
+    kron_s, _ = per_call(A.timer, "apply")
     A.timer = None
-    kron_s = sum(kt) / max(1, len(kt) // n_launch_per_sweep)
     kron_gbps = 16.0 * local_dof / kron_s / 1e9 if kron_s > 0 else 0.0
     if world > 1:
         t = torch.tensor([achieved, kron_gbps], dtype=torch.float64, device="cuda")
@@ -134,7 +137,8 @@ def main():
     traffic = None
     if args.pmc_json and Path(args.pmc_json).exists():
         pm = json.loads(Path(args.pmc_json).read_text())
-        traffic = pm.get("hbm_bytes_per_launch")
+        if pm.get("bytes_per_dof"):   # per-DOF HBM bytes of the same kernel, scaled to this rank's slab
+            traffic = pm["bytes_per_dof"] * local_dof
 
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
@@ -171,11 +175,12 @@ def main():
                 "parallelism": f"slab{world}",
             },
             "roofline": {
-                "kernel": f"kron_v3_kernel<P={args.p},3D,SUM,JACOBI> (variant {A.variant}: Kron apply + damped-Jacobi update)",
+                "kernel": (f"kron_v3_kernel<P={args.p},3D,SUM,JACOBI> (operator variant {A.variant} = auto: v3 with "
+                           f"whole-array buffer resources; Kron apply + damped-Jacobi update)"),
                 "bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBPS, "unit": "GB/s",
                 "frac": achieved / HBM_PEAK_GBPS, "traffic": traffic,
                 "algorithmic_bytes_per_launch": bytes_sweep, "avg_launch_us": sweep_s * 1e6,
-                "launches_timed": len(jac),
+                "launches_timed": n_sweeps,
             },
             "kron_spmv": {"achieved": kron_gbps, "unit": "GB/s", "frac": kron_gbps / HBM_PEAK_GBPS,
                           "avg_launch_us": kron_s * 1e6, "bytes_per_dof": 16},

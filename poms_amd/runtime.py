@@ -89,9 +89,11 @@ class Comm:
         return t
 
     def allreduce_scalar(self, v: float) -> float:
+        """Sum of one double over the ranks (a device tensor for RCCL: nccl has no CPU path)."""
         if not self.enabled:
             return v
-        t = torch.tensor([v], dtype=torch.float64)
+        dev = torch.device("cuda", torch.cuda.current_device()) if self.cuda_transport else torch.device("cpu")
+        t = torch.tensor([v], dtype=torch.float64, device=dev)
         import torch.distributed as dist
         dist.all_reduce(t, group=self.group)
         return float(t.item())

@@ -393,7 +393,8 @@ class KronOperator:
         n0g = V.npts[0] if nd == 3 else 1
         _lib.call("poms_op_create", V.ctx, 3 if nd == 3 else 2, C.byref(V.layout), cform, self.pmax,
                   farr, g0, n0g, C.byref(self._h))
-        self.timer = None  # list -> (kind, start_event, end_event) per kernel launch
+        self.timer = None  # list -> (kind, start_event, end_event, call) per kernel launch
+        self._calls = 0    # operator calls (one call = 1 launch, or 3 when a halo exchange is overlapped)
 
     # -- constructors ------------------------------------------------------------
     @classmethod
@@ -492,6 +493,7 @@ class KronOperator:
                 V.dist.finish_exchange(handle)
                 handle = None
         total = 0
+        self._calls += 1
         for idx, (zb, ze) in enumerate(ranges):
             if idx == 1 and handle is not None:
                 V.dist.finish_exchange(handle)
@@ -501,7 +503,7 @@ class KronOperator:
                 e0.record()
                 fn(*args, zb, ze, st)
                 e1.record()
-                self.timer.append((kind, e0, e1))
+                self.timer.append((kind, e0, e1, self._calls))
             else:
                 fn(*args, zb, ze, st)
             if want_norm or want_dot:

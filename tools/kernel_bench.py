@@ -73,7 +73,7 @@ def main():
                         ev.append((e0, e1))
                     torch.cuda.synchronize()
                     if A.timer:   # per-launch kernel events (operator kinds)
-                        ts = [e0.elapsed_time(e1) * 1e3 for _, e0, e1 in A.timer]
+                        ts = [e0.elapsed_time(e1) * 1e3 for _, e0, e1, _c in A.timer]
                     else:         # whole call (dot includes its reduction + host read)
                         ts = [e0.elapsed_time(e1) * 1e3 for e0, e1 in ev]
                     A.timer = None
