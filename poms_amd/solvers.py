@@ -144,19 +144,33 @@ def _damped_jacobi(A, b, x0=None, tol=1e-6, maxiter=10, verbose=False, want_dot=
         _print_header("Damped Jacobi method:")
         template = "| {:7d} | {:19.2e} |"
 
+    # Norms are read one sweep late: sweep k is queued before the host waits for
+    # ||dr_{k-1}||^2 (copied to pinned memory), so the GPU never idles on the stop
+    # test.  If sweep k-1 met it, x_{k-1} is returned -- sweep k wrote the other
+    # buffer -- exactly the reference's result (`sources/solvers.py:219-222`).
+    lazy = need and not verbose and V.lazy_reductions
+    pending = None                      # (LazyScalar of sweep k-1, buffer holding x_{k-1})
+
+    def settle(pend):
+        lz, xbuf = pend
+        return lz.value() < tol_sqr, xbuf
+
     k0 = 1
     if x0 is None:
         if maxiter < 1:
             return V.zeros(), None
         # k = 1 from x = 0:  r = b - A.0 = b,  dr = omega b / diag,  x = dr
         x = V.empty()
-        nrmr = A.diag_scale(b, x, omega, want_norm=need)
-        if need and nrmr < tol_sqr:
+        nrmr = A.diag_scale(b, x, omega, want_norm=need, lazy=lazy)
+        if lazy:
+            pending = (nrmr, x)
+        else:
+            if need and nrmr < tol_sqr:
+                if verbose:
+                    print("+---------+---------------------+")
+                return x, None
             if verbose:
-                print("+---------+---------------------+")
-            return x, None
-        if verbose:
-            print(template.format(1, sqrt(nrmr)))
+                print(template.format(1, sqrt(nrmr)))
         k0 = 2
     else:
         assert x0.shape == (A.shape[0],)
@@ -169,12 +183,22 @@ def _damped_jacobi(A, b, x0=None, tol=1e-6, maxiter=10, verbose=False, want_dot=
             if want_dot and k == maxiter:   # the last sweep also forms x_out . b
                 nrmr, dot = A.jacobi_sweep(b, x, xn, omega, want_norm=need, want_dot=True)
             else:
-                nrmr = A.jacobi_sweep(b, x, xn, omega, want_norm=need)
+                nrmr = A.jacobi_sweep(b, x, xn, omega, want_norm=need, lazy=lazy)
+            if pending is not None:         # stop test of the previous sweep
+                done, xprev = settle(pending)
+                pending = None
+                if done:
+                    return xprev, None
             x, xn = xn, x
+            if lazy and not (want_dot and k == maxiter):
+                pending = (nrmr, x)
+                continue
             if need and nrmr < tol_sqr:
                 break
             if verbose:
                 print(template.format(k, sqrt(nrmr)))
+    if pending is not None:             # the last sweep's test cannot change the result
+        pending[0].value()
     if verbose:
         print("+---------+---------------------+")
     return x, dot

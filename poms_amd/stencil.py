@@ -71,6 +71,7 @@ class StencilVectorSpace:
         self.device = rt.device_index(device)
         self.ctx = rt.ctx(self.device)
         self._scal = None
+        self._pinned = None
 
     # ------------------------------------------------------------------
     @property
@@ -101,6 +102,25 @@ class StencilVectorSpace:
             self._scal = torch.zeros(8, dtype=F64, device=f"cuda:{self.device}")
         return self._scal
 
+    @property
+    def lazy_reductions(self) -> bool:
+        """Global sums can stay on the device stream (single rank, or RCCL)."""
+        return not self.is_distributed or self.dist.cuda_transport
+
+    def lazy_sum(self, partial_sums: torch.Tensor) -> "LazyScalar":
+        """Global sum of device partial sums, copied to pinned host memory without
+        blocking the host; ``.value()`` waits for that copy only."""
+        tot = partial_sums.sum().reshape(1)
+        if self.is_distributed:
+            import torch.distributed as dist
+            dist.all_reduce(tot, group=self.dist.group)
+        if self._pinned is None:
+            self._pinned = torch.zeros(4, dtype=F64).pin_memory()
+            self._pin_next = 0
+        slot = self._pinned[self._pin_next:self._pin_next + 1]
+        self._pin_next = (self._pin_next + 1) % 4
+        return LazyScalar(tot, slot)
+
     def global_dot(self, local: float) -> float:
         if self.is_distributed:
             comm = rt.Comm.from_env(self.dist.group)
@@ -109,6 +129,20 @@ class StencilVectorSpace:
 
     def __repr__(self):
         return f"StencilVectorSpace(npts={self.npts}, pads={self.pads}, starts={self.starts}, ends={self.ends})"
+
+
+class LazyScalar:
+    """A device scalar being copied to pinned host memory on the launch stream."""
+
+    def __init__(self, dev_value: torch.Tensor, host_slot: torch.Tensor):
+        host_slot.copy_(dev_value, non_blocking=True)
+        self._ev = torch.cuda.Event()
+        self._ev.record()
+        self._host = host_slot
+
+    def value(self) -> float:
+        self._ev.synchronize()
+        return float(self._host[0])
 
 
 def _stream():
@@ -556,11 +590,13 @@ class KronOperator:
         return bool(v.value)
 
     def jacobi_sweep(self, b: StencilVector, x_in: StencilVector, x_out: StencilVector,
-                     omega: float, want_norm: bool = False, want_dot: bool = False):
+                     omega: float, want_norm: bool = False, want_dot: bool = False, lazy: bool = False):
         """x_out = x_in + omega (b - A x_in)/diag(A).
 
         Returns the global ``||dr||^2`` (or None); with ``want_dot`` returns
-        ``(||dr||^2 or None, x_out . b)``, the dot fused into the sweep.
+        ``(||dr||^2 or None, x_out . b)``, the dot fused into the sweep.  With
+        ``lazy`` (and ``want_norm``) the norm comes back as a :class:`LazyScalar`
+        so the host can queue the next sweep before reading it.
         """
         self._check(b, x_in, x_out)
         if x_in is x_out:
@@ -581,9 +617,12 @@ class KronOperator:
             return nrm, V.global_dot(float(host[4:4 + n].sum()))
         if not want_norm:
             return None
+        if lazy and V.lazy_reductions:
+            return V.lazy_sum(nb[:n])
         return V.global_dot(float(nb[:n].sum().item()))
 
-    def diag_scale(self, b: StencilVector, out: StencilVector, scale: float = 1.0, want_norm: bool = False):
+    def diag_scale(self, b: StencilVector, out: StencilVector, scale: float = 1.0, want_norm: bool = False,
+                   lazy: bool = False):
         """out = scale * b / diag(A); returns global ||out||^2 or None."""
         self._check(b, out)
         V = self.space
@@ -597,6 +636,8 @@ class KronOperator:
         _lib.call("poms_op_last_partials", self._h, C.byref(cnt))
         nb = V.scalar_buffer()
         _lib.call("poms_reduce_partials", V.ctx, cnt.value, rt.ptr(nb), st)
+        if lazy and V.lazy_reductions:
+            return V.lazy_sum(nb[0:1])
         return V.global_dot(float(nb[0].item()))
 
     # -- host-side views of the operator (set-up / API parity) --------------------
