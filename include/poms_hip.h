@@ -122,6 +122,16 @@ int poms_op_jacobi_sweep_dot(poms_op* op, double omega, const double* b,
                              const double* x_in, double* x_out, int64_t z_begin,
                              int64_t z_end, int want_norm, void* stream);
 int poms_op_fused_dot_supported(poms_op* op, int* yes);
+/* Sweeps 1 and 2 of damped_jacobi from x0 = 0 in one pass over b:
+ * x1 = omega b / diag(A) (poms_op_diag_scale) formed as the planes are read,
+ * x_out = x1 + omega (b - A x1) / diag(A).  With want_norm, ||dr_2||^2 partials
+ * go to scratch[0, count) and ||x1||^2 = ||dr_1||^2 partials to
+ * scratch[count, 2 count).  Replaces the first two iterations of
+ * `sources/solvers.py:207-219` (x0 = None).  3D, variants 8/9, arrays < 2 GiB
+ * (poms_op_from_zero_supported).                                              */
+int poms_op_jacobi_from_zero(poms_op* op, double omega, const double* b, double* x_out,
+                             int64_t z_begin, int64_t z_end, int want_norm, void* stream);
+int poms_op_from_zero_supported(poms_op* op, int* yes);
 /* x = scale * b / diag(A) on the interior.  With scale = 1 this is
  * `jacobi(A, b)` (`sources/solvers.py:139-163`); with scale = omega it is the
  * first damped-Jacobi sweep from x0 = 0 (A.0 = 0 exactly).                    */

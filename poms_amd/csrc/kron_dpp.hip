@@ -53,7 +53,12 @@ kron_v3_kernel(const double* __restrict__ x, double* __restrict__ y,
     constexpr int NS = IS3D ? W : 1;
     typedef double d2 __attribute__((ext_vector_type(2)));
 
-    constexpr bool XRING = (EPI == EPI_JACOBI) && IS3D;
+    // EPI_JACOBI0: the x planes are b; each loaded value becomes x1 = omega b / diag(A)
+    // (sweep 1 from x0 = 0), and the epilogue is sweep 2 -- x2 from one pass over b
+    constexpr bool J0 = (EPI == EPI_JACOBI0);
+    constexpr bool JAC = (EPI == EPI_JACOBI) || J0;
+    static_assert(!J0 || (IS3D && FLAT), "EPI_JACOBI0 is built for the 3D whole-array kernel");
+    constexpr bool XRING = JAC && IS3D;
     constexpr int NRING = P + 1;            // x planes kept for the Jacobi update
     __shared__ d2 ab_[SUM ? 2 * XRP * 64 : 1];
     // x of the tile's output rows for the last P+1 planes (the Jacobi epilogue's
@@ -169,7 +174,7 @@ kron_v3_kernel(const double* __restrict__ x, double* __restrict__ y,
             const uint32_t so = (uint32_t)(zo + g.pd0) * plane8;
 #pragma unroll
             for (int r = 0; r < R; ++r) eb[r] = bload_s(rb_all, obase + r * rowstep, so);
-            if constexpr (EPI == EPI_JACOBI && !XRING) {
+            if constexpr (JAC && !XRING) {
 #pragma unroll
                 for (int r = 0; r < R; ++r) ex[r] = bload_s(rx_all, obase + r * rowstep, so);
             }
@@ -179,7 +184,7 @@ kron_v3_kernel(const double* __restrict__ x, double* __restrict__ y,
             const __amdgpu_buffer_rsrc_t bs = make_rsrc(bvec + (int64_t)sp * g.s0, nb);
 #pragma unroll
             for (int r = 0; r < R; ++r) eb[r] = bload(bs, obase + r * rowstep);
-            if constexpr (EPI == EPI_JACOBI && !XRING) {
+            if constexpr (JAC && !XRING) {
                 const __amdgpu_buffer_rsrc_t xsr = make_rsrc(x + (int64_t)sp * g.s0, nb);
 #pragma unroll
                 for (int r = 0; r < R; ++r) ex[r] = bload(xsr, obase + r * rowstep);
@@ -191,7 +196,7 @@ kron_v3_kernel(const double* __restrict__ x, double* __restrict__ y,
         const int sp = zo + g.pd0;
         const __amdgpu_buffer_rsrc_t ys = make_rsrc(y + (int64_t)sp * g.s0, plane_bytes(nsp - sp, g.s0));
         double d0a = 1.0, d0b = 0.0;
-        if constexpr (EPI == EPI_JACOBI && IS3D) {
+        if constexpr (JAC && IS3D) {
             const int i0g = g.g0 + zo;
             d0a = a0t[(i0g + P) * W + P];
             if constexpr (SUM) d0b = b0t[(i0g + P) * W + P];
@@ -216,7 +221,8 @@ kron_v3_kernel(const double* __restrict__ x, double* __restrict__ y,
                 const double dr = omega * (eb[r] - v[r]) * rc;
                 outv = ex[r] + dr;
                 nrm = ok ? fma(dr, dr, nrm) : nrm;
-                dotp = ok ? fma(outv, eb[r], dotp) : dotp;   // x_out . b (pcg's s.r)
+                if constexpr (J0) dotp = ok ? fma(ex[r], ex[r], dotp) : dotp;   // ||x1||^2 = ||dr_1||^2
+                else dotp = ok ? fma(outv, eb[r], dotp) : dotp;                  // x_out . b (pcg's s.r)
             }
             if constexpr (MODE == 2) {
                 if (outv == 12345.678) bstore(ys, ok ? obase + r * rowstep : 0x7ffffff0, outv);
@@ -249,6 +255,27 @@ kron_v3_kernel(const double* __restrict__ x, double* __restrict__ y,
                 for (int j = 0; j < NRW; ++j) {
                     double sh[W];
                     sh[P] = xr[xb][j];
+                    if constexpr (J0) {
+                        // x1 = (omega b) / diag(A) at (plane m, row, column) -- the
+                        // diag_scale kernel's expression; clamped indices keep diag
+                        // finite where b is a zero ghost
+                        const int m = g.g0 + z0 - P + t;
+                        const int mc = min(max(m, 0), g.g0 + g.n0 + g.pd0 - 1);
+                        const double q0a = a0t[(mc + P) * W + P];
+                        const double q0b = SUM ? b0t[(mc + P) * W + P] : 0.0;
+                        const int row = min(max(r0 - P + wv + j * NW, 0), g.n1 - 1);
+                        const double q1a = a1[row * W + P];
+                        const double q1b = SUM ? b1[row * W + P] : 0.0;
+                        double dg = SUM ? q0a * (q1a * ca2[P]) + q0b * (q1b * ca2[P] + q1a * cb2[P])
+                                        : q0a * q1a * ca2[P];
+                        double rc = __builtin_amdgcn_rcp(dg);
+                        double e = fma(-dg, rc, 1.0);
+                        rc = fma(rc, e, rc);
+                        e = fma(-dg, rc, 1.0);
+                        rc = fma(rc, e, rc);
+                        rc = dg != 0.0 ? rc : 0.0;
+                        sh[P] = omega * sh[P] * rc;
+                    }
 #pragma unroll
                     for (int d = 1; d <= P; ++d) {
                         sh[P - d] = dpp_shr1(sh[P - d + 1]);  // column i2 - d
@@ -267,7 +294,7 @@ kron_v3_kernel(const double* __restrict__ x, double* __restrict__ y,
                     if constexpr (XRING) {
                         const int orow = rr - P;   // output row of this tile row, if any
                         if (orow >= 0 && orow < T1)
-                            xring[(((t + NRING) % NRING) * T1 + orow) * 64 + lane] = xr[xb][j];
+                            xring[(((t + NRING) % NRING) * T1 + orow) * 64 + lane] = sh[P];
                     }
                     if (XR % NW == 0 || rr < XR) {
                         if constexpr (SUM) {
@@ -374,7 +401,7 @@ kron_v3_kernel(const double* __restrict__ x, double* __restrict__ y,
         }
     }
 
-    if constexpr (EPI == EPI_JACOBI) {
+    if constexpr (JAC) {
         if (partial != nullptr) {
 #pragma unroll
             for (int off = 32; off > 0; off >>= 1) nrm += __shfl_xor(nrm, off, 64);
@@ -412,6 +439,14 @@ static void v3_launch_t(const KronPtrs& p, const KronGeom& g, const ToepConst& t
 template <int P, int R, int NW, bool IS3D, int FORM, int PF, bool FLAT = false>
 static int v3_launch_e(int epi, const KronPtrs& p, const KronGeom& g, const ToepConst& tc,
                        double omega, hipStream_t st) {
+    if (epi == EPI_JACOBI0) {
+        if constexpr (IS3D && FLAT) {
+            v3_launch_t<P, R, NW, IS3D, FORM, EPI_JACOBI0, PF, 0, FLAT>(p, g, tc, omega, st);
+            return 0;
+        }
+        set_error("two sweeps from zero: 3D operators with the whole-array kernel (variant 8/9) only");
+        return 1;
+    }
     switch (epi) {
         case EPI_APPLY: v3_launch_t<P, R, NW, IS3D, FORM, EPI_APPLY, PF, 0, FLAT>(p, g, tc, omega, st); return 0;
         case EPI_RESID: v3_launch_t<P, R, NW, IS3D, FORM, EPI_RESID, PF, 0, FLAT>(p, g, tc, omega, st); return 0;

@@ -316,8 +316,12 @@ static int op_run(poms_op* o, int epi, double omega, const double* x, double* y,
                   int64_t zb, int64_t ze, int want_norm, void* stream, int want_dot = 0) {
     if (!o || !x || !y) { set_error("null operator or vector"); return 1; }
     if (epi != EPI_APPLY && !b) { set_error("null right-hand side"); return 1; }
-    if (want_dot && (epi != EPI_JACOBI || !fused_dot_ok(o))) {
+    if (want_dot && ((epi != EPI_JACOBI && epi != EPI_JACOBI0) || !fused_dot_ok(o))) {
         set_error("fused x_out.b needs a Jacobi sweep on kernel variants 4-9");
+        return 1;
+    }
+    if (epi == EPI_JACOBI0 && !(o->variant == 8 || o->variant == 9)) {
+        set_error("two sweeps from zero: kernel variant 8 or 9 only");
         return 1;
     }
     KronGeom g;
@@ -331,7 +335,7 @@ static int op_run(poms_op* o, int epi, double omega, const double* x, double* y,
     // epilogue -- v4 (7) for apply / residual at p <= 3, v3 with whole-array
     // buffer resources (9; falls back to 4 for arrays >= 2 GiB) otherwise
     int v = o->variant;
-    if (v == 8) v = (epi != EPI_JACOBI && o->pmax <= 3) ? 7 : 9;
+    if (v == 8) v = (epi != EPI_JACOBI && epi != EPI_JACOBI0 && o->pmax <= 3) ? 7 : 9;
     const int rc = v == 0
         ? kron_launch(o->pmax, o->ndim == 3, o->form, epi, p, g, omega, as_stream(stream))
         : (v == 7 || (v >= 92 && v <= 100))
@@ -365,6 +369,22 @@ int poms_op_jacobi_sweep_dot(poms_op* op, double omega, const double* b, const d
                              double* x_out, int64_t zb, int64_t ze, int want_norm, void* stream) {
     if (x_in == x_out) { set_error("jacobi sweep: x_out must not alias x_in"); return 1; }
     return op_run(op, EPI_JACOBI, omega, x_in, x_out, b, zb, ze, want_norm, stream, 1);
+}
+
+int poms_op_jacobi_from_zero(poms_op* op, double omega, const double* b, double* x_out,
+                             int64_t zb, int64_t ze, int want_norm, void* stream) {
+    if (!op || !b || !x_out) { set_error("jacobi from zero: null argument"); return 1; }
+    if (b == x_out) { set_error("jacobi from zero: x_out must not alias b"); return 1; }
+    if (op->ndim != 3) { set_error("jacobi from zero: 3D operators only"); return 1; }
+    return op_run(op, EPI_JACOBI0, omega, b, x_out, b, zb, ze, want_norm, stream, want_norm);
+}
+
+int poms_op_from_zero_supported(poms_op* op, int* yes) {
+    if (!op || !yes) { set_error("poms_op_from_zero_supported: null argument"); return 1; }
+    const int64_t bytes = (int64_t)(op->L.n[0] + 2 * op->L.pads[0]) * (op->L.n[1] + 2 * op->L.pads[1]) *
+                          (op->L.n[2] + 2 * op->L.pads[2]) * 8;
+    *yes = (op->ndim == 3 && (op->variant == 8 || op->variant == 9) && bytes < 0x7fffffffLL) ? 1 : 0;
+    return 0;
 }
 
 int poms_op_fused_dot_supported(poms_op* op, int* yes) {

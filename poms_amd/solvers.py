@@ -20,7 +20,10 @@ Differences that do not change results:
 * with ``tol == 0`` the norms that can never stop the iteration are not
   computed (no host synchronisation);
 * inside ``pcg`` with this module's ``damped_jacobi`` as ``psolve``, ``s.dot(r)``
-  is accumulated by the final smoothing sweep (``poms_op_jacobi_sweep_dot``).
+  is accumulated by the final smoothing sweep (``poms_op_jacobi_sweep_dot``);
+* from ``x0 = None`` sweeps 1 and 2 run as one pass over ``b``
+  (``poms_op_jacobi_from_zero``); if the reference would stop after sweep 1,
+  ``x1`` is formed separately and returned.
 
 Inputs must be :mod:`poms_amd.stencil` device objects; there is no CPU path.
 """
@@ -152,11 +155,34 @@ def _damped_jacobi(A, b, x0=None, tol=1e-6, maxiter=10, verbose=False, want_dot=
     pending = None                      # (LazyScalar of sweep k-1, buffer holding x_{k-1})
 
     def settle(pend):
+        if len(pend) == 3:          # sweeps 1 and 2 from zero: (norms, x2 buffer, b)
+            lz, xbuf, rhs = pend
+            if lz.value(0) < tol_sqr:
+                x1 = V.empty()
+                A.diag_scale(rhs, x1, omega)
+                return True, x1
+            return lz.value(1) < tol_sqr, xbuf
         lz, xbuf = pend
         return lz.value() < tol_sqr, xbuf
 
     k0 = 1
-    if x0 is None:
+    if x0 is None and maxiter >= 2 and not verbose and not (want_dot and maxiter == 2) \
+            and A.from_zero_supported:
+        # k = 1, 2 from x = 0 in one pass over b (x1 = omega b / diag is formed on the fly)
+        x = V.empty()
+        res = A.jacobi_from_zero(b, x, omega, want_norm=need, lazy=lazy)
+        if lazy:
+            pending = (res, x, b)
+        elif need:
+            n1, n2 = res
+            if n1 < tol_sqr:        # the reference stops after sweep 1: return x1 itself
+                x1 = V.empty()
+                A.diag_scale(b, x1, omega)
+                return x1, None
+            if n2 < tol_sqr:
+                return x, None
+        k0 = 3
+    elif x0 is None:
         if maxiter < 1:
             return V.zeros(), None
         # k = 1 from x = 0:  r = b - A.0 = b,  dr = omega b / diag,  x = dr

@@ -107,18 +107,21 @@ class StencilVectorSpace:
         """Global sums can stay on the device stream (single rank, or RCCL)."""
         return not self.is_distributed or self.dist.cuda_transport
 
-    def lazy_sum(self, partial_sums: torch.Tensor) -> "LazyScalar":
-        """Global sum of device partial sums, copied to pinned host memory without
-        blocking the host; ``.value()`` waits for that copy only."""
-        tot = partial_sums.sum().reshape(1)
+    def lazy_sum(self, *partial_sums: torch.Tensor) -> "LazyScalar":
+        """Global sums of device partial-sum slices, copied to pinned host memory
+        without blocking the host; ``.value(i)`` waits for that copy only."""
+        tot = torch.stack([ps.sum() for ps in partial_sums])
         if self.is_distributed:
             import torch.distributed as dist
             dist.all_reduce(tot, group=self.dist.group)
         if self._pinned is None:
-            self._pinned = torch.zeros(4, dtype=F64).pin_memory()
+            self._pinned = torch.zeros(8, dtype=F64).pin_memory()
             self._pin_next = 0
-        slot = self._pinned[self._pin_next:self._pin_next + 1]
-        self._pin_next = (self._pin_next + 1) % 4
+        k = tot.numel()
+        if self._pin_next + k > 8:
+            self._pin_next = 0
+        slot = self._pinned[self._pin_next:self._pin_next + k]
+        self._pin_next += k
         return LazyScalar(tot, slot)
 
     def global_dot(self, local: float) -> float:
@@ -140,9 +143,9 @@ class LazyScalar:
         self._ev.record()
         self._host = host_slot
 
-    def value(self) -> float:
+    def value(self, i: int = 0) -> float:
         self._ev.synchronize()
-        return float(self._host[0])
+        return float(self._host[i])
 
 
 def _stream():
@@ -620,6 +623,38 @@ class KronOperator:
         if lazy and V.lazy_reductions:
             return V.lazy_sum(nb[:n])
         return V.global_dot(float(nb[:n].sum().item()))
+
+    @property
+    def from_zero_supported(self) -> bool:
+        v = C.c_int()
+        _lib.call("poms_op_from_zero_supported", self._h, C.byref(v))
+        return bool(v.value)
+
+    def jacobi_from_zero(self, b: StencilVector, x_out: StencilVector, omega: float,
+                         want_norm: bool = False, lazy: bool = False):
+        """Damped-Jacobi sweeps 1 and 2 from x0 = 0 in one pass over b; x_out = x2.
+
+        Returns ``(||dr_1||^2, ||dr_2||^2)`` (floats), a :class:`LazyScalar` with
+        those two values (``lazy``), or None without ``want_norm``.
+        """
+        self._check(b, x_out)
+        if x_out is b:
+            raise ValueError("x_out must not alias b")
+        V = self.space
+        nb = V.scalar_buffer()
+
+        def fn(zb, ze, st):
+            _lib.call("poms_op_jacobi_from_zero", self._h, float(omega), rt.ptr(b._data), rt.ptr(x_out._data),
+                      zb, ze, int(want_norm), st)
+
+        n = self._launch(fn, b, want_norm=want_norm, norm_buf=nb, kind="jacobi2", want_dot=want_norm)
+        x_out._mark_written()
+        if not want_norm:
+            return None
+        if lazy and V.lazy_reductions:
+            return V.lazy_sum(nb[4:4 + n], nb[:n])
+        host = nb.cpu()
+        return V.global_dot(float(host[4:4 + n].sum())), V.global_dot(float(host[:n].sum()))
 
     def diag_scale(self, b: StencilVector, out: StencilVector, scale: float = 1.0, want_norm: bool = False,
                    lazy: bool = False):

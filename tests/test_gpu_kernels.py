@@ -204,3 +204,29 @@ def test_jacobi_sweep_fused_dot(gpu, variant, ndim, cells, p):
     assert abs(dot_only - dot) <= 1e-14 * abs(dot) + 1e-300
     A.set_variant(0)
     assert not A.fused_dot_supported
+
+
+@pytest.mark.parametrize("ndim,cells,p", [(3, (25, 18, 70), 3), (3, (20, 24, 65), 2), (3, (14, 12, 66), 5)])
+def test_jacobi_from_zero(gpu, ndim, cells, p):
+    """poms_op_jacobi_from_zero == diag_scale (sweep 1) followed by one sweep, with both norms."""
+    from poms_amd.stencil import KronOperator
+    rng = np.random.default_rng(5)
+    F = [assemble_1d(uniform_knots(p, N), p) for N in cells]
+    n = [N + p for N in cells]
+    V = _space(n, [p] * ndim)
+    A = KronOperator.laplace(V, [f[0] for f in F], [f[1] for f in F])
+    assert A.from_zero_supported
+    b = V.zeros().from_numpy(rng.standard_normal(n))
+    x1, x2 = V.zeros(), V.zeros()
+    n1 = A.diag_scale(b, x1, 2.0 / 3.0, want_norm=True)
+    n2 = A.jacobi_sweep(b, x1, x2, 2.0 / 3.0, want_norm=True)
+    y = V.zeros()
+    m1, m2 = A.jacobi_from_zero(b, y, 2.0 / 3.0, want_norm=True)
+    assert rel(y.to_local_numpy(), x2.to_local_numpy()) <= TOL
+    assert abs(m1 - n1) <= 1e-12 * n1 and abs(m2 - n2) <= 1e-12 * n2
+    lz = A.jacobi_from_zero(b, y, 2.0 / 3.0, want_norm=True, lazy=True)
+    assert abs(lz.value(0) - m1) <= 1e-14 * m1 and abs(lz.value(1) - m2) <= 1e-14 * m2
+    # ghosts of the output stay zero
+    g = y._data.clone()
+    V.interior(g).zero_()
+    assert not bool(g.any())
