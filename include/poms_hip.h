@@ -100,6 +100,13 @@ int poms_op_get_variant(poms_op* op, int* variant);
  * spl `StencilMatrix.dot` (`sources/solvers.py:103`).                         */
 int poms_op_apply(poms_op* op, const double* x, double* y, int64_t z_begin,
                   int64_t z_end, void* stream);
+/* y = A x, also accumulating x . y per block into scratch[count, 2 count)
+ * (count from poms_op_last_partials; reduce with poms_reduce_partials_at).
+ * pcg's `q = A.dot(p)` + `p.dot(q)` (`sources/solvers.py:103-104`) in one
+ * pass.  Kernel variants 4, 5, 6, 8, 9 (poms_op_apply_dot_supported).        */
+int poms_op_apply_dot(poms_op* op, const double* x, double* y, int64_t z_begin,
+                      int64_t z_end, void* stream);
+int poms_op_apply_dot_supported(poms_op* op, int* yes);
 /* r = b - A x (fused).  Replaces: `r = b - A.dot(x)` at `sources/solvers.py:85`,
  * `sources/solvers.py:209`, `sources/mg_jac.py:93`.                           */
 int poms_op_residual(poms_op* op, const double* b, const double* x, double* r,

@@ -59,6 +59,8 @@ _SIGS = {
     "poms_op_get_variant": [_vp, C.POINTER(_i)],
     "poms_op_apply": [_vp, _vp, _vp, _i64, _i64, _vp],
     "poms_op_residual": [_vp, _vp, _vp, _vp, _i64, _i64, _vp],
+    "poms_op_apply_dot": [_vp, _vp, _vp, _i64, _i64, _vp],
+    "poms_op_apply_dot_supported": [_vp, C.POINTER(_i)],
     "poms_op_jacobi_sweep": [_vp, _d, _vp, _vp, _vp, _i64, _i64, _i, _vp],
     "poms_op_jacobi_sweep_dot": [_vp, _d, _vp, _vp, _vp, _i64, _i64, _i, _vp],
     "poms_op_fused_dot_supported": [_vp, C.POINTER(_i)],

@@ -10,7 +10,8 @@ constexpr int kBlock = 256;  // 4 wave64s per workgroup
 
 enum Form : int { FORM_SINGLE = 0, FORM_SUM = 1 };
 enum Epi : int { EPI_APPLY = 0, EPI_RESID = 1, EPI_JACOBI = 2,
-                 EPI_JACOBI0 = 3 /* two damped-Jacobi sweeps from x0 = 0 (x planes = b) */ };
+                 EPI_JACOBI0 = 3,   /* two damped-Jacobi sweeps from x0 = 0 (x planes = b) */
+                 EPI_APPLYDOT = 4   /* y = A x and per-block sums of x . y              */ };
 
 // Geometry of one fused Kronecker launch (all extents local to this rank's slab).
 struct KronGeom {

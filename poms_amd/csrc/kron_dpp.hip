@@ -58,7 +58,8 @@ kron_v3_kernel(const double* __restrict__ x, double* __restrict__ y,
     constexpr bool J0 = (EPI == EPI_JACOBI0);
     constexpr bool JAC = (EPI == EPI_JACOBI) || J0;
     static_assert(!J0 || (IS3D && FLAT), "EPI_JACOBI0 is built for the 3D whole-array kernel");
-    constexpr bool XRING = JAC && IS3D;
+    constexpr bool APD = (EPI == EPI_APPLYDOT);     // apply + x.(Ax) (pcg's p.q)
+    constexpr bool XRING = (JAC || APD) && IS3D;
     constexpr int NRING = P + 1;            // x planes kept for the Jacobi update
     __shared__ d2 ab_[SUM ? 2 * XRP * 64 : 1];
     // x of the tile's output rows for the last P+1 planes (the Jacobi epilogue's
@@ -127,7 +128,7 @@ kron_v3_kernel(const double* __restrict__ x, double* __restrict__ y,
     // host); planes are addressed by the scalar offset -- no per-plane descriptor math
     const uint32_t arr_bytes = FLAT ? (uint32_t)((int64_t)nsp * g.s0 * 8) : 0u;
     const __amdgpu_buffer_rsrc_t rx_all = make_rsrc(x, arr_bytes);
-    const __amdgpu_buffer_rsrc_t rb_all = make_rsrc(bvec, EPI != EPI_APPLY ? arr_bytes : 0u);
+    const __amdgpu_buffer_rsrc_t rb_all = make_rsrc(bvec, (EPI != EPI_APPLY && !APD) ? arr_bytes : 0u);
     const __amdgpu_buffer_rsrc_t ry_all = make_rsrc(y, arr_bytes);
     const uint32_t plane8 = (uint32_t)(g.s0 * 8);
     auto load_plane = [&](int jj, int xb) {
@@ -170,7 +171,14 @@ kron_v3_kernel(const double* __restrict__ x, double* __restrict__ y,
     };
     auto epi_issue = [&](int zo, int eb_i) {
         double* eb = ebb[eb_i];
-        if constexpr (EPI != EPI_APPLY && FLAT) {
+        if constexpr (APD && !XRING) {   // 2D: x at the output rows from memory
+            const uint32_t so = FLAT ? (uint32_t)(zo + g.pd0) * plane8 : 0u;
+            const __amdgpu_buffer_rsrc_t xsr = FLAT ? rx_all : make_rsrc(x + (int64_t)(zo + g.pd0) * g.s0,
+                                                                         plane_bytes(nsp - zo - g.pd0, g.s0));
+#pragma unroll
+            for (int r = 0; r < R; ++r) ex[r] = bload_s(xsr, obase + r * rowstep, so);
+        } else if constexpr (APD) {
+        } else if constexpr (EPI != EPI_APPLY && FLAT) {
             const uint32_t so = (uint32_t)(zo + g.pd0) * plane8;
 #pragma unroll
             for (int r = 0; r < R; ++r) eb[r] = bload_s(rb_all, obase + r * rowstep, so);
@@ -207,6 +215,9 @@ kron_v3_kernel(const double* __restrict__ x, double* __restrict__ y,
             double outv;
             if constexpr (EPI == EPI_APPLY) {
                 outv = v[r];
+            } else if constexpr (APD) {
+                outv = v[r];
+                dotp = ok ? fma(ex[r], outv, dotp) : dotp;
             } else if constexpr (EPI == EPI_RESID) {
                 outv = eb[r] - v[r];
             } else {
@@ -401,7 +412,7 @@ kron_v3_kernel(const double* __restrict__ x, double* __restrict__ y,
         }
     }
 
-    if constexpr (JAC) {
+    if constexpr (JAC || APD) {
         if (partial != nullptr) {
 #pragma unroll
             for (int off = 32; off > 0; off >>= 1) nrm += __shfl_xor(nrm, off, 64);
@@ -439,6 +450,10 @@ static void v3_launch_t(const KronPtrs& p, const KronGeom& g, const ToepConst& t
 template <int P, int R, int NW, bool IS3D, int FORM, int PF, bool FLAT = false>
 static int v3_launch_e(int epi, const KronPtrs& p, const KronGeom& g, const ToepConst& tc,
                        double omega, hipStream_t st) {
+    if (epi == EPI_APPLYDOT) {
+        v3_launch_t<P, R, NW, IS3D, FORM, EPI_APPLYDOT, PF, 0, FLAT>(p, g, tc, omega, st);
+        return 0;
+    }
     if (epi == EPI_JACOBI0) {
         if constexpr (IS3D && FLAT) {
             v3_launch_t<P, R, NW, IS3D, FORM, EPI_JACOBI0, PF, 0, FLAT>(p, g, tc, omega, st);

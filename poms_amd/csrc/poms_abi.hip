@@ -316,7 +316,12 @@ static int op_run(poms_op* o, int epi, double omega, const double* x, double* y,
                   int64_t zb, int64_t ze, int want_norm, void* stream, int want_dot = 0) {
     if (!o || !x || !y) { set_error("null operator or vector"); return 1; }
     if (epi != EPI_APPLY && !b) { set_error("null right-hand side"); return 1; }
-    if (want_dot && ((epi != EPI_JACOBI && epi != EPI_JACOBI0) || !fused_dot_ok(o))) {
+    if (epi == EPI_APPLYDOT && !(o->variant == 4 || o->variant == 5 || o->variant == 6 || o->variant == 8 ||
+                                 o->variant == 9)) {
+        set_error("apply + x.y: kernel variants 4, 5, 6, 8, 9 only");
+        return 1;
+    }
+    if (want_dot && ((epi != EPI_JACOBI && epi != EPI_JACOBI0 && epi != EPI_APPLYDOT) || !fused_dot_ok(o))) {
         set_error("fused x_out.b needs a Jacobi sweep on kernel variants 4-9");
         return 1;
     }
@@ -335,7 +340,7 @@ static int op_run(poms_op* o, int epi, double omega, const double* x, double* y,
     // epilogue -- v4 (7) for apply / residual at p <= 3, v3 with whole-array
     // buffer resources (9; falls back to 4 for arrays >= 2 GiB) otherwise
     int v = o->variant;
-    if (v == 8) v = (epi != EPI_JACOBI && epi != EPI_JACOBI0 && o->pmax <= 3) ? 7 : 9;
+    if (v == 8) v = ((epi == EPI_APPLY || epi == EPI_RESID) && o->pmax <= 3) ? 7 : 9;
     const int rc = v == 0
         ? kron_launch(o->pmax, o->ndim == 3, o->form, epi, p, g, omega, as_stream(stream))
         : (v == 7 || (v >= 92 && v <= 100))
@@ -369,6 +374,18 @@ int poms_op_jacobi_sweep_dot(poms_op* op, double omega, const double* b, const d
                              double* x_out, int64_t zb, int64_t ze, int want_norm, void* stream) {
     if (x_in == x_out) { set_error("jacobi sweep: x_out must not alias x_in"); return 1; }
     return op_run(op, EPI_JACOBI, omega, x_in, x_out, b, zb, ze, want_norm, stream, 1);
+}
+
+int poms_op_apply_dot(poms_op* op, const double* x, double* y, int64_t zb, int64_t ze, void* stream) {
+    if (x == y) { set_error("apply: y must not alias x"); return 1; }
+    return op_run(op, EPI_APPLYDOT, 0.0, x, y, x, zb, ze, 0, stream, 1);
+}
+
+int poms_op_apply_dot_supported(poms_op* op, int* yes) {
+    if (!op || !yes) { set_error("poms_op_apply_dot_supported: null argument"); return 1; }
+    const int v = op->variant;
+    *yes = (v == 4 || v == 5 || v == 6 || v == 8 || v == 9) ? 1 : 0;
+    return 0;
 }
 
 int poms_op_jacobi_from_zero(poms_op* op, double omega, const double* b, double* x_out,

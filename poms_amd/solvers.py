@@ -21,6 +21,7 @@ Differences that do not change results:
   computed (no host synchronisation);
 * inside ``pcg`` with this module's ``damped_jacobi`` as ``psolve``, ``s.dot(r)``
   is accumulated by the final smoothing sweep (``poms_op_jacobi_sweep_dot``);
+* ``q = A.dot(p)`` and ``p.dot(q)`` come from one pass (``poms_op_apply_dot``);
 * from ``x0 = None`` sweeps 1 and 2 run as one pass over ``b``
   (``poms_op_jacobi_from_zero``); if the reference would stop after sweep 1,
   ``x1`` is formed separately and returned.
@@ -76,9 +77,14 @@ def pcg(A, psolve, b, x0=None, tol=1e-6, maxiter=100, verbose=False):
 
     k = 0
     nrmr = nrmr0 * nrmr0
+    fused_pq = A.apply_dot_supported
     for k in range(1, maxiter + 1):
-        A.dot(p, out=q)
-        alpha = sr / p.dot(q)
+        if fused_pq:
+            pq = A.dot_inner(p, q)       # q = A p and p.q in one pass
+        else:
+            A.dot(p, out=q)
+            pq = p.dot(q)
+        alpha = sr / pq
         nrmr = _pcg_update(V, alpha, x, p, r, q)   # x += alpha p ; r -= alpha q ; r.r
         if nrmr < tol * nrmr0:
             k -= 1

@@ -572,6 +572,27 @@ class KronOperator:
         y._mark_written()
         return y
 
+    @property
+    def apply_dot_supported(self) -> bool:
+        v = C.c_int()
+        _lib.call("poms_op_apply_dot_supported", self._h, C.byref(v))
+        return bool(v.value)
+
+    def dot_inner(self, x: StencilVector, out: StencilVector) -> float:
+        """``out = A x`` and the global ``x . out`` from the same pass (pcg's q and p.q)."""
+        self._check(x, out)
+        if out is x:
+            raise ValueError("out must not alias x")
+        V = self.space
+        nb = V.scalar_buffer()
+
+        def fn(zb, ze, st):
+            _lib.call("poms_op_apply_dot", self._h, rt.ptr(x._data), rt.ptr(out._data), zb, ze, st)
+
+        n = self._launch(fn, x, norm_buf=nb, kind="apply", want_dot=True)
+        out._mark_written()
+        return V.global_dot(float(nb[4:4 + n].sum().item()))
+
     def residual(self, b: StencilVector, x: StencilVector, out: StencilVector | None = None) -> StencilVector:
         """r = b - A x, fused (`sources/solvers.py:85`, `sources/mg_jac.py:93`)."""
         self._check(b, x)

@@ -230,3 +230,26 @@ def test_jacobi_from_zero(gpu, ndim, cells, p):
     g = y._data.clone()
     V.interior(g).zero_()
     assert not bool(g.any())
+
+
+@pytest.mark.parametrize("variant", [4, 8, 9])
+@pytest.mark.parametrize("ndim,cells,p", [(3, (25, 18, 70), 3), (2, (64, 64), 3), (3, (14, 12, 66), 5)])
+def test_apply_fused_inner(gpu, variant, ndim, cells, p):
+    """poms_op_apply_dot: q = A p bit-identical to the apply of the same kernel family, p.q == dot."""
+    from poms_amd.stencil import KronOperator
+    rng = np.random.default_rng(8)
+    F = [assemble_1d(uniform_knots(p, N), p) for N in cells]
+    n = [N + p for N in cells]
+    V = _space(n, [p] * ndim)
+    A = KronOperator.laplace(V, [f[0] for f in F], [f[1] for f in F])
+    A.set_variant(variant)
+    assert A.apply_dot_supported
+    x = V.zeros().from_numpy(rng.standard_normal(n))
+    q = V.zeros()
+    pq = A.dot_inner(x, q)
+    ref = orc.kron_sum_apply(rng.standard_normal(n) * 0 + x.to_local_numpy(), [f[0] for f in F], [f[1] for f in F])
+    assert rel(q.to_local_numpy(), ref) <= TOL
+    want = float(np.vdot(x.to_local_numpy(), q.to_local_numpy()))
+    assert abs(pq - want) <= 1e-12 * (abs(want) + np.linalg.norm(x.to_local_numpy()) * np.linalg.norm(ref))
+    A.set_variant(7)
+    assert not A.apply_dot_supported
