@@ -181,6 +181,14 @@ int poms_vec_dot(poms_ctx* ctx, const poms_layout* L, const double* x,
 int poms_pcg_update(poms_ctx* ctx, const poms_layout* L, double alpha, double* x,
                     const double* p, double* r, const double* q, double* out_dev,
                     void* stream);
+/* r -= alpha q; out_dev[0] = r.r (local).  With poms_pcg_xp_update this splits
+ * poms_pcg_update so that x's update can ride on the p update one psolve later. */
+int poms_pcg_r_update(poms_ctx* ctx, const poms_layout* L, double alpha, double* r,
+                      const double* q, double* out_dev, void* stream);
+/* x += alpha p; p = s + beta p (both from the old p, one pass):
+ * `sources/solvers.py:106` of iteration k and :124 of the same iteration.    */
+int poms_pcg_xp_update(poms_ctx* ctx, const poms_layout* L, double alpha, double beta,
+                       double* x, double* p, const double* s, void* stream);
 /* Reduce `count` partials from the context scratch into out_dev[0]. */
 int poms_reduce_partials(poms_ctx* ctx, int64_t count, double* out_dev, void* stream);
 /* Same, starting at scratch[offset]. */

@@ -75,6 +75,8 @@ _SIGS = {
     "poms_vec_fill": [_vp, _LP, _d, _vp, _vp],
     "poms_vec_dot": [_vp, _LP, _vp, _vp, _vp, _vp],
     "poms_pcg_update": [_vp, _LP, _d, _vp, _vp, _vp, _vp, _vp, _vp],
+    "poms_pcg_r_update": [_vp, _LP, _d, _vp, _vp, _vp, _vp],
+    "poms_pcg_xp_update": [_vp, _LP, _d, _d, _vp, _vp, _vp, _vp],
     "poms_reduce_partials": [_vp, _i64, _vp, _vp],
     "poms_reduce_partials_at": [_vp, _i64, _i64, _vp, _vp],
     "poms_transfer_create": [_vp, _i, _LP, _i64, _vp, _vp, C.POINTER(C.c_void_p), _pp],

@@ -35,7 +35,7 @@ int dense_matvec_launch(int n, const double* M, const double* x, double* y, hipS
 int transfer_pass_launch(bool restrict_dir, int ncm, const AxisPass& ps, const double* Pm,
                          const double* in, double* out, hipStream_t st);
 
-enum { V_AXPBY = 0, V_SCALE = 1, V_FILL = 2, V_DOT = 3, V_PCGUPD = 4 };
+enum { V_AXPBY = 0, V_SCALE = 1, V_FILL = 2, V_DOT = 3, V_PCGUPD = 4, V_RUPD = 5, V_XPUPD = 6 };
 constexpr int64_t kScratch = 1 << 16;
 
 }  // namespace poms
@@ -507,7 +507,7 @@ static int vec_common(poms_ctx* ctx, const poms_layout* L, int op, double a, dou
     if (!ctx || !layout_ok(L)) { set_error("vector op: bad context or layout"); return 1; }
     const RowGeom g = row_geom(L);
     int nb = 0;
-    const bool red = (op == V_DOT || op == V_PCGUPD);
+    const bool red = (op == V_DOT || op == V_PCGUPD || op == V_RUPD);
     if (vec_launch(op, g, a, b, x, y, z, w, q, red ? ctx->scratch : nullptr, as_stream(stream), &nb))
         return 1;
     if (red) reduce_launch(ctx->scratch, nb, out_dev, as_stream(stream));
@@ -542,6 +542,18 @@ int poms_pcg_update(poms_ctx* ctx, const poms_layout* L, double alpha, double* x
                     double* r, const double* q, double* out_dev, void* stream) {
     if (!x || !p || !r || !q || !out_dev) { set_error("pcg_update: null argument"); return 1; }
     return vec_common(ctx, L, V_PCGUPD, alpha, 0.0, nullptr, p, x, r, q, out_dev, stream);
+}
+
+int poms_pcg_r_update(poms_ctx* ctx, const poms_layout* L, double alpha, double* r, const double* q,
+                      double* out_dev, void* stream) {
+    if (!r || !q || !out_dev) { set_error("pcg_r_update: null argument"); return 1; }
+    return vec_common(ctx, L, V_RUPD, alpha, 0.0, nullptr, nullptr, nullptr, r, q, out_dev, stream);
+}
+
+int poms_pcg_xp_update(poms_ctx* ctx, const poms_layout* L, double alpha, double beta, double* x,
+                       double* p, const double* s, void* stream) {
+    if (!x || !p || !s) { set_error("pcg_xp_update: null argument"); return 1; }
+    return vec_common(ctx, L, V_XPUPD, alpha, beta, s, nullptr, x, p, nullptr, nullptr, stream);
 }
 
 int poms_reduce_partials(poms_ctx* ctx, int64_t count, double* out_dev, void* stream) {

@@ -9,7 +9,7 @@
 
 namespace poms {
 
-enum VecOp : int { V_AXPBY = 0, V_SCALE = 1, V_FILL = 2, V_DOT = 3, V_PCGUPD = 4 };
+enum VecOp : int { V_AXPBY = 0, V_SCALE = 1, V_FILL = 2, V_DOT = 3, V_PCGUPD = 4, V_RUPD = 5, V_XPUPD = 6 };
 
 constexpr int kMaxPartials = 4096;
 
@@ -38,15 +38,23 @@ vec_rows_kernel(const RowGeom g, const double a, const double b,
                 z[o] = a;
             } else if constexpr (OP == V_DOT) {
                 s = fma(x[o], yv[o], s);
-            } else {  // V_PCGUPD: z = x += a*p (yv = p), w = r -= a*q
+            } else if constexpr (OP == V_PCGUPD) {  // z = x += a*p (yv = p), w = r -= a*q
                 z[o] = fma(a, yv[o], z[o]);
                 const double rn = fma(-a, q[o], w[o]);
                 w[o] = rn;
                 s = fma(rn, rn, s);
+            } else if constexpr (OP == V_RUPD) {    // w = r -= a*q, r.r
+                const double rn = fma(-a, q[o], w[o]);
+                w[o] = rn;
+                s = fma(rn, rn, s);
+            } else {                                 // V_XPUPD: z = x += a*p_old; w = p = s + b*p_old (x = s)
+                const double po = w[o];
+                z[o] = fma(a, po, z[o]);
+                w[o] = x[o] + b * po;
             }
         }
     }
-    if constexpr (OP == V_DOT || OP == V_PCGUPD) {
+    if constexpr (OP == V_DOT || OP == V_PCGUPD || OP == V_RUPD) {
         const double t = block_sum_256(s, red);
         if (threadIdx.x == 0) partial[blockIdx.x] = t;
     }
@@ -156,6 +164,8 @@ int vec_launch(int op, const RowGeom& g, double a, double b, const double* x, co
         POMS_VL(V_FILL)
         POMS_VL(V_DOT)
         POMS_VL(V_PCGUPD)
+        POMS_VL(V_RUPD)
+        POMS_VL(V_XPUPD)
 #undef POMS_VL
     }
     set_error("unknown vector op");

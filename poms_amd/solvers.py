@@ -85,8 +85,9 @@ def pcg(A, psolve, b, x0=None, tol=1e-6, maxiter=100, verbose=False):
             A.dot(p, out=q)
             pq = p.dot(q)
         alpha = sr / pq
-        nrmr = _pcg_update(V, alpha, x, p, r, q)   # x += alpha p ; r -= alpha q ; r.r
+        nrmr = _pcg_r_update(V, alpha, r, q)        # r -= alpha q ; r.r
         if nrmr < tol * nrmr0:
+            _vec(V, "poms_vec_axpby", 1.0, x, alpha, p, x)   # x += alpha p
             k -= 1
             break
         srold = sr
@@ -94,7 +95,7 @@ def pcg(A, psolve, b, x0=None, tol=1e-6, maxiter=100, verbose=False):
         beta = sr / srold
         if p is s:
             raise RuntimeError("psolve returned its input buffer")
-        p.axpby_(1.0, s, beta)           # p = s + beta p (in place; p's buffer is never s's)
+        _pcg_xp_update(V, alpha, beta, x, p, s)     # x += alpha p ; p = s + beta p  (old p, one pass)
         if verbose:
             print(template.format(k, sqrt(nrmr)))
 
@@ -114,6 +115,33 @@ def _psolve_dot(A, psolve, r):
         return s, s.dot(r)
     s = psolve(A, r)
     return s, s.dot(r)
+
+
+def _vec(V, name, a, xv, b, yv, zv):
+    from . import _lib, runtime as rt
+    import ctypes as C
+    _lib.call(name, V.ctx, C.byref(V.layout), float(a), rt.ptr(xv._data), float(b), rt.ptr(yv._data),
+              rt.ptr(zv._data), rt.stream_handle())
+    zv._mark_written()
+
+
+def _pcg_r_update(V, alpha, r, q) -> float:
+    from . import _lib, runtime as rt
+    import ctypes as C
+    buf = V.scalar_buffer()
+    _lib.call("poms_pcg_r_update", V.ctx, C.byref(V.layout), float(alpha), rt.ptr(r._data), rt.ptr(q._data),
+              rt.ptr(buf), rt.stream_handle())
+    r._mark_written()
+    return V.global_dot(float(buf[0].item()))
+
+
+def _pcg_xp_update(V, alpha, beta, x, p, s):
+    from . import _lib, runtime as rt
+    import ctypes as C
+    _lib.call("poms_pcg_xp_update", V.ctx, C.byref(V.layout), float(alpha), float(beta), rt.ptr(x._data),
+              rt.ptr(p._data), rt.ptr(s._data), rt.stream_handle())
+    x._mark_written()
+    p._mark_written()
 
 
 def _pcg_update(V, alpha, x, p, r, q) -> float:
