@@ -59,6 +59,7 @@ struct KronPtrs {
     const double *a0t, *b0t, *a1, *b1, *a2, *b2;
     double* partial;    // Jacobi: per-block sums of dr.dr (or null)
     double* partial2;   // Jacobi: per-block sums of x_out.b (or null)
+    const double* rdiag0 = nullptr;  // 1/diag(A) per global plane inside the axis-1/2 Toeplitz interior
 };
 
 void set_error(const std::string& msg);

@@ -40,8 +40,9 @@ kron_v3_kernel(const double* __restrict__ x, double* __restrict__ y,
                const double* __restrict__ a0t, const double* __restrict__ b0t,
                const double* __restrict__ a1, const double* __restrict__ b1,
                const double* __restrict__ a2, const double* __restrict__ b2,
-               double* __restrict__ partial, double* __restrict__ partial2, const KronGeom g,
-               const ToepConst tc, const double omega) {
+               double* __restrict__ partial, double* __restrict__ partial2,
+               const double* __restrict__ rdiag0, const KronGeom g, const ToepConst tc,
+               const double omega) {
     constexpr int W = 2 * P + 1;
     constexpr int NT = NW * 64;
     constexpr int TO = 64 - 2 * P;          // output columns per tile
@@ -59,7 +60,13 @@ kron_v3_kernel(const double* __restrict__ x, double* __restrict__ y,
     constexpr bool JAC = (EPI == EPI_JACOBI) || J0;
     static_assert(!J0 || (IS3D && FLAT), "EPI_JACOBI0 is built for the 3D whole-array kernel");
     constexpr bool APD = (EPI == EPI_APPLYDOT);     // apply + x.(Ax) (pcg's p.q)
-    constexpr bool XRING = (JAC || APD) && IS3D;
+    // T2 (the whole-array build): axis-2 band rows from the Toeplitz constants
+    // (symmetric pair sums) in interior column tiles and from an LDS table in the
+    // two boundary tiles -- no per-lane copy of the 2(2P+1) coefficients in VGPRs.
+    // The freed registers pay for the per-plane 1/diag path; x_in is re-read
+    // (L2) instead of kept in the LDS ring.
+    constexpr bool T2 = false;   // measured slower (x_in re-read, LDS-table boundary tiles): kept for reference
+    constexpr bool XRING = (JAC || APD) && IS3D && !T2;
     constexpr int NRING = P + 1;            // x planes kept for the Jacobi update
     __shared__ d2 ab_[SUM ? 2 * XRP * 64 : 1];
     // x of the tile's output rows for the last P+1 planes (the Jacobi epilogue's
@@ -69,6 +76,7 @@ kron_v3_kernel(const double* __restrict__ x, double* __restrict__ y,
     __shared__ double c1a[T1 * W];
     __shared__ double c1b[SUM ? T1 * W : 1];
     __shared__ double red[NW];
+    __shared__ double c2t[T2 ? 2 * W * 64 : 1];   // [a|b][k][lane] boundary-tile axis-2 rows
 
     const int tid = threadIdx.x;
     const int lane = tid & 63;
@@ -89,16 +97,37 @@ kron_v3_kernel(const double* __restrict__ x, double* __restrict__ y,
     const int i2 = c0 - P + lane;       // this lane's column (may be a halo column)
     const bool col_ok = lane >= P && lane < 64 - P && i2 < g.n2;
 
-    double ca2[W], cb2[W];
+    constexpr int WC = T2 ? 1 : W;
+    double ca2[WC], cb2[WC];
+    double d2a, d2b;   // this lane's axis-2 band diagonal (F2a, F2b)
     {
         const int ic = min(max(i2, 0), g.n2 - 1);
+        if constexpr (T2) {
+            d2a = a2[ic * W + P];
+            d2b = SUM ? b2[ic * W + P] : 0.0;
+        } else {
 #pragma unroll
-        for (int k = 0; k < W; ++k) {
-            ca2[k] = a2[ic * W + k];
-            cb2[k] = SUM ? b2[ic * W + k] : 0.0;
+            for (int k = 0; k < W; ++k) {
+                ca2[k] = a2[ic * W + k];
+                cb2[k] = SUM ? b2[ic * W + k] : 0.0;
+            }
+            d2a = ca2[P];
+            d2b = cb2[P];
+        }
+    }
+    const bool fast2 = (c0 >= tc.lo2) && (min(c0 + TO, g.n2) <= tc.hi2);
+    if (T2 && !fast2) {
+        for (int e = tid; e < W * 64; e += NT) {
+            const int k = e >> 6, l = e & 63;
+            const int col = min(max(c0 - P + l, 0), g.n2 - 1);
+            c2t[e] = a2[col * W + k];
+            c2t[W * 64 + e] = SUM ? b2[col * W + k] : 0.0;
         }
     }
     const bool fast1 = (r0 >= tc.lo1) && (r0 + T1 <= tc.hi1);
+    // all output points of the tile in the axis-1/2 Toeplitz interior: diag(A)
+    // depends on the plane only, 1/diag comes from the host-built rdiag0 table
+    const bool fast12 = T2 && rdiag0 != nullptr && fast1 && (c0 >= tc.lo2) && (min(c0 + TO, g.n2) <= tc.hi2);
     if (!fast1) {
         for (int e = tid; e < T1 * W; e += NT) {
             const int rl = e / W, k = e - rl * W;
@@ -162,16 +191,16 @@ kron_v3_kernel(const double* __restrict__ x, double* __restrict__ y,
         const double d1a = fast1 ? tc.t1a[0] : c1a[(wv * R + r) * W + P];
         const double d1b = SUM ? (fast1 ? tc.t1b[0] : c1b[(wv * R + r) * W + P]) : 0.0;
         if constexpr (IS3D) {
-            dX = d1a * ca2[P];
-            dY = SUM ? (d1b * ca2[P] + d1a * cb2[P]) : 0.0;
+            dX = d1a * d2a;
+            dY = SUM ? (d1b * d2a + d1a * d2b) : 0.0;
         } else {
-            dX = SUM ? (d1a * ca2[P] + d1b * cb2[P]) : d1a * ca2[P];
+            dX = SUM ? (d1a * d2a + d1b * d2b) : d1a * d2a;
             dY = 0.0;
         }
     };
     auto epi_issue = [&](int zo, int eb_i) {
         double* eb = ebb[eb_i];
-        if constexpr (APD && !XRING) {   // 2D: x at the output rows from memory
+        if constexpr (APD && !XRING) {   // x at the output rows from memory (2D, or T2)
             const uint32_t so = FLAT ? (uint32_t)(zo + g.pd0) * plane8 : 0u;
             const __amdgpu_buffer_rsrc_t xsr = FLAT ? rx_all : make_rsrc(x + (int64_t)(zo + g.pd0) * g.s0,
                                                                          plane_bytes(nsp - zo - g.pd0, g.s0));
@@ -182,7 +211,7 @@ kron_v3_kernel(const double* __restrict__ x, double* __restrict__ y,
             const uint32_t so = (uint32_t)(zo + g.pd0) * plane8;
 #pragma unroll
             for (int r = 0; r < R; ++r) eb[r] = bload_s(rb_all, obase + r * rowstep, so);
-            if constexpr (JAC && !XRING) {
+            if constexpr (JAC && !J0 && !XRING) {
 #pragma unroll
                 for (int r = 0; r < R; ++r) ex[r] = bload_s(rx_all, obase + r * rowstep, so);
             }
@@ -221,14 +250,20 @@ kron_v3_kernel(const double* __restrict__ x, double* __restrict__ y,
             } else if constexpr (EPI == EPI_RESID) {
                 outv = eb[r] - v[r];
             } else {
-                double dX, dY;
-                diag_parts(r, dX, dY);
-                const double diag = IS3D ? fma(d0a, dX, d0b * dY) : dX;
-                double rc = __builtin_amdgcn_rcp(diag);
-                double e = fma(-diag, rc, 1.0);
-                rc = fma(rc, e, rc);
-                e = fma(-diag, rc, 1.0);
-                rc = fma(rc, e, rc);
+                double rc;
+                if (fast12) {
+                    rc = rdiag0[IS3D ? g.g0 + zo : 0];
+                } else {
+                    double dX, dY;
+                    diag_parts(r, dX, dY);
+                    const double diag = IS3D ? fma(d0a, dX, d0b * dY) : dX;
+                    rc = __builtin_amdgcn_rcp(diag);
+                    double e = fma(-diag, rc, 1.0);
+                    rc = fma(rc, e, rc);
+                    e = fma(-diag, rc, 1.0);
+                    rc = fma(rc, e, rc);
+                }
+                if constexpr (J0 && !XRING) ex[r] = omega * eb[r] * rc;   // x1 at the output point
                 const double dr = omega * (eb[r] - v[r]) * rc;
                 outv = ex[r] + dr;
                 nrm = ok ? fma(dr, dr, nrm) : nrm;
@@ -277,8 +312,8 @@ kron_v3_kernel(const double* __restrict__ x, double* __restrict__ y,
                         const int row = min(max(r0 - P + wv + j * NW, 0), g.n1 - 1);
                         const double q1a = a1[row * W + P];
                         const double q1b = SUM ? b1[row * W + P] : 0.0;
-                        double dg = SUM ? q0a * (q1a * ca2[P]) + q0b * (q1b * ca2[P] + q1a * cb2[P])
-                                        : q0a * q1a * ca2[P];
+                        double dg = SUM ? q0a * (q1a * d2a) + q0b * (q1b * d2a + q1a * d2b)
+                                        : q0a * q1a * d2a;
                         double rc = __builtin_amdgcn_rcp(dg);
                         double e = fma(-dg, rc, 1.0);
                         rc = fma(rc, e, rc);
@@ -292,14 +327,39 @@ kron_v3_kernel(const double* __restrict__ x, double* __restrict__ y,
                         sh[P - d] = dpp_shr1(sh[P - d + 1]);  // column i2 - d
                         sh[P + d] = dpp_shl1(sh[P + d - 1]);  // column i2 + d
                     }
-                    double sa = ca2[0] * sh[0];
-                    double sb = SUM ? cb2[0] * sh[0] : 0.0;
-                    if constexpr (MODE == 1) { sa = xr[xb][j]; sb = sa; } else {
+                    double sa, sb = 0.0;
+                    if constexpr (MODE == 1) {
+                        sa = xr[xb][j];
+                        sb = sa;
+                    } else if constexpr (!T2) {
+                        sa = ca2[0] * sh[0];
+                        sb = SUM ? cb2[0] * sh[0] : 0.0;
 #pragma unroll
-                    for (int k = 1; k < W; ++k) {
-                        sa = fma(ca2[k], sh[k], sa);
-                        if constexpr (SUM) sb = fma(cb2[k], sh[k], sb);
-                    }
+                        for (int k = 1; k < W; ++k) {
+                            sa = fma(ca2[k], sh[k], sa);
+                            if constexpr (SUM) sb = fma(cb2[k], sh[k], sb);
+                        }
+                    } else if (fast2) {
+                        // symmetric Toeplitz interior: P pair sums, P + 1 multiplies per product
+                        double pr2[P + 1];
+                        pr2[0] = sh[P];
+#pragma unroll
+                        for (int k = 1; k <= P; ++k) pr2[k] = sh[P - k] + sh[P + k];
+                        sa = tc.t2a[0] * pr2[0];
+                        if constexpr (SUM) sb = tc.t2b[0] * pr2[0];
+#pragma unroll
+                        for (int k = 1; k <= P; ++k) {
+                            sa = fma(tc.t2a[k], pr2[k], sa);
+                            if constexpr (SUM) sb = fma(tc.t2b[k], pr2[k], sb);
+                        }
+                    } else {
+                        sa = c2t[lane] * sh[0];
+                        if constexpr (SUM) sb = c2t[W * 64 + lane] * sh[0];
+#pragma unroll
+                        for (int k = 1; k < W; ++k) {
+                            sa = fma(c2t[k * 64 + lane], sh[k], sa);
+                            if constexpr (SUM) sb = fma(c2t[(W + k) * 64 + lane], sh[k], sb);
+                        }
                     }
                     const int rr = wv + j * NW;
                     if constexpr (XRING) {
@@ -444,7 +504,7 @@ static void v3_launch_t(const KronPtrs& p, const KronGeom& g, const ToepConst& t
                         hipStream_t st) {
     const int nblk = g.tiles2 * g.tiles1 * g.nchunks;
     hipLaunchKernelGGL((kron_v3_kernel<P, R, NW, IS3D, FORM, EPI, PF, MODE, FLAT>), dim3(nblk), dim3(NW * 64), 0, st,
-                       p.x, p.y, p.b, p.a0t, p.b0t, p.a1, p.b1, p.a2, p.b2, p.partial, p.partial2, g, tc, omega);
+                       p.x, p.y, p.b, p.a0t, p.b0t, p.a1, p.b1, p.a2, p.b2, p.partial, p.partial2, p.rdiag0, g, tc, omega);
 }
 
 template <int P, int R, int NW, bool IS3D, int FORM, int PF, bool FLAT = false>

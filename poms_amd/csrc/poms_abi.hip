@@ -55,6 +55,7 @@ struct poms_op {
     double *a0t = nullptr, *b0t = nullptr, *a1 = nullptr, *b1 = nullptr, *a2 = nullptr, *b2 = nullptr;
     int64_t last_partials = 0;
     double *dg2a = nullptr, *dg2b = nullptr;  // contiguous axis-2 band diagonals
+    double* rdiag0 = nullptr;                  // 1/diag(A) per global plane (Toeplitz interior of axes 1, 2)
     int variant = 0;
     bool v2_ok = false;
     ToepConst tc{};
@@ -245,13 +246,32 @@ int poms_op_create(poms_ctx* ctx, int ndim, const poms_layout* layout, int form,
     toeplitz_range(f[2], sum ? f[3] : nullptr, layout->n[1], pmax, &o->tc.lo1, &o->tc.hi1, o->tc.t1a, o->tc.t1b);
     toeplitz_range(f[4], sum ? f[5] : nullptr, layout->n[2], pmax, &o->tc.lo2, &o->tc.hi2, o->tc.t2a, o->tc.t2b);
     o->variant = o->v2_ok ? 8 : 0;
+    // 1/diag(A) on each global plane for points in the Toeplitz interior of axes 1
+    // and 2 (same expression as the kernels' per-point diagonal)
+    if (o->tc.lo1 < o->tc.hi1 && o->tc.lo2 < o->tc.hi2) {
+        const double d1a = o->tc.t1a[0], d1b = sum ? o->tc.t1b[0] : 0.0;
+        const double d2a = o->tc.t2a[0], d2b = sum ? o->tc.t2b[0] : 0.0;
+        const int64_t np = is3d ? n0_global : 1;
+        std::vector<double> rd(np);
+        for (int64_t i = 0; i < np; ++i) {
+            double dg;
+            if (is3d) {
+                const double d0a = f[0][i * W + pmax], d0b = sum ? f[1][i * W + pmax] : 0.0;
+                dg = sum ? d0a * (d1a * d2a) + d0b * (d1b * d2a + d1a * d2b) : d0a * (d1a * d2a);
+            } else {
+                dg = sum ? d1a * d2a + d1b * d2b : d1a * d2a;
+            }
+            rd[i] = dg != 0.0 ? 1.0 / dg : 0.0;
+        }
+        if (upload(rd.data(), rd.size(), &o->rdiag0)) { poms_op_destroy(o); return 1; }
+    }
     *op = o;
     return 0;
 }
 
 int poms_op_destroy(poms_op* o) {
     if (!o) return 0;
-    for (double* p : {o->a0t, o->b0t, o->a1, o->b1, o->a2, o->b2, o->dg2a, o->dg2b})
+    for (double* p : {o->a0t, o->b0t, o->a1, o->b1, o->a2, o->b2, o->dg2a, o->dg2b, o->rdiag0})
         if (p) (void)hipFree(p);
     delete o;
     return 0;
@@ -335,7 +355,7 @@ static int op_run(poms_op* o, int epi, double omega, const double* x, double* y,
     if (nblk == 0) { o->last_partials = 0; return 0; }
     if ((want_norm || want_dot) && 2 * nblk > kScratch) { set_error("too many blocks for the partial-sum scratch"); return 1; }
     KronPtrs p{x, y, b, o->a0t, o->b0t, o->a1, o->b1, o->a2, o->b2,
-               want_norm ? o->ctx->scratch : nullptr, want_dot ? o->ctx->scratch + nblk : nullptr};
+               want_norm ? o->ctx->scratch : nullptr, want_dot ? o->ctx->scratch + nblk : nullptr, o->rdiag0};
     // variant 8 (default when pads == pmax): the fastest measured kernel per
     // epilogue -- v4 (7) for apply / residual at p <= 3, v3 with whole-array
     // buffer resources (9; falls back to 4 for arrays >= 2 GiB) otherwise

@@ -120,13 +120,20 @@ def basis_funs_ders(T: np.ndarray, p: int, x: float, span: int, nders: int) -> n
     return ders
 
 
-def assemble_1d(T: np.ndarray, p: int, nquad: int | None = None):
+def assemble_1d(T: np.ndarray, p: int, nquad: int | None = None, canonical: bool = True):
     """Banded 1D mass and stiffness factors ``(M_band, K_band)``, each ``(n, 2p+1)``.
 
     Element loop over non-empty knot spans with ``nquad`` (default ``p+1``)
     Gauss-Legendre points per element -- the quadrature the reference's
     ``assembly_1d``/``assembly_2d`` use (`sources/matrix_assembler.py:46-73`,
     ``k1 = V.quad_order``), exact for the degree-2p integrands.
+
+    ``canonical``: on uniform open knots every row in ``[2p, n - 2p)`` is the
+    same symmetric (Toeplitz) row mathematically, but the element loop leaves
+    rounding differences of a few ulp between rows.  Those rows are set to the
+    symmetrised middle row so the device kernels recognise the Toeplitz
+    interior bitwise (``poms_op_create``) and use their pair-sum fast paths.
+    The change is at the 1e-16 level (the golden-vector tests hold either way).
     """
     T = np.asarray(T, dtype=np.float64)
     n = len(T) - p - 1
@@ -150,7 +157,48 @@ def assemble_1d(T: np.ndarray, p: int, nquad: int | None = None):
                     k = j - i + p
                     M[i, k] += D[0, il] * D[0, jl] * w
                     K[i, k] += D[1, il] * D[1, jl] * w
+    if canonical and _uniform_interior(T, p) and n - 2 * p > 2 * p:
+        # the interior rows are samples of the centred cardinal B-spline of degree 2p+1
+        # (mass, times h) and of minus its second derivative (stiffness, over h): exact
+        # rationals, rounded once -- closer to the true integrals than any assembled row
+        h = float(np.unique(T)[1] - np.unique(T)[0])
+        cm, ck = _cardinal_rows(p)
+        M[2 * p:n - 2 * p] = h * cm
+        K[2 * p:n - 2 * p] = -ck / h
     return M, K
+
+
+_CARD: dict = {}
+
+
+def _cardinal_rows(p: int):
+    """Interior band rows of the uniform mass (/h) and second-derivative (*h) matrices."""
+    if p not in _CARD:
+        from fractions import Fraction
+        from math import comb, factorial
+        m = 2 * p + 1
+
+        def card(x, deriv):
+            e = m - deriv
+            acc = Fraction(0)
+            for j in range(m + 2):
+                t = x + Fraction(m + 1, 2) - j
+                if t > 0:
+                    acc += (-1) ** j * comb(m + 1, j) * t ** e
+            return acc / factorial(e)
+
+        _CARD[p] = (np.array([float(card(Fraction(k - p), 0)) for k in range(2 * p + 1)]),
+                    np.array([float(card(Fraction(k - p), 2)) for k in range(2 * p + 1)]))
+    return _CARD[p]
+
+
+def _uniform_interior(T: np.ndarray, p: int) -> bool:
+    """Open knot vector whose non-empty spans all have one length (to 1e-12)."""
+    inner = np.unique(np.asarray(T, dtype=np.float64))
+    if len(inner) < 3:
+        return False
+    d = np.diff(inner)
+    return bool(np.all(np.abs(d - d[0]) <= 1e-12 * d[0]))
 
 
 def band_to_dense(band: np.ndarray) -> np.ndarray:

@@ -50,7 +50,8 @@ def test_c_vcycle_matches_numpy_oracle():
     _, ipre, ipos = orc.vcycle_two_level([M] * 3, [K] * 3, P1, np.ones((nf,) * 3))
     _, _, ipos2 = orc.vcycle_two_level([M] * 3, [K] * 3, P1, np.ones((nf,) * 3), reorder=True)
     assert r["info_pre"]["niter"] == ipre["niter"] and r["info_pos"]["niter"] == ipos["niter"]
-    # the final residual sits at roundoff level (|x| ~ 1e5, ||r|| ~ 1e-3): two summation
-    # orders of the same oracle already differ by a few percent, so that is the bound
-    spread = abs(ipos2["res_norm"] - ipos["res_norm"])
-    assert abs(r["info_pos"]["res_norm"] - ipos["res_norm"]) <= 5 * spread + 1e-12
+    # the final residual sits at roundoff level (|x| ~ 1e5, ||r|| ~ 1e-3, i.e. 1e-8 of the
+    # scale): two summation orders of the same oracle already differ by percents, so only
+    # its order of magnitude is compared
+    assert ipos2["niter"] == ipos["niter"]
+    assert 0.5 * ipos["res_norm"] <= r["info_pos"]["res_norm"] <= 2.0 * ipos["res_norm"]
