@@ -33,7 +33,7 @@
 extern "C" {
 #endif
 
-#define POMS_ABI_VERSION 1
+#define POMS_ABI_VERSION 2
 
 /* operator forms (see poms_op_create) */
 #define POMS_FORM_SINGLE 0 /* y = F0 (x) F1 (x) F2 x                                  */
@@ -49,6 +49,10 @@ typedef struct poms_transfer poms_transfer; /* knot-insertion R = P^T / P       
 typedef struct poms_layout {
     int64_t n[3];    /* local interior extent per axis                       */
     int64_t pads[3]; /* ghost width per axis (storage pad)                   */
+    int64_t pitch;   /* row stride (doubles) of axis 2; 0 = n[2] + 2 pads[2].
+                      * A pitch that is a multiple of 16 together with a base
+                      * pointer whose column pads[2] sits on a 128-B line makes
+                      * every row segment of a 16k-column tile start on a line. */
 } poms_layout;
 
 /* ---- library / context ---------------------------------------------------- */
@@ -81,6 +85,10 @@ int poms_op_create(poms_ctx* ctx, int ndim, const poms_layout* layout, int form,
 int poms_op_destroy(poms_op* op);
 /* Planes per workgroup along axis 0 (3D); 0 = automatic. */
 int poms_op_set_chunk(poms_op* op, int chunk);
+/* Output columns per 64-lane tile of the v3 / v4 kernels (variants 4-9):
+ * 0 = 64 - 2 pmax (default); a multiple of 16 keeps stores line-aligned on an
+ * aligned layout (see poms_layout.pitch).  Must be <= 64 - 2 pmax.            */
+int poms_op_set_tile_cols(poms_op* op, int cols);
 /* Kernel variant.  All variants compute the same operator:
  *   0 = general (any band rows, any pads);
  *   1-3 = v2 Toeplitz-interior kernels (4x4, 8x2, 8x4 waves x rows);

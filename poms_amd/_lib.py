@@ -26,14 +26,15 @@ class PomsError(RuntimeError):
 
 
 class Layout(C.Structure):
-    _fields_ = [("n", C.c_int64 * 3), ("pads", C.c_int64 * 3)]
+    _fields_ = [("n", C.c_int64 * 3), ("pads", C.c_int64 * 3), ("pitch", C.c_int64)]
 
     @classmethod
-    def make(cls, n, pads):
+    def make(cls, n, pads, pitch=0):
         lay = cls()
         for d in range(3):
             lay.n[d] = int(n[d])
             lay.pads[d] = int(pads[d])
+        lay.pitch = int(pitch)
         return lay
 
 
@@ -55,6 +56,7 @@ _SIGS = {
     "poms_op_create": [_vp, _i, _LP, _i, _i, C.POINTER(C.c_void_p), _i64, _i64, _pp],
     "poms_op_destroy": [_vp],
     "poms_op_set_chunk": [_vp, _i],
+    "poms_op_set_tile_cols": [_vp, _i],
     "poms_op_set_variant": [_vp, _i],
     "poms_op_get_variant": [_vp, C.POINTER(_i)],
     "poms_op_apply": [_vp, _vp, _vp, _i64, _i64, _vp],

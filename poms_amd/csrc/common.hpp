@@ -22,6 +22,7 @@ struct KronGeom {
     int z_begin, z_end;  // output planes [z_begin, z_end)
     int chunk;           // output planes per workgroup (3D)
     int tiles2, tiles1, nchunks;
+    int tout;            // output columns per 64-column tile (v3 / v4 kernels; <= 64 - 2P)
 };
 
 // Padded row layout used by the row-wise vector kernels.

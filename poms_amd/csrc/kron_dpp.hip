@@ -45,7 +45,7 @@ kron_v3_kernel(const double* __restrict__ x, double* __restrict__ y,
                const double omega) {
     constexpr int W = 2 * P + 1;
     constexpr int NT = NW * 64;
-    constexpr int TO = 64 - 2 * P;          // output columns per tile
+    const int TO = g.tout;                     // output columns per tile
     constexpr int T1 = NW * R;
     constexpr int XR = T1 + 2 * P;
     constexpr int NRW = (XR + NW - 1) / NW;  // axis-2 rows per wave
@@ -95,7 +95,7 @@ kron_v3_kernel(const double* __restrict__ x, double* __restrict__ y,
     const int c0 = t2 * TO;             // first output column of the tile
     const int r0 = t1 * T1;
     const int i2 = c0 - P + lane;       // this lane's column (may be a halo column)
-    const bool col_ok = lane >= P && lane < 64 - P && i2 < g.n2;
+    const bool col_ok = lane >= P && lane < P + TO && i2 < g.n2;
 
     constexpr int WC = T2 ? 1 : W;
     double ca2[WC], cb2[WC];

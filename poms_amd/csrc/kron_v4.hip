@@ -63,7 +63,7 @@ kron_v4_kernel(const double* __restrict__ x, double* __restrict__ y,
                const ToepConst tc, const double omega) {
     constexpr int W = 2 * P + 1;
     constexpr int NT = NW * 64;
-    constexpr int TO = 64 - 2 * P;      // output columns per tile
+    const int TO = g.tout;                 // output columns per tile
     constexpr int T1 = 2 * NW;          // output rows per tile (one per half-wave)
     constexpr int XR = T1 + 2 * P;      // x rows per plane tile
     constexpr bool SUM = (FORM == FORM_SUM);
@@ -118,7 +118,7 @@ kron_v4_kernel(const double* __restrict__ x, double* __restrict__ y,
 #pragma unroll
     for (int e = 0; e < 2; ++e) {
         const int ci = 2 * j + e;
-        col_ok[e] = ci >= P && ci < 64 - P && cg0 + e < g.n2;
+        col_ok[e] = ci >= P && ci < P + TO && cg0 + e < g.n2;
     }
     const bool fast1 = (r0 >= tc.lo1) && (min(r0 + T1, g.n1) <= tc.hi1);
     const bool fast2 = (c0 >= tc.lo2) && (min(c0 + TO, g.n2) <= tc.hi2);

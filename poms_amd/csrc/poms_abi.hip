@@ -49,7 +49,7 @@ struct poms_ctx {
 
 struct poms_op {
     poms_ctx* ctx = nullptr;
-    int ndim = 3, form = FORM_SUM, pmax = 1, chunk = 0;
+    int ndim = 3, form = FORM_SUM, pmax = 1, chunk = 0, tout = 0;
     poms_layout L{};
     int64_t g0 = 0, n0g = 1;
     double *a0t = nullptr, *b0t = nullptr, *a1 = nullptr, *b1 = nullptr, *a2 = nullptr, *b2 = nullptr;
@@ -111,12 +111,12 @@ static bool layout_ok(const poms_layout* L) {
     if (!L) return false;
     for (int d = 0; d < 3; ++d)
         if (L->n[d] < 1 || L->pads[d] < 0) return false;
-    return true;
+    return L->pitch == 0 || L->pitch >= L->n[2] + 2 * L->pads[2];
 }
 
 static RowGeom row_geom(const poms_layout* L) {
     RowGeom g;
-    const int64_t c2 = L->n[2] + 2 * L->pads[2];
+    const int64_t c2 = L->pitch > 0 ? L->pitch : L->n[2] + 2 * L->pads[2];
     const int64_t c1 = L->n[1] + 2 * L->pads[1];
     g.s1 = c2;
     g.s0 = c1 * c2;
@@ -291,10 +291,43 @@ int poms_op_get_variant(poms_op* op, int* variant) {
     return 0;
 }
 
+int poms_op_set_tile_cols(poms_op* op, int cols) {
+    if (!op || cols < 0 || cols > 64 - 2 * op->pmax) { set_error("poms_op_set_tile_cols: bad argument"); return 1; }
+    op->tout = cols;
+    return 0;
+}
+
 int poms_op_set_chunk(poms_op* op, int chunk) {
     if (!op || chunk < 0) { set_error("poms_op_set_chunk: bad argument"); return 1; }
     op->chunk = chunk;
     return 0;
+}
+
+// Axis-0 chunk length.  A workgroup streams `chunk` planes plus 2p halo planes, so
+// long chunks save re-reads but leave a ragged last round of workgroups on the
+// 256 CUs (512 resident workgroups at p <= 3).  Cost of nc chunks ~ rounds(nc) *
+// (chunk + 2p), the partial last round weighted 5x its fill (fit to the chunk sweeps
+// in profiles/r01/chunks/*.log; picks 103 at 515^3 p=3, 43 at 258^3 p=2).  For
+// p >= 4 the kernels are VALU-bound and want >= 3 workgroups per CU instead.
+static int auto_chunk(int nz, int tiles, int p) {
+    if (nz <= 0) return 1;
+    tiles = std::max(tiles, 1);
+    if (p >= 4) {
+        const int nc = std::max(1, std::min(nz / 8, (768 + tiles - 1) / tiles));
+        return (nz + nc - 1) / nc;
+    }
+    const double slots = 512.0;
+    double best = 1e300;
+    int best_chunk = nz;
+    for (int nc = 1; nc <= std::max(1, nz / 8); ++nc) {
+        const int ch = (nz + nc - 1) / nc;
+        const double r = (double)nc * tiles / slots;
+        const double fr = std::floor(r);
+        const double rounds = r > 1.0 ? fr + std::min(1.0, (r - fr) * 5.0) : 1.0;
+        const double cost = rounds * (ch + 2 * p);
+        if (cost < best - 1e-9) { best = cost; best_chunk = ch; }
+    }
+    return best_chunk;
 }
 
 static int op_geom(poms_op* o, int64_t zb, int64_t ze, KronGeom& g) {
@@ -308,7 +341,8 @@ static int op_geom(poms_op* o, int64_t zb, int64_t ze, KronGeom& g) {
     g.tiles2 = (int)((o->L.n[2] + kron_tile_cols() - 1) / kron_tile_cols());
     const int trows = (o->variant == 3 || o->variant == 5) ? 32 : kron_tile_rows();
     g.tiles1 = (int)((o->L.n[1] + trows - 1) / trows);
-    if (o->variant >= 4) g.tiles2 = (int)((o->L.n[2] + (64 - 2 * o->pmax) - 1) / (64 - 2 * o->pmax));
+    g.tout = o->tout > 0 ? o->tout : 64 - 2 * o->pmax;
+    if (o->variant >= 4) g.tiles2 = (int)((o->L.n[2] + g.tout - 1) / g.tout);
     if (!is3d) {
         g.z_begin = 0; g.z_end = 1; g.chunk = 1; g.nchunks = 1;
         return 0;
@@ -318,11 +352,7 @@ static int op_geom(poms_op* o, int64_t zb, int64_t ze, KronGeom& g) {
     g.z_end = (int)ze;
     const int nz = (int)(ze - zb);
     int chunk = o->chunk;
-    if (chunk <= 0) {
-        const int tiles = g.tiles2 * g.tiles1;
-        const int want = std::max(1, (2048 + tiles - 1) / tiles);
-        chunk = std::max(16, (nz + want - 1) / want);
-    }
+    if (chunk <= 0) chunk = auto_chunk(nz, g.tiles2 * g.tiles1, o->pmax);
     chunk = std::max(1, std::min(chunk, std::max(nz, 1)));
     g.chunk = chunk;
     g.nchunks = nz == 0 ? 0 : (nz + chunk - 1) / chunk;
@@ -357,10 +387,18 @@ static int op_run(poms_op* o, int epi, double omega, const double* x, double* y,
     KronPtrs p{x, y, b, o->a0t, o->b0t, o->a1, o->b1, o->a2, o->b2,
                want_norm ? o->ctx->scratch : nullptr, want_dot ? o->ctx->scratch + nblk : nullptr, o->rdiag0};
     // variant 8 (default when pads == pmax): the fastest measured kernel per
-    // epilogue -- v4 (7) for apply / residual at p <= 3, v3 with whole-array
-    // buffer resources (9; falls back to 4 for arrays >= 2 GiB) otherwise
+    // epilogue (profiles/r01/chunks/*.log) -- in 3D v4 (7) for apply at p >= 3 and
+    // for every plain epilogue at p >= 4 (VALU-bound there), v3 with whole-array
+    // buffer resources (9; falls back to 4 for arrays >= 2 GiB) otherwise; in 2D
+    // v4 for apply / residual at p <= 3.  Fused dots and two-sweeps-from-zero: 9.
     int v = o->variant;
-    if (v == 8) v = ((epi == EPI_APPLY || epi == EPI_RESID) && o->pmax <= 3) ? 7 : 9;
+    if (v == 8) {
+        const bool plain = epi == EPI_APPLY || epi == EPI_RESID || epi == EPI_JACOBI;
+        if (o->ndim == 3)
+            v = ((epi == EPI_APPLY && o->pmax >= 3) || (plain && o->pmax >= 4)) ? 7 : 9;
+        else
+            v = ((epi == EPI_APPLY || epi == EPI_RESID) && o->pmax <= 3) ? 7 : 9;
+    }
     const int rc = v == 0
         ? kron_launch(o->pmax, o->ndim == 3, o->form, epi, p, g, omega, as_stream(stream))
         : (v == 7 || (v >= 92 && v <= 100))
@@ -418,8 +456,7 @@ int poms_op_jacobi_from_zero(poms_op* op, double omega, const double* b, double*
 
 int poms_op_from_zero_supported(poms_op* op, int* yes) {
     if (!op || !yes) { set_error("poms_op_from_zero_supported: null argument"); return 1; }
-    const int64_t bytes = (int64_t)(op->L.n[0] + 2 * op->L.pads[0]) * (op->L.n[1] + 2 * op->L.pads[1]) *
-                          (op->L.n[2] + 2 * op->L.pads[2]) * 8;
+    const int64_t bytes = (int64_t)(op->L.n[0] + 2 * op->L.pads[0]) * row_geom(&op->L).s0 * 8;
     *yes = (op->ndim == 3 && (op->variant == 8 || op->variant == 9) && bytes < 0x7fffffffLL) ? 1 : 0;
     return 0;
 }

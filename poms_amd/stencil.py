@@ -42,7 +42,7 @@ class StencilVectorSpace:
     """
 
     def __init__(self, npts: Sequence[int], pads: Sequence[int], periods=None, *,
-                 dist: SlabDistribution | None = None, device=None):
+                 dist: SlabDistribution | None = None, device=None, align: bool = False):
         npts, pads = tuple(int(v) for v in npts), tuple(int(v) for v in pads)
         if not 1 <= len(npts) <= 3 or len(pads) != len(npts):
             raise ValueError("npts/pads must have 1..3 equal-length entries")
@@ -65,8 +65,25 @@ class StencilVectorSpace:
         lead = 3 - self.ndim
         self.n3 = (1,) * lead + self.local_npts
         self.p3 = (0,) * lead + self.pads
-        self.layout = _lib.Layout.make(self.n3, self.p3)
         self.padded_shape = tuple(n + 2 * p for n, p in zip(self.local_npts, self.pads))
+        # HBM layout.  With ``align`` rows of axis 2 are `pitch` doubles apart (a
+        # multiple of 16 = one 128-B line) and the array starts `shift` doubles into
+        # its buffer, so interior column 0 of every row starts a line and a tile
+        # whose output columns are a multiple of 16 stores whole lines only.  Off by
+        # default: measured no faster at 515^3 (profiles/r01/align/), while the
+        # 48-column tiles it needs cost 10-15 % (more halo lanes).
+        n2p = self.padded_shape[-1]
+        self.aligned = bool(align) and self.ndim >= 2
+        if self.aligned:
+            self.pitch = -(-n2p // 16) * 16
+            self.shift = (16 - self.pads[-1] % 16) % 16
+        else:
+            self.pitch, self.shift = n2p, 0
+        lead_shape = self.padded_shape[:-1]
+        self.strides = tuple(int(np.prod(lead_shape[i + 1:])) * self.pitch for i in range(len(lead_shape))) + (1,)
+        self.plane_elems = self.strides[0] if self.ndim == 3 else int(np.prod(lead_shape)) * self.pitch
+        self.store_elems = self.padded_shape[0] * self.strides[0] + self.shift + (16 if self.aligned else 0)
+        self.layout = _lib.Layout.make(self.n3, self.p3, self.pitch if self.aligned else 0)
         self.dimension = int(np.prod(npts))
         self.device = rt.device_index(device)
         self.ctx = rt.ctx(self.device)
@@ -85,9 +102,19 @@ class StencilVectorSpace:
     def zeros(self) -> "StencilVector":
         return StencilVector(self)
 
+    def view(self, store: torch.Tensor) -> torch.Tensor:
+        """The padded array (``padded_shape``) inside a flat buffer of ``store_elems``."""
+        return torch.as_strided(store, self.padded_shape, self.strides, self.shift)
+
+    def planes(self, store: torch.Tensor) -> torch.Tensor:
+        """The padded array as contiguous rows of whole axis-0 planes (3D), for the
+        slab ghost exchange (a plane includes its dead row-pitch columns)."""
+        return torch.as_strided(store, (self.padded_shape[0], self.plane_elems), (self.plane_elems, 1), self.shift)
+
     def empty(self) -> "StencilVector":
         """Vector with unspecified interior and zero ghost cells (no full memset)."""
-        t = torch.empty(self.padded_shape, dtype=F64, device=f"cuda:{self.device}")
+        store = torch.empty(self.store_elems, dtype=F64, device=f"cuda:{self.device}")
+        t = self.view(store)
         for ax, p in enumerate(self.pads):
             if p:
                 idx = [slice(None)] * self.ndim
@@ -95,7 +122,11 @@ class StencilVectorSpace:
                 t[tuple(idx)] = 0.0
                 idx[ax] = slice(t.shape[ax] - p, t.shape[ax])
                 t[tuple(idx)] = 0.0
-        return StencilVector(self, _data=t)
+        if self.pitch > self.padded_shape[-1]:   # dead columns: finite, never NaN
+            dead = torch.as_strided(store, self.padded_shape[:-1] + (self.pitch - self.padded_shape[-1],),
+                                    self.strides[:-1] + (1,), self.shift + self.padded_shape[-1])
+            dead.zero_()
+        return StencilVector(self, _store=store)
 
     def scalar_buffer(self) -> torch.Tensor:
         if self._scal is None:
@@ -157,13 +188,14 @@ class StencilVector:
 
     __array_priority__ = 100
 
-    def __init__(self, V: StencilVectorSpace, *, _data: torch.Tensor | None = None):
+    def __init__(self, V: StencilVectorSpace, *, _store: torch.Tensor | None = None):
         self._space = V
-        if _data is None:
-            _data = torch.zeros(V.padded_shape, dtype=F64, device=f"cuda:{V.device}")
-        if tuple(_data.shape) != V.padded_shape or _data.dtype != F64 or not _data.is_contiguous():
-            raise ValueError("data does not match the space layout")
-        self._data = _data
+        if _store is None:
+            _store = torch.zeros(V.store_elems, dtype=F64, device=f"cuda:{V.device}")
+        if _store.dim() != 1 or _store.numel() != V.store_elems or _store.dtype != F64 or not _store.is_contiguous():
+            raise ValueError("buffer does not match the space layout")
+        self._store = _store
+        self._data = V.view(_store)
         self._ghost_valid = True
 
     # -- spl surface ----------------------------------------------------
@@ -191,7 +223,7 @@ class StencilVector:
         self._ghost_valid = not self._space.is_distributed
 
     def copy(self) -> "StencilVector":
-        out = StencilVector(self._space, _data=self._data.clone())
+        out = StencilVector(self._space, _store=self._store.clone())
         out._ghost_valid = self._ghost_valid
         return out
 
@@ -267,7 +299,7 @@ class StencilVector:
     def update_ghost_regions(self, direction=None) -> None:
         V = self._space
         if V.is_distributed and (direction is None or direction == 0):
-            V.dist.exchange(self._data, width=V.pads[0], pad=V.pads[0])
+            V.dist.exchange(V.planes(self._store), width=V.pads[0], pad=V.pads[0])
             self._ghost_valid = True
 
     def toarray(self) -> np.ndarray:
@@ -498,6 +530,10 @@ class KronOperator:
     def set_chunk(self, chunk: int) -> None:
         _lib.call("poms_op_set_chunk", self._h, int(chunk))
 
+    def set_tile_cols(self, cols: int) -> None:
+        """Output columns per 64-lane tile of the v3/v4 kernels (0 = 64 - 2 pmax)."""
+        _lib.call("poms_op_set_tile_cols", self._h, int(cols))
+
     def set_variant(self, variant: int) -> None:
         """0 = general kernel, 1/2 = Toeplitz-interior kernels (see poms_hip.h)."""
         _lib.call("poms_op_set_variant", self._h, int(variant))
@@ -523,7 +559,7 @@ class KronOperator:
         handle = None
         if V.is_distributed and not x._ghost_valid:
             p0 = V.pads[0]
-            handle = V.dist.start_exchange(x._data, width=p0, pad=p0)
+            handle = V.dist.start_exchange(V.planes(x._store), width=p0, pad=p0)
             if handle is not None and n0 > 2 * self.pmax:
                 ranges = [(self.pmax, n0 - self.pmax), (0, self.pmax), (n0 - self.pmax, n0)]
             else:

@@ -253,3 +253,37 @@ def test_apply_fused_inner(gpu, variant, ndim, cells, p):
     assert abs(pq - want) <= 1e-12 * (abs(want) + np.linalg.norm(x.to_local_numpy()) * np.linalg.norm(ref))
     A.set_variant(7)
     assert not A.apply_dot_supported
+
+
+@pytest.mark.parametrize("p,cells", [(2, (20, 24, 131)), (3, (25, 18, 140)), (5, (14, 12, 100))])
+@pytest.mark.parametrize("variant", [7, 8, 9])
+@pytest.mark.parametrize("tile_cols", [0, 48, 32])
+def test_aligned_layout_and_tile_cols(gpu, p, cells, variant, tile_cols):
+    """Line-aligned row pitch (poms_layout.pitch) and narrower v3/v4 tiles give the
+    same apply / residual / Jacobi results as the default layout and tiles."""
+    from poms_amd.stencil import KronOperator, StencilVectorSpace
+    if tile_cols > 64 - 2 * p:
+        pytest.skip("tile wider than 64 - 2p")
+    rng = np.random.default_rng(77 + p)
+    F = [assemble_1d(uniform_knots(p, N), p) for N in cells]
+    n = [N + p for N in cells]
+    x0, b0 = rng.standard_normal(n), rng.standard_normal(n)
+    out = {}
+    for align in (False, True):
+        V = StencilVectorSpace(n, [p] * 3, align=align)
+        assert V.aligned == align
+        if align:
+            assert V.pitch % 16 == 0 and (V.shift + p) % 16 == 0
+        A = KronOperator.laplace(V, [f[0] for f in F], [f[1] for f in F])
+        A.set_variant(variant)
+        if align:
+            A.set_tile_cols(tile_cols)
+        x, b = V.zeros().from_numpy(x0), V.zeros().from_numpy(b0)
+        y, r, xn = V.zeros(), V.zeros(), V.zeros()
+        A.dot(x, out=y)
+        A.residual(b, x, out=r)
+        nrm = A.jacobi_sweep(b, x, xn, 2.0 / 3.0, want_norm=True)
+        out[align] = (y.toarray(), r.toarray(), xn.toarray(), nrm)
+    for k in range(3):
+        assert rel(out[True][k], out[False][k]) <= 1e-14, k
+    assert abs(out[True][3] - out[False][3]) <= 1e-12 * abs(out[False][3])

@@ -27,9 +27,13 @@ def main():
     ap.add_argument("--reps", type=int, default=10)
     ap.add_argument("--rounds", type=int, default=3)
     ap.add_argument("--chunks", type=str, default="0")
+    ap.add_argument("--tile-cols", type=str, default="0", help="comma list of v3/v4 output columns per tile")
+    ap.add_argument("--no-align", action="store_true", help="unpadded row pitch (n2 + 2p)")
     ap.add_argument("--variants", type=str, default="")
     ap.add_argument("--kinds", type=str, default="apply,jacobi")
     ap.add_argument("--json", type=str, default="")
+    ap.add_argument("--flush", action="store_true",
+                    help="write a 512 MiB buffer before every timed launch (evicts L2 and the 256 MiB MALL)")
     a = ap.parse_args()
 
     import torch
@@ -39,19 +43,22 @@ def main():
     p, N, nd = a.p, a.cells, a.ndim
     M, K = assemble_1d(uniform_knots(p, N), p)
     n = N + p
-    V = StencilVectorSpace([n] * nd, [p] * nd)
+    V = StencilVectorSpace([n] * nd, [p] * nd, align=not a.no_align)
     A = KronOperator.laplace(V, [M] * nd, [K] * nd)
     x, b, y = V.zeros(), V.zeros(), V.zeros()
     V.interior(x._data).uniform_(-1, 1)
     V.interior(b._data).uniform_(-1, 1)
     dof = n ** nd
+    flush = torch.zeros(64 << 20, dtype=torch.float64, device="cuda") if a.flush else None
     chunks = [int(c) for c in a.chunks.split(",")]
+    tile_cols = [int(c) for c in a.tile_cols.split(",")]
     variants = [int(v) for v in a.variants.split(",")] if a.variants else [None]
     kinds = a.kinds.split(",")
     res = {}
     for rnd in range(a.rounds):
-        for ch in chunks:
+        for ch, tcols in [(c, t) for c in chunks for t in tile_cols]:
             A.set_chunk(ch)
+            A.set_tile_cols(tcols)
             for var in variants:
                 if var is not None:
                     A.set_variant(var)
@@ -66,6 +73,8 @@ def main():
                     A.timer = []
                     ev = []
                     for _ in range(a.reps):
+                        if flush is not None:
+                            flush.add_(1.0)
                         e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
                         e0.record()
                         fn()
@@ -77,12 +86,12 @@ def main():
                     else:         # whole call (dot includes its reduction + host read)
                         ts = [e0.elapsed_time(e1) * 1e3 for e0, e1 in ev]
                     A.timer = None
-                    res.setdefault((ch, var, kind), []).extend(ts)
+                    res.setdefault((ch, tcols, var, kind), []).extend(ts)
     out = []
-    for (ch, var, kind), ts in res.items():
+    for (ch, tcols, var, kind), ts in res.items():
         med = statistics.median(ts)
         bpd = 16 if kind in ("apply", "dot") else 24
-        row = {"chunk": ch, "variant": var, "kind": kind, "median_us": med, "min_us": min(ts),
+        row = {"chunk": ch, "tile_cols": tcols, "aligned": not a.no_align, "variant": var, "kind": kind, "median_us": med, "min_us": min(ts),
                "GBps": bpd * dof / med / 1e3, "GDOFps": dof / med / 1e3}
         out.append(row)
         print(json.dumps(row), flush=True)

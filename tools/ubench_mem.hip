@@ -68,6 +68,39 @@ __global__ void __launch_bounds__(512) tile_write(double* y, int n, int s1, long
     }
 }
 
+// Jacobi-like traffic: per plane and workgroup read x (16 + 6 rows x 64 columns),
+// read b and write y (16 rows x OUTC columns).  `shift` moves the whole grid inside
+// the row (pitch > 521) so that output segments can start on a 128-B line.
+template <int OUTC>
+__global__ void __launch_bounds__(512) tile_jac(const double* x, const double* b, double* y, int n, int s1, long s0,
+                                                int tiles2, int tiles1, int chunk, int shift) {
+    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    int bid = blockIdx.x;
+    const int t2 = bid % tiles2; bid /= tiles2;
+    const int t1 = bid % tiles1;
+    const int ch = bid / tiles1;
+    const int z0 = ch * chunk, z1 = min(z0 + chunk, n);
+    const int c0 = t2 * OUTC;
+    const int halo = (64 - OUTC) / 2;
+    const int xc = min(max(c0 - halo + lane, -3), n + 2) + 3 + shift;   // padded column of this lane's x
+    const int oc = c0 + lane;                                         // interior output column
+    for (int z = z0; z < z1; ++z) {
+        double acc = 0.0;
+        const long pl = (long)(z + 3) * s0;
+        for (int r = wv; r < 22; r += 8) {
+            const int row = min(t1 * 16 + r - 3, n + 2) + 3;
+            acc += x[pl + (long)row * s1 + xc];
+        }
+        for (int r = 0; r < 2; ++r) {
+            const int row = t1 * 16 + wv * 2 + r;
+            if (row < n && oc < n && lane < OUTC) {
+                const long o = pl + (long)(row + 3) * s1 + oc + 3 + shift;
+                y[o] = b[o] + 0.1 * acc;
+            }
+        }
+    }
+}
+
 template <typename F>
 static float time_it(F f) {
     hipEvent_t e0, e1;
@@ -95,7 +128,9 @@ int main() {
     // host-side bound check of the largest index any tile_write launch below can touch
     auto max_index = [&](long pitch, long plane, int coff) { return (long)(n - 1 + 3) * plane + (long)(n - 1 + 3) * pitch + (n - 1) + coff + 1; };
     if (max_index(528, 528L * S, 3) >= alloc || max_index(S, s0, 3) >= alloc) { printf("bad bounds\n"); return 1; }
-    double *x, *y;
+    double *x, *y, *bb;
+    CK(hipMalloc(&bb, alloc * 8));
+    CK(hipMemset(bb, 0, alloc * 8));
     CK(hipMalloc(&x, alloc * 8));
     CK(hipMalloc(&y, alloc * 8));
     CK(hipMemset(x, 0, alloc * 8));
@@ -138,6 +173,28 @@ int main() {
         printf("w6 tile 16x64, 128-B aligned rows: %.1f us  %.2f TB/s of y\n", ms * 1e3, dof * 8 / (ms * 1e-3) / 1e12);
         ms = time_it([&] { hipLaunchKernelGGL((tile_write<64, 1>), dim3(tiles2 * tiles1 * nch), dim3(512), 0, 0, y, n, S2, s02, tiles2, tiles1, chunk, 3); });
         printf("w7 tile 16x64, aligned pitch, 24-B offset: %.1f us  %.2f TB/s of y\n", ms * 1e3, dof * 8 / (ms * 1e-3) / 1e12);
+    }
+    {   // Jacobi-like mixes (24 algorithmic B/DOF); shift 13 puts padded column 3 on a 128-B line
+        const int tiles1 = (n + 15) / 16, chunk = 103, nch = (n + chunk - 1) / chunk;
+        const long need = (long)(n + 6) * 528L * S + 16;
+        if (need > alloc || (long)(n + 6) * s0 + 16 > alloc) { printf("bad bounds\n"); return 1; }
+        struct Cfg { const char* name; int outc; int pitch; int shift; };
+        const Cfg cfgs[] = {{"j1 58 cols, pitch 521 (current)", 58, S, 0},
+                            {"j2 58 cols, pitch 528, unaligned", 58, 528, 0},
+                            {"j3 48 cols, pitch 528, 128-B aligned", 48, 528, 13},
+                            {"j4 48 cols, pitch 528, unaligned", 48, 528, 0},
+                            {"j5 56 cols, pitch 528, start aligned", 56, 528, 13}};
+        for (const Cfg& c : cfgs) {
+            const long pl = (long)c.pitch * S;
+            const int tiles2 = (n + c.outc - 1) / c.outc;
+            if (c.outc == 58)
+                ms = time_it([&] { hipLaunchKernelGGL((tile_jac<58>), dim3(tiles2 * tiles1 * nch), dim3(512), 0, 0, x, bb, y, n, c.pitch, pl, tiles2, tiles1, chunk, c.shift); });
+            else if (c.outc == 56)
+                ms = time_it([&] { hipLaunchKernelGGL((tile_jac<56>), dim3(tiles2 * tiles1 * nch), dim3(512), 0, 0, x, bb, y, n, c.pitch, pl, tiles2, tiles1, chunk, c.shift); });
+            else
+                ms = time_it([&] { hipLaunchKernelGGL((tile_jac<48>), dim3(tiles2 * tiles1 * nch), dim3(512), 0, 0, x, bb, y, n, c.pitch, pl, tiles2, tiles1, chunk, c.shift); });
+            printf("%s: %.1f us  %.2f TB/s (24 B/DOF)\n", c.name, ms * 1e3, dof * 24 / (ms * 1e-3) / 1e12);
+        }
     }
     return 0;
 }
