@@ -97,8 +97,12 @@ int poms_op_set_tile_cols(poms_op* op, int cols);
  *   7 = v4: axis-1-first, x planes DMA'd into an LDS ring (buffer_load ... lds),
  *       two columns per lane, symmetric Toeplitz pair sums;
  *   8 = auto (default when pads == pmax): the fastest measured kernel per epilogue;
- *   9 = v3 addressing each array through one buffer resource (arrays < 2 GiB).
- * Variants 1-8 need storage pads == pmax on every used axis.                  */
+ *   9 = v3 addressing each array through one buffer resource (arrays < 2 GiB);
+ *  10 = v5: 128-column tiles (112 line-aligned output columns on an aligned
+ *       layout), one row per wave, x DMA'd into an LDS ring, axis-1-first
+ *       (3D FORM_SUM, arrays < 2 GiB; other operators and two-sweeps-from-zero
+ *       run variant 9).
+ * Variants 1-10 need storage pads == pmax on every used axis.                 */
 int poms_op_set_variant(poms_op* op, int variant);
 int poms_op_get_variant(poms_op* op, int* variant);
 
@@ -111,7 +115,7 @@ int poms_op_apply(poms_op* op, const double* x, double* y, int64_t z_begin,
 /* y = A x, also accumulating x . y per block into scratch[count, 2 count)
  * (count from poms_op_last_partials; reduce with poms_reduce_partials_at).
  * pcg's `q = A.dot(p)` + `p.dot(q)` (`sources/solvers.py:103-104`) in one
- * pass.  Kernel variants 4, 5, 6, 8, 9 (poms_op_apply_dot_supported).        */
+ * pass.  Kernel variants 4, 5, 6, 8, 9, 10 (poms_op_apply_dot_supported).    */
 int poms_op_apply_dot(poms_op* op, const double* x, double* y, int64_t z_begin,
                       int64_t z_end, void* stream);
 int poms_op_apply_dot_supported(poms_op* op, int* yes);
@@ -132,7 +136,7 @@ int poms_op_jacobi_sweep(poms_op* op, double omega, const double* b,
  * scratch[count, 2 count) with count from poms_op_last_partials; reduce them
  * with poms_reduce_partials_at.  With b = r this is pcg's `sr = s.dot(r)`
  * (`sources/solvers.py:91,120`) fused into the last smoothing sweep.
- * Kernel variants 4-9 only (poms_op_fused_dot_supported).                    */
+ * Kernel variants 4-10 only (poms_op_fused_dot_supported).                   */
 int poms_op_jacobi_sweep_dot(poms_op* op, double omega, const double* b,
                              const double* x_in, double* x_out, int64_t z_begin,
                              int64_t z_end, int want_norm, void* stream);
@@ -142,7 +146,7 @@ int poms_op_fused_dot_supported(poms_op* op, int* yes);
  * x_out = x1 + omega (b - A x1) / diag(A).  With want_norm, ||dr_2||^2 partials
  * go to scratch[0, count) and ||x1||^2 = ||dr_1||^2 partials to
  * scratch[count, 2 count).  Replaces the first two iterations of
- * `sources/solvers.py:207-219` (x0 = None).  3D, variants 8/9, arrays < 2 GiB
+ * `sources/solvers.py:207-219` (x0 = None).  3D, variants 8-10, arrays < 2 GiB
  * (poms_op_from_zero_supported).                                              */
 int poms_op_jacobi_from_zero(poms_op* op, double omega, const double* b, double* x_out,
                              int64_t z_begin, int64_t z_end, int want_norm, void* stream);

@@ -113,6 +113,14 @@ __device__ __forceinline__ void bstore2_p(__amdgpu_buffer_rsrc_t r, int off_byte
     __builtin_amdgcn_raw_buffer_store_b128(v, r, off_bytes, 0, AUX);
 }
 
+// 16-B store of two doubles with a scalar (per-plane) offset on a whole-array resource
+__device__ __forceinline__ void bstore2_s(__amdgpu_buffer_rsrc_t r, int voff, unsigned soff, double d0, double d1) {
+    u32x4 v;
+    const u32x2 a = __builtin_bit_cast(u32x2, d0), b = __builtin_bit_cast(u32x2, d1);
+    v.x = a.x; v.y = a.y; v.z = b.x; v.w = b.y;
+    __builtin_amdgcn_raw_buffer_store_b128(v, r, voff, (int)soff, 0);
+}
+
 // bytes of `planes_left` padded planes of s0 doubles, clamped to 2^31-1
 __device__ __forceinline__ uint32_t plane_bytes(int64_t planes_left, int64_t s0) {
     if (planes_left <= 0) return 0u;

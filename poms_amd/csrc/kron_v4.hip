@@ -212,15 +212,17 @@ kron_v4_kernel(const double* __restrict__ x, double* __restrict__ y,
                 } else if constexpr (!IS3D) {
                     wait_vm<0>();
                 } else if constexpr (HASB) {
-                    // after b(t) (issued in iteration t-1): that iteration's x DMAs + 2 stores
+                    // Loads return in order but a store may be acknowledged before an
+                    // older load returns: count only the LOADS issued after the one
+                    // waited for.  After b(t) (issued in iteration t-1): that iteration's x DMAs
                     if (t == 0) wait_vm<0>();
-                    else if (wv < P) wait_vm<2 + 2>();
-                    else wait_vm<1 + 2>();
+                    else if (wv < P) wait_vm<2>();
+                    else wait_vm<1>();
                 } else {
-                    // after x(t) (issued in iteration t-PFX): its 2 stores + (PFX-1) x (x DMAs + 2 stores)
+                    // after x(t) (issued in iteration t-PFX): (PFX-1) iterations' x DMAs
                     if (t < PFX) wait_vm<0>();
-                    else if (wv < P) wait_vm<(PFX - 1) * (2 + 2) + 2>();
-                    else wait_vm<(PFX - 1) * (1 + 2) + 2>();
+                    else if (wv < P) wait_vm<(PFX - 1) * 2>();
+                    else wait_vm<(PFX - 1) * 1>();
                 }
                 if constexpr (MODE != 4 && MODE != 7) __builtin_amdgcn_s_barrier();
                 // ---- prefetch (dummies past the end keep the counts fixed)

@@ -1,0 +1,491 @@
+// Fused Kronecker-sum operator, v5 (variant 10): 128-column tiles, one row per
+// wave, x planes DMA'd into an LDS ring, axis 1 first.
+//
+// Why this shape (tools/ubench_copy.hip, tools/ubench_rowtile.hip at 515^3):
+// the 64-column tiles of v3/v4 store 58-column row segments that start anywhere
+// in a 128-B line, so two workgroups write parts of the same line at different
+// times; the access pattern alone (no arithmetic) ran 621-681 us against
+// 436 us for a plain copy of the same bytes.  128-column tiles whose 112 output
+// columns start on a line (the aligned layout: row pitch a multiple of 16
+// doubles, interior column 0 on a line) write whole lines only, and ran 513 us.
+//
+//   * workgroup: 16 waves = 16 output rows (axis 1) x 128 lane-columns (each
+//     lane owns two adjacent columns: 16-B loads / stores), marching a chunk of
+//     axis-0 planes.  The first H and last 128-H-TO lane-columns are halo
+//     (H = 8, TO = 112 on the aligned layout; H = P rounded up to even,
+//     TO = 128 - 2H otherwise);
+//   * memory: each x plane tile (T1 + 2P rows x 128 columns) is DMA'd by
+//     buffer_load ... lds straight into a D-deep LDS ring, D-1 planes ahead;
+//     b (residual / Jacobi) through a 2-deep ring one plane ahead.  vmcnt is
+//     counted by hand, one barrier per plane;
+//   * axis 1 (first) on the wave's own row: u = F1a x, v = F1b x (symmetric
+//     Toeplitz pair sums inside the interior, per-row scalar coefficients
+//     outside); axis 2 with the column neighbours shifted in by DPP
+//     (c = F2a u, d = F2a v + F2b u); axis 0 scattered into 2P+1 rotating
+//     accumulators;
+//   * epilogues: APPLY, RESID, JACOBI (x_in of the output plane DMA'd next to
+//     b; 1/diag from the host table inside the Toeplitz interior, else from the
+//     plane-invariant pieces of the diagonal), APPLYDOT (x . Ax, with x at the
+//     output point from a P-deep register history of the lane's centre tap).
+// Preconditions (host): 3D, FORM_SUM, P <= 3, storage pads == P, array < 2 GiB.
+#include "common.hpp"
+
+namespace poms {
+
+typedef __attribute__((address_space(3))) void lds5_void_t;
+
+__device__ __forceinline__ void dma16s(__amdgpu_buffer_rsrc_t r, double* lds_dst, int voff, unsigned soff) {
+    __builtin_amdgcn_raw_ptr_buffer_load_lds(r, (lds5_void_t*)lds_dst, 16, voff, (int)soff, 0, 0);
+}
+
+__device__ __forceinline__ double v5_shr1(double v) {  // lane l <- lane l-1 (lane 0 <- 0)
+    const int2 w = __builtin_bit_cast(int2, v);
+    const int lo = __builtin_amdgcn_update_dpp(0, w.x, 0x138, 0xf, 0xf, true);
+    const int hi = __builtin_amdgcn_update_dpp(0, w.y, 0x138, 0xf, 0xf, true);
+    return __builtin_bit_cast(double, make_int2(lo, hi));
+}
+__device__ __forceinline__ double v5_shl1(double v) {  // lane l <- lane l+1 (lane 63 <- 0)
+    const int2 w = __builtin_bit_cast(int2, v);
+    const int lo = __builtin_amdgcn_update_dpp(0, w.x, 0x130, 0xf, 0xf, true);
+    const int hi = __builtin_amdgcn_update_dpp(0, w.y, 0x130, 0xf, 0xf, true);
+    return __builtin_bit_cast(double, make_int2(lo, hi));
+}
+
+template <int N>
+__device__ __forceinline__ void v5_wait_vm() {  // s_waitcnt vmcnt(N) (gfx9 encoding)
+    static_assert(N >= 0 && N < 64, "vmcnt range");
+    __builtin_amdgcn_s_waitcnt((N & 15) | (7 << 4) | (15 << 8) | ((N >> 4) << 14));
+}
+
+__device__ __forceinline__ void v5_barrier() {
+    __asm__ volatile("" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    __asm__ volatile("" ::: "memory");
+}
+
+template <int P, int EPI, int D>
+__global__ void __launch_bounds__(1024, 1)
+kron_v5_kernel(const double* __restrict__ x, double* __restrict__ y, const double* __restrict__ bvec,
+               const double* __restrict__ a0t, const double* __restrict__ b0t,
+               const double* __restrict__ a1, const double* __restrict__ b1,
+               const double* __restrict__ a2, const double* __restrict__ b2,
+               double* __restrict__ partial, double* __restrict__ partial2,
+               const double* __restrict__ rdiag0, const KronGeom g, const ToepConst tc,
+               const int H, const double omega) {
+    constexpr int W = 2 * P + 1;
+    constexpr int NW = 16;
+    constexpr int T1 = NW;              // output rows per tile: one per wave
+    constexpr int XR = T1 + 2 * P;      // x rows per plane tile
+    constexpr int TC = 128;             // lane-columns per tile
+    constexpr int NS = W;               // rotating axis-0 accumulators
+    constexpr int PFX = D - 1;          // x prefetch distance (planes)
+    constexpr bool HASB = (EPI == EPI_RESID) || (EPI == EPI_JACOBI);
+    constexpr bool JAC = (EPI == EPI_JACOBI);
+    constexpr bool APD = (EPI == EPI_APPLYDOT);
+    constexpr bool HIST = APD;          // x at the output point from a register history
+    constexpr bool XIN = JAC;           // ... or DMA'd next to b (saves VGPRs in the Jacobi sweep)
+    constexpr int NWIN = 2 * P + 2;     // columns 2j-P .. 2j+1+P of a lane's pair
+    static_assert(D >= 3 || !HASB, "the b ring's wait count assumes x(t) was issued before b(t)");
+    typedef double d2 __attribute__((ext_vector_type(2)));
+
+    constexpr int XS_OFF = 0;
+    constexpr int BS_OFF = XS_OFF + D * XR * TC;
+    constexpr int XI_OFF = BS_OFF + (HASB ? 2 * T1 * TC : 0);
+    constexpr int C2_OFF = XI_OFF + (XIN ? 2 * T1 * TC : 0);
+    constexpr int RED_OFF = C2_OFF + 2 * W * TC;
+    constexpr int LDS_N = RED_OFF + NW;
+    __shared__ __attribute__((aligned(16))) double lds[LDS_N];
+
+    const int tid = threadIdx.x;
+    const int lane = tid & 63;
+    const int wv = __builtin_amdgcn_readfirstlane(tid >> 6);
+
+    const int nblk = gridDim.x;
+    int bid;
+    {   // consecutive tiles on one XCD (round-robin dispatch over the 8 XCDs)
+        const int b = blockIdx.x, q = nblk >> 3, rr = nblk & 7, xcd = b & 7, k = b >> 3;
+        bid = (xcd < rr ? xcd * (q + 1) : rr * (q + 1) + (xcd - rr) * q) + k;
+    }
+    const int TO = g.tout;
+    const int t2 = bid % g.tiles2;
+    bid /= g.tiles2;
+    const int t1 = bid % g.tiles1;
+    const int ch = bid / g.tiles1;
+    const int c0 = t2 * TO;             // lane-column ci <-> interior column c0 - H + ci
+    const int r0 = t1 * T1;
+    const int orow = r0 + wv;           // this wave's output row
+    const bool row_ok = orow < g.n1;
+    const int cg0 = c0 - H + 2 * lane;  // interior column of this lane's element 0
+    bool col_ok[2];
+#pragma unroll
+    for (int e = 0; e < 2; ++e) {
+        const int ci = 2 * lane + e;
+        col_ok[e] = ci >= H && ci < H + TO && cg0 + e < g.n2;
+    }
+    const bool fast1 = orow >= tc.lo1 && orow < tc.hi1;                          // per wave
+    const bool fast2 = (c0 >= tc.lo2) && (min(c0 + TO, g.n2) <= tc.hi2);         // per workgroup
+
+    // axis-2 band rows of the tile's columns (only outside the Toeplitz interior)
+    if (!fast2) {
+        for (int e = tid; e < W * TC; e += NW * 64) {
+            const int k = e / TC, ci = e - k * TC;
+            const int col = min(max(c0 - H + ci, 0), g.n2 - 1);
+            lds[C2_OFF + e] = a2[col * W + k];
+            lds[C2_OFF + W * TC + e] = b2[col * W + k];
+        }
+    }
+    // this wave's axis-1 band row (read by scalar loads where used: kept out of
+    // SGPRs, which the per-plane axis-0 coefficients and Toeplitz constants fill)
+    const int orc = min(orow, g.n1 - 1);
+    const double* __restrict__ ra = a1 + orc * W;
+    const double* __restrict__ rb = b1 + orc * W;
+    // plane-invariant parts of diag(A) = d0a X + d0b Y at this lane's columns
+    double dX[2] = {0.0, 0.0}, dY[2] = {0.0, 0.0};
+    if constexpr (JAC) {
+        const double d1a = ra[P], d1b = rb[P];
+#pragma unroll
+        for (int e = 0; e < 2; ++e) {
+            const int col = min(max(cg0 + e, 0), g.n2 - 1);
+            const double d2a = a2[col * W + P], d2b = b2[col * W + P];
+            dX[e] = d1a * d2a;
+            dY[e] = fma(d1b, d2a, d1a * d2b);
+        }
+    }
+
+    const int z0 = g.z_begin + ch * g.chunk;
+    const int z1 = min(z0 + g.chunk, g.z_end);
+    const int nplanes = (z1 - z0) + 2 * P;
+    const int nsp = g.n0 + 2 * g.pd0;
+    const int s1 = (int)g.s1;
+    const uint32_t arr_bytes = (uint32_t)((int64_t)nsp * g.s0 * 8);
+    const uint32_t plane8 = (uint32_t)(g.s0 * 8);
+    const __amdgpu_buffer_rsrc_t rx = make_rsrc(x, arr_bytes);
+    const __amdgpu_buffer_rsrc_t rbv = make_rsrc(bvec, HASB ? arr_bytes : 0u);
+    const __amdgpu_buffer_rsrc_t ry = make_rsrc(y, arr_bytes);
+    auto zo_of = [&](int t) { return max(z0 - 2 * P + t, z0); };
+    // storage column of lane-column 0 (pads == P): c0 - H + P
+    const int colb = (c0 - H + P) * 8 + 16 * lane;
+
+    // ---- LDS-DMA issue (per wave per plane: x 1 or 2 rows, b 1 row) ----
+    auto dma_x = [&](int m, int slot) {
+        const int sp = m + g.pd0;
+        const uint32_t so = (sp >= 0 && sp < nsp) ? (uint32_t)sp * plane8 : 0x80000000u;
+        // x-tile row q = storage row r0 + q
+        dma16s(rx, lds + XS_OFF + (slot * XR + wv) * TC, (r0 + wv) * s1 * 8 + colb, so);
+        if (wv < XR - NW) dma16s(rx, lds + XS_OFF + (slot * XR + NW + wv) * TC, (r0 + NW + wv) * s1 * 8 + colb, so);
+    };
+    auto dma_b = [&](int zo, int slot) {
+        const uint32_t so = (uint32_t)(zo + g.pd0) * plane8;
+        dma16s(rbv, lds + BS_OFF + (slot * T1 + wv) * TC, (orow + P) * s1 * 8 + colb, so);
+        if constexpr (XIN) dma16s(rx, lds + XI_OFF + (slot * T1 + wv) * TC, (orow + P) * s1 * 8 + colb, so);
+    };
+
+    double acc[NS][2];
+#pragma unroll
+    for (int s = 0; s < NS; ++s) { acc[s][0] = 0.0; acc[s][1] = 0.0; }
+    double hist[HIST ? P : 1][2];
+#pragma unroll
+    for (int i = 0; i < (HIST ? P : 1); ++i) { hist[i][0] = 0.0; hist[i][1] = 0.0; }
+    double nrm = 0.0, dotp = 0.0;
+
+    __syncthreads();  // C2 table visible; no DMA in flight yet
+
+#pragma unroll
+    for (int i = 0; i < PFX; ++i) dma_x(i < nplanes ? z0 - P + i : -(1 << 20), i);
+    if constexpr (HASB) dma_b(zo_of(0), 0);
+
+    const bool xtra = wv < XR - NW;   // this wave issues 2 x DMAs per plane
+    for (int tb = 0; tb < nplanes; tb += NS) {
+#pragma unroll
+        for (int q = 0; q < NS; ++q) {
+            const int t = tb + q;
+            if (t < nplanes) {
+                // ---- x(t) (and b(t)) landed: own DMAs by vmcnt, everyone's by the barrier.
+                // Per iteration each wave issues, in order: b(t+1) [x_in(t+1)], x(t+PFX) (1 or
+                // 2), 1 store.  Loads return in order, but a store may be acknowledged
+                // before an older load returns, so the counts below are the LOADS issued
+                // after the one waited for (stores never count): vmcnt <= that number
+                // implies the load has landed.  Waiting for b(t) also covers x(t) (issued
+                // before it, PFX >= 2).
+                if constexpr (HASB) {
+                    if (t == 0) v5_wait_vm<0>();
+                    else if (xtra) v5_wait_vm<2>();
+                    else v5_wait_vm<1>();
+                } else {
+                    if (t < PFX) v5_wait_vm<0>();
+                    else if (xtra) v5_wait_vm<(PFX - 1) * 2>();
+                    else v5_wait_vm<(PFX - 1) * 1>();
+                }
+                v5_barrier();
+                if constexpr (HASB) dma_b(zo_of(t + 1), (t + 1) & 1);
+                dma_x(t + PFX < nplanes ? z0 - P + t + PFX : -(1 << 20), (t + PFX) % D);
+
+                // ---- axis 1: u = F1a x, v = F1b x on this wave's row, 2 columns per lane
+                const double* xs = lds + XS_OFF + (t % D) * XR * TC + 2 * lane;
+                d2 xv[W];
+#pragma unroll
+                for (int k = 0; k < W; ++k) xv[k] = *(const d2*)(xs + (wv + k) * TC);
+                double u[2], v[2];
+                if (fast1) {
+#pragma unroll
+                    for (int e = 0; e < 2; ++e) {
+                        double pr[P + 1];
+                        pr[0] = xv[P][e];
+#pragma unroll
+                        for (int k = 1; k <= P; ++k) pr[k] = xv[P - k][e] + xv[P + k][e];
+                        double su = tc.t1a[0] * pr[0], sv = tc.t1b[0] * pr[0];
+#pragma unroll
+                        for (int k = 1; k <= P; ++k) {
+                            su = fma(tc.t1a[k], pr[k], su);
+                            sv = fma(tc.t1b[k], pr[k], sv);
+                        }
+                        u[e] = su;
+                        v[e] = sv;
+                    }
+                } else {
+#pragma unroll
+                    for (int e = 0; e < 2; ++e) {
+                        double su = ra[0] * xv[0][e], sv = rb[0] * xv[0][e];
+#pragma unroll
+                        for (int k = 1; k < W; ++k) {
+                            su = fma(ra[k], xv[k][e], su);
+                            sv = fma(rb[k], xv[k][e], sv);
+                        }
+                        u[e] = su;
+                        v[e] = sv;
+                    }
+                }
+
+                // ---- axis 2: column windows by whole-lane DPP shifts (2 columns per lane)
+                double wu[NWIN], wvv[NWIN];
+                wu[P] = u[0];
+                wu[P + 1] = u[1];
+                wvv[P] = v[0];
+                wvv[P + 1] = v[1];
+#pragma unroll
+                for (int i = P - 1; i >= 0; --i) {
+                    wu[i] = v5_shr1(wu[i + 2]);
+                    wvv[i] = v5_shr1(wvv[i + 2]);
+                }
+#pragma unroll
+                for (int i = P + 2; i <= 2 * P + 1; ++i) {
+                    wu[i] = v5_shl1(wu[i - 2]);
+                    wvv[i] = v5_shl1(wvv[i - 2]);
+                }
+                double cc[2], dd[2];
+                if (fast2) {
+#pragma unroll
+                    for (int e = 0; e < 2; ++e) {
+                        double pu[P + 1], pv[P + 1];
+                        pu[0] = wu[e + P];
+                        pv[0] = wvv[e + P];
+#pragma unroll
+                        for (int k = 1; k <= P; ++k) {
+                            pu[k] = wu[e + P - k] + wu[e + P + k];
+                            pv[k] = wvv[e + P - k] + wvv[e + P + k];
+                        }
+                        double c = tc.t2a[0] * pu[0];
+                        double d = fma(tc.t2a[0], pv[0], tc.t2b[0] * pu[0]);
+#pragma unroll
+                        for (int k = 1; k <= P; ++k) {
+                            c = fma(tc.t2a[k], pu[k], c);
+                            d = fma(tc.t2a[k], pv[k], fma(tc.t2b[k], pu[k], d));
+                        }
+                        cc[e] = c;
+                        dd[e] = d;
+                    }
+                } else {
+                    double c[2] = {0.0, 0.0}, d[2] = {0.0, 0.0};
+#pragma unroll
+                    for (int k = 0; k < W; ++k) {
+                        const d2 fa = *(const d2*)(lds + C2_OFF + k * TC + 2 * lane);
+                        const d2 fb = *(const d2*)(lds + C2_OFF + (W + k) * TC + 2 * lane);
+#pragma unroll
+                        for (int e = 0; e < 2; ++e) {
+                            c[e] = fma(fa[e], wu[e + k], c[e]);
+                            d[e] = fma(fa[e], wvv[e + k], fma(fb[e], wu[e + k], d[e]));
+                        }
+                    }
+                    cc[0] = c[0]; cc[1] = c[1];
+                    dd[0] = d[0]; dd[1] = d[1];
+                }
+
+                // ---- axis 0: scatter into the rotating slots
+                const int jrow = (g.g0 + z0 - P + t + P) * W;
+#pragma unroll
+                for (int s = 0; s < W; ++s) {
+                    const int slot = (q - P + s + NS) % NS;
+                    const double ka = a0t[jrow + s];
+                    const double kb = b0t[jrow + s];
+#pragma unroll
+                    for (int e = 0; e < 2; ++e) acc[slot][e] = fma(ka, cc[e], fma(kb, dd[e], acc[slot][e]));
+                }
+                const int done = (q + P + 1) % NS;
+                double vo[2] = {acc[done][0], acc[done][1]};
+                acc[done][0] = 0.0;
+                acc[done][1] = 0.0;
+                const bool en = t >= 2 * P;
+                const int zo = zo_of(t);
+
+                // ---- epilogue of the finished plane zo
+                double xin[2] = {0.0, 0.0};
+                if constexpr (HIST) {
+                    xin[0] = hist[0][0];
+                    xin[1] = hist[0][1];
+#pragma unroll
+                    for (int i = 0; i + 1 < P; ++i) { hist[i][0] = hist[i + 1][0]; hist[i][1] = hist[i + 1][1]; }
+                    hist[P - 1][0] = xv[P][0];
+                    hist[P - 1][1] = xv[P][1];
+                }
+                bool ok[2];
+#pragma unroll
+                for (int e = 0; e < 2; ++e) ok[e] = en && row_ok && col_ok[e];
+                double outv[2];
+                if constexpr (EPI == EPI_APPLY) {
+                    outv[0] = vo[0];
+                    outv[1] = vo[1];
+                } else if constexpr (APD) {
+                    outv[0] = vo[0];
+                    outv[1] = vo[1];
+#pragma unroll
+                    for (int e = 0; e < 2; ++e) dotp = ok[e] ? fma(xin[e], outv[e], dotp) : dotp;
+                } else {
+                    const d2 bv = *(const d2*)(lds + BS_OFF + ((t & 1) * T1 + wv) * TC + 2 * lane);
+                    if constexpr (EPI == EPI_RESID) {
+                        outv[0] = bv[0] - vo[0];
+                        outv[1] = bv[1] - vo[1];
+                    } else {
+                        const d2 xi = *(const d2*)(lds + XI_OFF + ((t & 1) * T1 + wv) * TC + 2 * lane);
+                        xin[0] = xi[0];
+                        xin[1] = xi[1];
+                        double rc[2];
+                        if (fast1 && fast2 && rdiag0 != nullptr) {
+                            rc[0] = rc[1] = rdiag0[g.g0 + zo];
+                        } else {
+                            const int i0 = (g.g0 + zo + P) * W + P;
+                            const double d0a = a0t[i0], d0b = b0t[i0];
+#pragma unroll
+                            for (int e = 0; e < 2; ++e) {
+                                const double dg = fma(d0a, dX[e], d0b * dY[e]);
+                                double r = __builtin_amdgcn_rcp(dg);
+                                double ee = fma(-dg, r, 1.0);
+                                r = fma(r, ee, r);
+                                ee = fma(-dg, r, 1.0);
+                                rc[e] = fma(r, ee, r);
+                            }
+                        }
+#pragma unroll
+                        for (int e = 0; e < 2; ++e) {
+                            const double dr = omega * (bv[e] - vo[e]) * rc[e];
+                            outv[e] = xin[e] + dr;
+                            nrm = ok[e] ? fma(dr, dr, nrm) : nrm;
+                            dotp = ok[e] ? fma(outv[e], bv[e], dotp) : dotp;
+                        }
+                    }
+                }
+                // one 16-B store per lane; a lane whose second column lies past n2 (a
+                // ghost or dead pitch column) writes 0 there, which keeps ghosts zero
+                const bool any = ok[0] || ok[1];
+                const double o1 = ok[1] ? outv[1] : 0.0;
+                bstore2_s(ry, any ? (orow + P) * s1 * 8 + colb : 0x7ffffff0, (uint32_t)(zo + g.pd0) * plane8,
+                          outv[0], o1);
+            }
+        }
+    }
+    v5_wait_vm<0>();  // no LDS-DMA may outlive the workgroup
+
+    if constexpr (JAC || APD) {
+        if (partial != nullptr) {
+#pragma unroll
+            for (int off = 32; off > 0; off >>= 1) nrm += __shfl_xor(nrm, off, 64);
+            __syncthreads();
+            if (lane == 0) lds[RED_OFF + wv] = nrm;
+            __syncthreads();
+            if (tid == 0) {
+                double s = 0.0;
+                for (int w = 0; w < NW; ++w) s += lds[RED_OFF + w];
+                partial[blockIdx.x] = s;
+            }
+        }
+        if (partial2 != nullptr) {
+#pragma unroll
+            for (int off = 32; off > 0; off >>= 1) dotp += __shfl_xor(dotp, off, 64);
+            __syncthreads();
+            if (lane == 0) lds[RED_OFF + wv] = dotp;
+            __syncthreads();
+            if (tid == 0) {
+                double s = 0.0;
+                for (int w = 0; w < NW; ++w) s += lds[RED_OFF + w];
+                partial2[blockIdx.x] = s;
+            }
+        }
+    }
+}
+
+template <int P, int EPI, int D>
+static int v5_launch_t(const KronPtrs& p, const KronGeom& g, const ToepConst& tc, int H, double omega,
+                       hipStream_t st) {
+    // the hand-counted vmcnt waits assume the only VMEM ops in the loop are the
+    // DMAs and the store: a build that spills to scratch would break them
+    static int scratch = -1;
+    if (scratch < 0) {
+        hipFuncAttributes at{};
+        if (hipFuncGetAttributes(&at, reinterpret_cast<const void*>(&kron_v5_kernel<P, EPI, D>)) != hipSuccess) {
+            set_error("v5: hipFuncGetAttributes failed");
+            return 1;
+        }
+        scratch = (int)at.localSizeBytes;
+    }
+    if (scratch > 0) {
+        set_error("v5: kernel build spills to scratch (vmcnt counting invalid)");
+        return 1;
+    }
+    const int nblk = g.tiles2 * g.tiles1 * g.nchunks;
+    hipLaunchKernelGGL((kron_v5_kernel<P, EPI, D>), dim3(nblk), dim3(1024), 0, st, p.x, p.y, p.b, p.a0t, p.b0t,
+                       p.a1, p.b1, p.a2, p.b2, p.partial, p.partial2, p.rdiag0, g, tc, H, omega);
+    return 0;
+}
+
+template <int P>
+static int v5_launch_p(int epi, const KronPtrs& p, const KronGeom& g, const ToepConst& tc, int H, double omega,
+                       hipStream_t st) {
+    switch (epi) {
+        case EPI_APPLY: return v5_launch_t<P, EPI_APPLY, 4>(p, g, tc, H, omega, st);
+        case EPI_RESID: return v5_launch_t<P, EPI_RESID, 3>(p, g, tc, H, omega, st);
+        case EPI_JACOBI: return v5_launch_t<P, EPI_JACOBI, 3>(p, g, tc, H, omega, st);
+        case EPI_APPLYDOT: return v5_launch_t<P, EPI_APPLYDOT, 4>(p, g, tc, H, omega, st);
+    }
+    set_error("v5: epilogue not built (two sweeps from zero: variant 9)");
+    return 1;
+}
+
+// Tile geometry for the v5 kernel: halo lane-columns H on the left and output
+// columns TO per tile.  Line-aligned (interior column 0 of every row on a 128-B
+// line, pitch a multiple of 16): H = 8, TO = 112, so every stored row segment is
+// whole lines.  Otherwise H = P rounded up to even, TO = 128 - 2H.
+void kron_v5_tile(int pmax, bool aligned, int* H, int* TO) {
+    if (aligned && pmax <= 8) {
+        *H = 8;
+        *TO = 112;
+    } else {
+        *H = (pmax + 1) & ~1;
+        *TO = 128 - 2 * *H;
+    }
+}
+
+int kron_v5_launch(int pmax, int epi, const KronPtrs& p, const KronGeom& g, const ToepConst& tc, int H,
+                   double omega, hipStream_t st) {
+    if (H < pmax || (H & 1) || (g.tout & 1) || H + g.tout + pmax > 128) {
+        set_error("v5: bad tile geometry");
+        return 1;
+    }
+    switch (pmax) {   // p >= 4 does not fit 128 VGPRs without spilling: the host runs 7 / 9
+        case 1: return v5_launch_p<1>(epi, p, g, tc, H, omega, st);
+        case 2: return v5_launch_p<2>(epi, p, g, tc, H, omega, st);
+        case 3: return v5_launch_p<3>(epi, p, g, tc, H, omega, st);
+    }
+    set_error("v5: pmax must be in 1..3");
+    return 1;
+}
+
+}  // namespace poms

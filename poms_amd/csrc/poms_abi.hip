@@ -19,6 +19,9 @@ int kron_v3_launch(int variant, int pmax, bool is3d, int form, int epi, const Kr
                    const KronGeom& g, const ToepConst& tc, double omega, hipStream_t st);
 int kron_v4_launch(int pmax, bool is3d, int form, int epi, const KronPtrs& p, const KronGeom& g,
                    const ToepConst& tc, double omega, hipStream_t st, int diag_mode);
+int kron_v5_launch(int pmax, int epi, const KronPtrs& p, const KronGeom& g, const ToepConst& tc, int H,
+                   double omega, hipStream_t st);
+void kron_v5_tile(int pmax, bool aligned, int* H, int* TO);
 int kron_v2_stamps(int variant, int epi, const KronPtrs& p, const KronGeom& g, const ToepConst& tc,
                    double omega, unsigned long long* dbg, hipStream_t st);
 int kron_tile_rows();
@@ -278,7 +281,7 @@ int poms_op_destroy(poms_op* o) {
 }
 
 int poms_op_set_variant(poms_op* op, int variant) {
-    if (!op || variant < 0 || (variant > 9 && (variant < 90 || variant > 100))) { set_error("poms_op_set_variant: bad argument"); return 1; }
+    if (!op || variant < 0 || (variant > 10 && (variant < 90 || variant > 100))) { set_error("poms_op_set_variant: bad argument"); return 1; }
     if (variant > 0 && !op->v2_ok) { set_error("poms_op_set_variant: variant needs pads == pmax"); return 1; }
     if (variant == 5 && op->pmax > 3) variant = 4;  // 32-row tile does not fit LDS at p >= 4
     op->variant = variant;
@@ -309,14 +312,13 @@ int poms_op_set_chunk(poms_op* op, int chunk) {
 // (chunk + 2p), the partial last round weighted 5x its fill (fit to the chunk sweeps
 // in profiles/r01/chunks/*.log; picks 103 at 515^3 p=3, 43 at 258^3 p=2).  For
 // p >= 4 the kernels are VALU-bound and want >= 3 workgroups per CU instead.
-static int auto_chunk(int nz, int tiles, int p) {
+static int auto_chunk(int nz, int tiles, int p, double slots = 512.0) {
     if (nz <= 0) return 1;
     tiles = std::max(tiles, 1);
-    if (p >= 4) {
+    if (p >= 4 && slots > 256.0) {
         const int nc = std::max(1, std::min(nz / 8, (768 + tiles - 1) / tiles));
         return (nz + nc - 1) / nc;
     }
-    const double slots = 512.0;
     double best = 1e300;
     int best_chunk = nz;
     for (int nc = 1; nc <= std::max(1, nz / 8); ++nc) {
@@ -330,7 +332,21 @@ static int auto_chunk(int nz, int tiles, int p) {
     return best_chunk;
 }
 
-static int op_geom(poms_op* o, int64_t zb, int64_t ze, KronGeom& g) {
+// v5 (variant 10) runs 3D FORM_SUM operators, p <= 3, pads == pmax, arrays < 2 GiB
+static bool v5_ok(const poms_op* o) {
+    const int64_t bytes = (int64_t)(o->L.n[0] + 2 * o->L.pads[0]) * row_geom(&o->L).s0 * 8;
+    return o->ndim == 3 && o->form == FORM_SUM && o->v2_ok && o->pmax <= 3 && bytes < 0x7fffffffLL;
+}
+
+// v5 tiles are line-aligned when the row pitch is a multiple of 16 doubles and
+// interior column 0 of x starts a 128-B line
+static bool v5_aligned(const poms_op* o, const double* x) {
+    const int64_t pitch = row_geom(&o->L).s1;
+    return pitch % 16 == 0 && (reinterpret_cast<uintptr_t>(x + o->L.pads[2]) & 127) == 0;
+}
+
+static int op_geom(poms_op* o, int64_t zb, int64_t ze, KronGeom& g, int v = -1, int v5_to = 0) {
+    if (v < 0) v = o->variant;
     const bool is3d = o->ndim == 3;
     const RowGeom r = row_geom(&o->L);
     g.s0 = r.s0;
@@ -339,10 +355,10 @@ static int op_geom(poms_op* o, int64_t zb, int64_t ze, KronGeom& g) {
     g.pd0 = r.pd0; g.pd1 = r.pd1; g.pd2 = r.pd2;
     g.g0 = (int)o->g0;
     g.tiles2 = (int)((o->L.n[2] + kron_tile_cols() - 1) / kron_tile_cols());
-    const int trows = (o->variant == 3 || o->variant == 5) ? 32 : kron_tile_rows();
+    const int trows = (v == 3 || v == 5 || v == 10) ? (v == 10 ? 16 : 32) : kron_tile_rows();
     g.tiles1 = (int)((o->L.n[1] + trows - 1) / trows);
-    g.tout = o->tout > 0 ? o->tout : 64 - 2 * o->pmax;
-    if (o->variant >= 4) g.tiles2 = (int)((o->L.n[2] + g.tout - 1) / g.tout);
+    g.tout = v == 10 ? v5_to : (o->tout > 0 ? o->tout : 64 - 2 * o->pmax);
+    if (v >= 4) g.tiles2 = (int)((o->L.n[2] + g.tout - 1) / g.tout);
     if (!is3d) {
         g.z_begin = 0; g.z_end = 1; g.chunk = 1; g.nchunks = 1;
         return 0;
@@ -352,7 +368,7 @@ static int op_geom(poms_op* o, int64_t zb, int64_t ze, KronGeom& g) {
     g.z_end = (int)ze;
     const int nz = (int)(ze - zb);
     int chunk = o->chunk;
-    if (chunk <= 0) chunk = auto_chunk(nz, g.tiles2 * g.tiles1, o->pmax);
+    if (chunk <= 0) chunk = auto_chunk(nz, g.tiles2 * g.tiles1, o->pmax, v == 10 ? 256.0 : 512.0);
     chunk = std::max(1, std::min(chunk, std::max(nz, 1)));
     g.chunk = chunk;
     g.nchunks = nz == 0 ? 0 : (nz + chunk - 1) / chunk;
@@ -360,37 +376,31 @@ static int op_geom(poms_op* o, int64_t zb, int64_t ze, KronGeom& g) {
 }
 
 // variants whose Jacobi epilogue also accumulates x_out . b (v3 and v4 kernels)
-static bool fused_dot_ok(const poms_op* o) { return o->variant >= 4 && o->variant <= 9; }
+static bool fused_dot_ok(const poms_op* o) { return o->variant >= 4 && o->variant <= 10; }
 
 static int op_run(poms_op* o, int epi, double omega, const double* x, double* y, const double* b,
                   int64_t zb, int64_t ze, int want_norm, void* stream, int want_dot = 0) {
     if (!o || !x || !y) { set_error("null operator or vector"); return 1; }
     if (epi != EPI_APPLY && !b) { set_error("null right-hand side"); return 1; }
     if (epi == EPI_APPLYDOT && !(o->variant == 4 || o->variant == 5 || o->variant == 6 || o->variant == 8 ||
-                                 o->variant == 9)) {
-        set_error("apply + x.y: kernel variants 4, 5, 6, 8, 9 only");
+                                 o->variant == 9 || o->variant == 10)) {
+        set_error("apply + x.y: kernel variants 4, 5, 6, 8, 9, 10 only");
         return 1;
     }
     if (want_dot && ((epi != EPI_JACOBI && epi != EPI_JACOBI0 && epi != EPI_APPLYDOT) || !fused_dot_ok(o))) {
         set_error("fused x_out.b needs a Jacobi sweep on kernel variants 4-9");
         return 1;
     }
-    if (epi == EPI_JACOBI0 && !(o->variant == 8 || o->variant == 9)) {
-        set_error("two sweeps from zero: kernel variant 8 or 9 only");
+    if (epi == EPI_JACOBI0 && !(o->variant == 8 || o->variant == 9 || o->variant == 10)) {
+        set_error("two sweeps from zero: kernel variant 8, 9 or 10 only");
         return 1;
     }
-    KronGeom g;
-    if (op_geom(o, zb, ze, g)) return 1;
-    const int64_t nblk = (int64_t)g.tiles2 * g.tiles1 * g.nchunks;
-    if (nblk == 0) { o->last_partials = 0; return 0; }
-    if ((want_norm || want_dot) && 2 * nblk > kScratch) { set_error("too many blocks for the partial-sum scratch"); return 1; }
-    KronPtrs p{x, y, b, o->a0t, o->b0t, o->a1, o->b1, o->a2, o->b2,
-               want_norm ? o->ctx->scratch : nullptr, want_dot ? o->ctx->scratch + nblk : nullptr, o->rdiag0};
     // variant 8 (default when pads == pmax): the fastest measured kernel per
     // epilogue (profiles/r01/chunks/*.log) -- in 3D v4 (7) for apply at p >= 3 and
     // for every plain epilogue at p >= 4 (VALU-bound there), v3 with whole-array
     // buffer resources (9; falls back to 4 for arrays >= 2 GiB) otherwise; in 2D
     // v4 for apply / residual at p <= 3.  Fused dots and two-sweeps-from-zero: 9.
+    // Variant 10 (v5) runs apply / residual / Jacobi / apply+dot; 9 otherwise.
     int v = o->variant;
     if (v == 8) {
         const bool plain = epi == EPI_APPLY || epi == EPI_RESID || epi == EPI_JACOBI;
@@ -399,7 +409,19 @@ static int op_run(poms_op* o, int epi, double omega, const double* x, double* y,
         else
             v = ((epi == EPI_APPLY || epi == EPI_RESID) && o->pmax <= 3) ? 7 : 9;
     }
-    const int rc = v == 0
+    if (v == 10 && (!v5_ok(o) || epi == EPI_JACOBI0)) v = 9;
+    int v5_h = 0, v5_to = 0;
+    if (v == 10) kron_v5_tile(o->pmax, v5_aligned(o, x), &v5_h, &v5_to);
+    KronGeom g;
+    if (op_geom(o, zb, ze, g, v, v5_to)) return 1;
+    const int64_t nblk = (int64_t)g.tiles2 * g.tiles1 * g.nchunks;
+    if (nblk == 0) { o->last_partials = 0; return 0; }
+    if ((want_norm || want_dot) && 2 * nblk > kScratch) { set_error("too many blocks for the partial-sum scratch"); return 1; }
+    KronPtrs p{x, y, b, o->a0t, o->b0t, o->a1, o->b1, o->a2, o->b2,
+               want_norm ? o->ctx->scratch : nullptr, want_dot ? o->ctx->scratch + nblk : nullptr, o->rdiag0};
+    const int rc = v == 10
+        ? kron_v5_launch(o->pmax, epi, p, g, o->tc, v5_h, omega, as_stream(stream))
+        : v == 0
         ? kron_launch(o->pmax, o->ndim == 3, o->form, epi, p, g, omega, as_stream(stream))
         : (v == 7 || (v >= 92 && v <= 100))
         ? kron_v4_launch(o->pmax, o->ndim == 3, o->form, epi, p, g, o->tc, omega, as_stream(stream),
@@ -442,7 +464,7 @@ int poms_op_apply_dot(poms_op* op, const double* x, double* y, int64_t zb, int64
 int poms_op_apply_dot_supported(poms_op* op, int* yes) {
     if (!op || !yes) { set_error("poms_op_apply_dot_supported: null argument"); return 1; }
     const int v = op->variant;
-    *yes = (v == 4 || v == 5 || v == 6 || v == 8 || v == 9) ? 1 : 0;
+    *yes = (v == 4 || v == 5 || v == 6 || v == 8 || v == 9 || v == 10) ? 1 : 0;
     return 0;
 }
 
@@ -457,7 +479,7 @@ int poms_op_jacobi_from_zero(poms_op* op, double omega, const double* b, double*
 int poms_op_from_zero_supported(poms_op* op, int* yes) {
     if (!op || !yes) { set_error("poms_op_from_zero_supported: null argument"); return 1; }
     const int64_t bytes = (int64_t)(op->L.n[0] + 2 * op->L.pads[0]) * row_geom(&op->L).s0 * 8;
-    *yes = (op->ndim == 3 && (op->variant == 8 || op->variant == 9) && bytes < 0x7fffffffLL) ? 1 : 0;
+    *yes = (op->ndim == 3 && (op->variant == 8 || op->variant == 9 || op->variant == 10) && bytes < 0x7fffffffLL) ? 1 : 0;
     return 0;
 }
 
