@@ -31,6 +31,7 @@ sys.path.insert(0, str(ROOT))
 
 METRIC = "V-cycle DOF/s + Kron-SpMV GB/s vs HBM roofline, 3D Poisson p=3"
 HBM_PEAK_GBPS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md)
+KERNEL_NAMES = {10: "kron_v5_kernel", 9: "kron_v3_kernel(flat)", 7: "kron_v4_kernel", 4: "kron_v3_kernel"}
 
 
 def parse():
@@ -109,6 +110,7 @@ def main():
                 calls[call] = calls.get(call, 0.0) + e0.elapsed_time(e1) * 1e-3
         return sum(calls.values()) / max(1, len(calls)), len(calls)
 
+    jac_v, app_v = A.kernel_variant("jacobi"), A.kernel_variant("apply")
     sweep_s, n_sweeps = per_call(timer, "jacobi")
     bytes_sweep = 24.0 * local_dof
     achieved = bytes_sweep / sweep_s / 1e9 if sweep_s > 0 else 0.0
@@ -175,14 +177,14 @@ def main():
                 "parallelism": f"slab{world}",
             },
             "roofline": {
-                "kernel": (f"kron_v3_kernel<P={args.p},3D,SUM,JACOBI> (operator variant {A.variant} = auto: v3 with "
-                           f"whole-array buffer resources; Kron apply + damped-Jacobi update)"),
+                "kernel": f"{KERNEL_NAMES.get(jac_v, f'variant {jac_v}')}<P={args.p},3D,SUM,JACOBI> (Kron apply + damped-Jacobi update)",
                 "bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBPS, "unit": "GB/s",
                 "frac": achieved / HBM_PEAK_GBPS, "traffic": traffic,
                 "algorithmic_bytes_per_launch": bytes_sweep, "avg_launch_us": sweep_s * 1e6,
                 "launches_timed": n_sweeps,
             },
-            "kron_spmv": {"achieved": kron_gbps, "unit": "GB/s", "frac": kron_gbps / HBM_PEAK_GBPS,
+            "kron_spmv": {"kernel": f"{KERNEL_NAMES.get(app_v, f'variant {app_v}')}<P={args.p},3D,SUM,APPLY>",
+                          "achieved": kron_gbps, "unit": "GB/s", "frac": kron_gbps / HBM_PEAK_GBPS,
                           "avg_launch_us": kron_s * 1e6, "bytes_per_dof": 16},
             "cpu_baseline": cpu,
             "solver": {"info_pre": ipre, "info_pos": ipos},

@@ -105,6 +105,10 @@ int poms_op_set_tile_cols(poms_op* op, int cols);
  * Variants 1-10 need storage pads == pmax on every used axis.                 */
 int poms_op_set_variant(poms_op* op, int variant);
 int poms_op_get_variant(poms_op* op, int* variant);
+/* The variant one launch of `epilogue` runs after automatic selection and
+ * fall-backs: 0 apply, 1 residual, 2 Jacobi sweep, 3 two sweeps from zero,
+ * 4 apply + x.y.                                                              */
+int poms_op_kernel_variant(poms_op* op, int epilogue, int* variant);
 
 /* y = A x on output planes [z_begin, z_end) (local axis-0 indices; 2D/1D: 0,1).
  * x must have current ghosts on the planes the range touches.

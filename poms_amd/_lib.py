@@ -59,6 +59,7 @@ _SIGS = {
     "poms_op_set_tile_cols": [_vp, _i],
     "poms_op_set_variant": [_vp, _i],
     "poms_op_get_variant": [_vp, C.POINTER(_i)],
+    "poms_op_kernel_variant": [_vp, _i, C.POINTER(_i)],
     "poms_op_apply": [_vp, _vp, _vp, _i64, _i64, _vp],
     "poms_op_residual": [_vp, _vp, _vp, _vp, _i64, _i64, _vp],
     "poms_op_apply_dot": [_vp, _vp, _vp, _i64, _i64, _vp],

@@ -50,6 +50,7 @@ struct ToepConst {
     double t0a[6], t0b[6];   // axis 0 (A0, M0), global rows
     double t2a[6], t2b[6];   // axis 2 (M2, K2)
     int lo1, hi1, lo0, hi0, lo2, hi2;
+    double rdi;              // 1/diag(A) inside the Toeplitz interior of every axis (3D; 0 if empty)
 };
 
 // Device pointers of one fused Kronecker launch.

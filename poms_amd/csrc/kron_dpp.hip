@@ -164,9 +164,10 @@ kron_v3_kernel(const double* __restrict__ x, double* __restrict__ y,
         const int sp = IS3D ? jj + g.pd0 : 0;
         const bool ok = (sp >= 0) && (sp < nsp);
         if constexpr (FLAT) {
-            const uint32_t so = ok ? (uint32_t)sp * plane8 : 0x80000000u;
+            // out-of-range planes by voffset (soffset is outside the range check)
+            const uint32_t so = ok ? (uint32_t)sp * plane8 : 0u;
 #pragma unroll
-            for (int j = 0; j < NRW; ++j) xr[xb][j] = bload_s(rx_all, xoff[j], so);
+            for (int j = 0; j < NRW; ++j) xr[xb][j] = bload_s(rx_all, ok ? xoff[j] : 0x7ffffff0, so);
             return;
         }
         const __amdgpu_buffer_rsrc_t rs =
@@ -552,7 +553,7 @@ int kron_v3_launch(int variant, int pmax, bool is3d, int form, int epi, const Kr
     }
     if (variant == 9) {   // v3 with whole-array buffer resources (arrays < 2 GiB)
         const int64_t bytes = (int64_t)(g.n0 + 2 * g.pd0) * g.s0 * 8;
-        if (bytes < 0x7fffffffLL) {
+        if (bytes < 0x7ffffff0LL) {
             switch (pmax) {
                 case 1: return v3_launch_p<1, 2, 8, 1, true>(is3d, form, epi, p, g, tc, omega, st);
                 case 2: return v3_launch_p<2, 2, 8, 1, true>(is3d, form, epi, p, g, tc, omega, st);

@@ -23,10 +23,13 @@
 //     outside); axis 2 with the column neighbours shifted in by DPP
 //     (c = F2a u, d = F2a v + F2b u); axis 0 scattered into 2P+1 rotating
 //     accumulators;
-//   * epilogues: APPLY, RESID, JACOBI (x_in of the output plane DMA'd next to
-//     b; 1/diag from the host table inside the Toeplitz interior, else from the
-//     plane-invariant pieces of the diagonal), APPLYDOT (x . Ax, with x at the
-//     output point from a P-deep register history of the lane's centre tap).
+//   * epilogues: APPLY, RESID, JACOBI (1/diag from the host table inside the
+//     Toeplitz interior, else from the plane-invariant pieces of the diagonal),
+//     APPLYDOT (x . Ax).  x at the output point (Jacobi's x_in, APPLYDOT's x)
+//     comes from a P-deep register history of the lane's centre tap -- no
+//     re-read (the x_in DMA next to b, kept as a tuning build, costs 8 B/DOF);
+//   * y stores and b DMAs are non-temporal (streamed once); x DMAs are not
+//     (the halo rows are re-read by the neighbouring tiles).
 // Preconditions (host): 3D, FORM_SUM, P <= 3, storage pads == P, array < 2 GiB.
 #include "common.hpp"
 
@@ -34,8 +37,16 @@ namespace poms {
 
 typedef __attribute__((address_space(3))) void lds5_void_t;
 
+template <int AUX = 0>   // cache policy (gfx950: bit 1 = nt, streaming)
 __device__ __forceinline__ void dma16s(__amdgpu_buffer_rsrc_t r, double* lds_dst, int voff, unsigned soff) {
-    __builtin_amdgcn_raw_ptr_buffer_load_lds(r, (lds5_void_t*)lds_dst, 16, voff, (int)soff, 0, 0);
+    __builtin_amdgcn_raw_ptr_buffer_load_lds(r, (lds5_void_t*)lds_dst, 16, voff, (int)soff, 0, AUX);
+}
+template <int AUX = 0>
+__device__ __forceinline__ void bstore2_sp(__amdgpu_buffer_rsrc_t r, int voff, unsigned soff, double d0, double d1) {
+    u32x4 v;
+    const u32x2 a = __builtin_bit_cast(u32x2, d0), b = __builtin_bit_cast(u32x2, d1);
+    v.x = a.x; v.y = a.y; v.z = b.x; v.w = b.y;
+    __builtin_amdgcn_raw_buffer_store_b128(v, r, voff, (int)soff, AUX);
 }
 
 __device__ __forceinline__ double v5_shr1(double v) {  // lane l <- lane l-1 (lane 0 <- 0)
@@ -63,7 +74,13 @@ __device__ __forceinline__ void v5_barrier() {
     __asm__ volatile("" ::: "memory");
 }
 
-template <int P, int EPI, int D>
+// MODE (diagnostic builds, apply only): 1 = memory only (the centre tap is stored,
+// no arithmetic), 2 = arithmetic only (no DMA; the LDS ring is never filled).
+// CP: cache policy bits -- 1: x DMAs nt, 2: b / x_in DMAs nt, 4: y stores nt.
+// XH: Jacobi x_in from the register history instead of a DMA next to b.
+// ST16: every lane's store address is 16-B aligned (host-checked; always on the
+// aligned layout): one 16-B store per lane, else two 8-B stores.
+template <int P, int EPI, int D, int MODE = 0, int CP = 0, bool XH = false, bool ST16 = true>
 __global__ void __launch_bounds__(1024, 1)
 kron_v5_kernel(const double* __restrict__ x, double* __restrict__ y, const double* __restrict__ bvec,
                const double* __restrict__ a0t, const double* __restrict__ b0t,
@@ -82,8 +99,9 @@ kron_v5_kernel(const double* __restrict__ x, double* __restrict__ y, const doubl
     constexpr bool HASB = (EPI == EPI_RESID) || (EPI == EPI_JACOBI);
     constexpr bool JAC = (EPI == EPI_JACOBI);
     constexpr bool APD = (EPI == EPI_APPLYDOT);
-    constexpr bool HIST = APD;          // x at the output point from a register history
-    constexpr bool XIN = JAC;           // ... or DMA'd next to b (saves VGPRs in the Jacobi sweep)
+    constexpr bool HIST = APD || (JAC && XH);   // x at the output point from a register history
+    constexpr bool XIN = JAC && !XH;            // ... or DMA'd next to b (fewer VGPRs, 8 B/DOF more reads)
+    constexpr int XAUX = (CP & 1) ? 2 : 0, BAUX = (CP & 2) ? 2 : 0, YAUX = (CP & 4) ? 2 : 0;
     constexpr int NWIN = 2 * P + 2;     // columns 2j-P .. 2j+1+P of a lane's pair
     static_assert(D >= 3 || !HASB, "the b ring's wait count assumes x(t) was issued before b(t)");
     typedef double d2 __attribute__((ext_vector_type(2)));
@@ -168,16 +186,21 @@ kron_v5_kernel(const double* __restrict__ x, double* __restrict__ y, const doubl
 
     // ---- LDS-DMA issue (per wave per plane: x 1 or 2 rows, b 1 row) ----
     auto dma_x = [&](int m, int slot) {
+        if constexpr (MODE == 2) return;
         const int sp = m + g.pd0;
-        const uint32_t so = (sp >= 0 && sp < nsp) ? (uint32_t)sp * plane8 : 0x80000000u;
+        // planes outside the array (the dummies past the march) are out of range by
+        // voffset: the soffset field is not covered by the buffer range check
+        const bool ok = sp >= 0 && sp < nsp;
+        const uint32_t so = ok ? (uint32_t)sp * plane8 : 0u;
         // x-tile row q = storage row r0 + q
-        dma16s(rx, lds + XS_OFF + (slot * XR + wv) * TC, (r0 + wv) * s1 * 8 + colb, so);
-        if (wv < XR - NW) dma16s(rx, lds + XS_OFF + (slot * XR + NW + wv) * TC, (r0 + NW + wv) * s1 * 8 + colb, so);
+        dma16s<XAUX>(rx, lds + XS_OFF + (slot * XR + wv) * TC, ok ? (r0 + wv) * s1 * 8 + colb : 0x7ffffff0, so);
+        if (wv < XR - NW)
+            dma16s<XAUX>(rx, lds + XS_OFF + (slot * XR + NW + wv) * TC, ok ? (r0 + NW + wv) * s1 * 8 + colb : 0x7ffffff0, so);
     };
     auto dma_b = [&](int zo, int slot) {
         const uint32_t so = (uint32_t)(zo + g.pd0) * plane8;
-        dma16s(rbv, lds + BS_OFF + (slot * T1 + wv) * TC, (orow + P) * s1 * 8 + colb, so);
-        if constexpr (XIN) dma16s(rx, lds + XI_OFF + (slot * T1 + wv) * TC, (orow + P) * s1 * 8 + colb, so);
+        dma16s<BAUX>(rbv, lds + BS_OFF + (slot * T1 + wv) * TC, (orow + P) * s1 * 8 + colb, so);
+        if constexpr (XIN) dma16s<BAUX>(rx, lds + XI_OFF + (slot * T1 + wv) * TC, (orow + P) * s1 * 8 + colb, so);
     };
 
     double acc[NS][2];
@@ -225,6 +248,12 @@ kron_v5_kernel(const double* __restrict__ x, double* __restrict__ y, const doubl
                 d2 xv[W];
 #pragma unroll
                 for (int k = 0; k < W; ++k) xv[k] = *(const d2*)(xs + (wv + k) * TC);
+                if constexpr (MODE == 1) {
+                    const bool ok0 = t >= 2 * P && row_ok && col_ok[0];
+                    bstore2_s(ry, ok0 ? (orow + P) * s1 * 8 + colb + (zo_of(t) + g.pd0) * (int)plane8 : 0x7ffffff0,
+                              0u, xv[P][0] + xv[0][0], xv[P][1] + xv[W - 1][1]);
+                    continue;
+                }
                 double u[2], v[2];
                 if (fast1) {
 #pragma unroll
@@ -310,7 +339,9 @@ kron_v5_kernel(const double* __restrict__ x, double* __restrict__ y, const doubl
                     dd[0] = d[0]; dd[1] = d[1];
                 }
 
-                // ---- axis 0: scatter into the rotating slots
+                // ---- axis 0: scatter into the rotating slots (column gm of the factors;
+                // scalar loads -- taking the Toeplitz constants from the kernel arguments
+                // instead ran slower: they no longer fit the SGPRs and are re-loaded)
                 const int jrow = (g.g0 + z0 - P + t + P) * W;
 #pragma unroll
                 for (int s = 0; s < W; ++s) {
@@ -355,9 +386,11 @@ kron_v5_kernel(const double* __restrict__ x, double* __restrict__ y, const doubl
                         outv[0] = bv[0] - vo[0];
                         outv[1] = bv[1] - vo[1];
                     } else {
-                        const d2 xi = *(const d2*)(lds + XI_OFF + ((t & 1) * T1 + wv) * TC + 2 * lane);
-                        xin[0] = xi[0];
-                        xin[1] = xi[1];
+                        if constexpr (XIN) {
+                            const d2 xi = *(const d2*)(lds + XI_OFF + ((t & 1) * T1 + wv) * TC + 2 * lane);
+                            xin[0] = xi[0];
+                            xin[1] = xi[1];
+                        }
                         double rc[2];
                         if (fast1 && fast2 && rdiag0 != nullptr) {
                             rc[0] = rc[1] = rdiag0[g.g0 + zo];
@@ -383,12 +416,25 @@ kron_v5_kernel(const double* __restrict__ x, double* __restrict__ y, const doubl
                         }
                     }
                 }
-                // one 16-B store per lane; a lane whose second column lies past n2 (a
-                // ghost or dead pitch column) writes 0 there, which keeps ghosts zero
-                const bool any = ok[0] || ok[1];
+                // one 16-B store per lane when 16-B aligned (ST16: the aligned layout); a
+                // lane whose second column lies past n2 (a ghost or dead pitch column)
+                // writes 0 there, which keeps ghosts zero.  Otherwise two 8-B stores.
+                // The plane offset goes into voffset with soffset = 0: gfx950 needs a wait
+                // state before a VALU overwrites the data VGPRs of a >8-B store, and the
+                // compiler only inserts it when soffset is not a register (with an SGPR
+                // soffset the next plane's accumulator reset raced the store and zeroed
+                // lanes 12-15 of each row: tools/diag_v5_fullsize.py).
+                const bool any = (ok[0] || ok[1]) && (MODE != 2 || outv[0] == 12345.678);
                 const double o1 = ok[1] ? outv[1] : 0.0;
-                bstore2_s(ry, any ? (orow + P) * s1 * 8 + colb : 0x7ffffff0, (uint32_t)(zo + g.pd0) * plane8,
-                          outv[0], o1);
+                const int voy = (orow + P) * s1 * 8 + colb + (zo + g.pd0) * (int)plane8;
+                if constexpr (ST16) {
+                    bstore2_sp<YAUX>(ry, any ? voy : 0x7ffffff0, 0u, outv[0], o1);
+                } else {
+                    __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(u32x2, outv[0]), ry,
+                                                          ok[0] ? voy : 0x7ffffff0, 0, YAUX);
+                    __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(u32x2, o1), ry,
+                                                          any ? voy + 8 : 0x7ffffff0, 0, YAUX);
+                }
             }
         }
     }
@@ -422,15 +468,15 @@ kron_v5_kernel(const double* __restrict__ x, double* __restrict__ y, const doubl
     }
 }
 
-template <int P, int EPI, int D>
-static int v5_launch_t(const KronPtrs& p, const KronGeom& g, const ToepConst& tc, int H, double omega,
-                       hipStream_t st) {
+template <int P, int EPI, int D, int MODE = 0, int CP = 0, bool XH = false, bool ST16 = true>
+static int v5_launch_t1(const KronPtrs& p, const KronGeom& g, const ToepConst& tc, int H, double omega,
+                        hipStream_t st) {
     // the hand-counted vmcnt waits assume the only VMEM ops in the loop are the
     // DMAs and the store: a build that spills to scratch would break them
     static int scratch = -1;
     if (scratch < 0) {
         hipFuncAttributes at{};
-        if (hipFuncGetAttributes(&at, reinterpret_cast<const void*>(&kron_v5_kernel<P, EPI, D>)) != hipSuccess) {
+        if (hipFuncGetAttributes(&at, reinterpret_cast<const void*>(&kron_v5_kernel<P, EPI, D, MODE, CP, XH, ST16>)) != hipSuccess) {
             set_error("v5: hipFuncGetAttributes failed");
             return 1;
         }
@@ -441,19 +487,36 @@ static int v5_launch_t(const KronPtrs& p, const KronGeom& g, const ToepConst& tc
         return 1;
     }
     const int nblk = g.tiles2 * g.tiles1 * g.nchunks;
-    hipLaunchKernelGGL((kron_v5_kernel<P, EPI, D>), dim3(nblk), dim3(1024), 0, st, p.x, p.y, p.b, p.a0t, p.b0t,
+    hipLaunchKernelGGL((kron_v5_kernel<P, EPI, D, MODE, CP, XH, ST16>), dim3(nblk), dim3(1024), 0, st, p.x, p.y, p.b, p.a0t, p.b0t,
                        p.a1, p.b1, p.a2, p.b2, p.partial, p.partial2, p.rdiag0, g, tc, H, omega);
     return 0;
+}
+
+// 16-B stores only where every lane's store address is 16-B aligned
+template <int P, int EPI, int D, int MODE = 0, int CP = 0, bool XH = false>
+static int v5_launch_t(const KronPtrs& p, const KronGeom& g, const ToepConst& tc, int H, double omega,
+                       hipStream_t st) {
+    const bool st16 = ((reinterpret_cast<uintptr_t>(p.y) + 8 * (int64_t)(g.pd2 - H)) & 15) == 0 &&
+                      g.s1 % 2 == 0 && g.s0 % 2 == 0;
+    // the Jacobi x_in history does not fit the VGPRs beside the split stores: the
+    // unaligned build DMAs x_in next to b instead
+    constexpr bool XHU = (EPI == EPI_JACOBI) ? false : XH;
+    return st16 ? v5_launch_t1<P, EPI, D, MODE, CP, XH, true>(p, g, tc, H, omega, st)
+                : v5_launch_t1<P, EPI, D, MODE, CP, XHU, false>(p, g, tc, H, omega, st);
 }
 
 template <int P>
 static int v5_launch_p(int epi, const KronPtrs& p, const KronGeom& g, const ToepConst& tc, int H, double omega,
                        hipStream_t st) {
     switch (epi) {
-        case EPI_APPLY: return v5_launch_t<P, EPI_APPLY, 4>(p, g, tc, H, omega, st);
-        case EPI_RESID: return v5_launch_t<P, EPI_RESID, 3>(p, g, tc, H, omega, st);
-        case EPI_JACOBI: return v5_launch_t<P, EPI_JACOBI, 3>(p, g, tc, H, omega, st);
-        case EPI_APPLYDOT: return v5_launch_t<P, EPI_APPLYDOT, 4>(p, g, tc, H, omega, st);
+        // non-temporal y stores and b DMAs; Jacobi x_in from the register history
+        // (tools/kernel_bench.py, variants 103-106 at 515^3: apply 555 -> 534 us,
+        // residual 713 -> 672, Jacobi 886 -> 777; nt x DMAs cost 15 %: the halo rows
+        // are re-read by the neighbouring tiles)
+        case EPI_APPLY: return v5_launch_t<P, EPI_APPLY, 4, 0, 6>(p, g, tc, H, omega, st);
+        case EPI_RESID: return v5_launch_t<P, EPI_RESID, 3, 0, 6>(p, g, tc, H, omega, st);
+        case EPI_JACOBI: return v5_launch_t<P, EPI_JACOBI, 3, 0, 6, true>(p, g, tc, H, omega, st);
+        case EPI_APPLYDOT: return v5_launch_t<P, EPI_APPLYDOT, 4, 0, 6>(p, g, tc, H, omega, st);
     }
     set_error("v5: epilogue not built (two sweeps from zero: variant 9)");
     return 1;
@@ -474,9 +537,36 @@ void kron_v5_tile(int pmax, bool aligned, int* H, int* TO) {
 }
 
 int kron_v5_launch(int pmax, int epi, const KronPtrs& p, const KronGeom& g, const ToepConst& tc, int H,
-                   double omega, hipStream_t st) {
+                   double omega, hipStream_t st, int diag_mode) {
     if (H < pmax || (H & 1) || (g.tout & 1) || H + g.tout + pmax > 128) {
         set_error("v5: bad tile geometry");
+        return 1;
+    }
+    if (diag_mode) {   // DIAGNOSTIC / tuning builds (p = 3)
+        if (pmax != 3) { set_error("v5 diag mode: p = 3 only"); return 1; }
+        if (diag_mode <= 2) {   // 1 = memory only, 2 = arithmetic only (apply)
+            if (epi != EPI_APPLY) { set_error("v5 diag mode 1/2: apply only"); return 1; }
+            return diag_mode == 1 ? v5_launch_t<3, EPI_APPLY, 4, 1>(p, g, tc, H, omega, st)
+                                  : v5_launch_t<3, EPI_APPLY, 4, 2>(p, g, tc, H, omega, st);
+        }
+#define V5CP(CP, XH)                                                                               \
+        switch (epi) {                                                                             \
+            case EPI_APPLY: return v5_launch_t<3, EPI_APPLY, 4, 0, CP, XH>(p, g, tc, H, omega, st);   \
+            case EPI_RESID: return v5_launch_t<3, EPI_RESID, 3, 0, CP, XH>(p, g, tc, H, omega, st);   \
+            case EPI_JACOBI: return v5_launch_t<3, EPI_JACOBI, 3, 0, CP, XH>(p, g, tc, H, omega, st); \
+        }                                                                                          \
+        break;
+        switch (diag_mode) {   // 3: nt y stores; 4: + nt b / x_in; 5: + nt x; 6: 3 + Jacobi x_in history;
+                               // 7: default policy everywhere; 8: nt b only
+            case 3: V5CP(4, false)
+            case 4: V5CP(6, false)
+            case 5: V5CP(7, false)
+            case 6: V5CP(4, true)
+            case 7: V5CP(0, false)
+            case 8: V5CP(2, false)
+        }
+#undef V5CP
+        set_error("v5 diag mode: bad mode / epilogue");
         return 1;
     }
     switch (pmax) {   // p >= 4 does not fit 128 VGPRs without spilling: the host runs 7 / 9

@@ -20,7 +20,7 @@ int kron_v3_launch(int variant, int pmax, bool is3d, int form, int epi, const Kr
 int kron_v4_launch(int pmax, bool is3d, int form, int epi, const KronPtrs& p, const KronGeom& g,
                    const ToepConst& tc, double omega, hipStream_t st, int diag_mode);
 int kron_v5_launch(int pmax, int epi, const KronPtrs& p, const KronGeom& g, const ToepConst& tc, int H,
-                   double omega, hipStream_t st);
+                   double omega, hipStream_t st, int diag_mode);
 void kron_v5_tile(int pmax, bool aligned, int* H, int* TO);
 int kron_v2_stamps(int variant, int epi, const KronPtrs& p, const KronGeom& g, const ToepConst& tc,
                    double omega, unsigned long long* dbg, hipStream_t st);
@@ -63,6 +63,8 @@ struct poms_op {
     bool v2_ok = false;
     ToepConst tc{};
 };
+
+static int resolve_variant(const poms_op* o, int epi);
 
 // Largest row range [lo, hi) around the middle whose band rows equal one
 // symmetric row (bitwise), for the pair (fa, fb) (fb may be null).
@@ -267,6 +269,9 @@ int poms_op_create(poms_ctx* ctx, int ndim, const poms_layout* layout, int form,
             rd[i] = dg != 0.0 ? 1.0 / dg : 0.0;
         }
         if (upload(rd.data(), rd.size(), &o->rdiag0)) { poms_op_destroy(o); return 1; }
+        // the same value on every plane of the axis-0 Toeplitz interior (bitwise: those
+        // rows equal the middle row)
+        if (is3d && o->tc.lo0 < o->tc.hi0) o->tc.rdi = rd[(o->tc.lo0 + o->tc.hi0) / 2];
     }
     *op = o;
     return 0;
@@ -281,10 +286,19 @@ int poms_op_destroy(poms_op* o) {
 }
 
 int poms_op_set_variant(poms_op* op, int variant) {
-    if (!op || variant < 0 || (variant > 10 && (variant < 90 || variant > 100))) { set_error("poms_op_set_variant: bad argument"); return 1; }
+    if (!op || variant < 0 || (variant > 10 && (variant < 90 || variant > 108))) { set_error("poms_op_set_variant: bad argument"); return 1; }
     if (variant > 0 && !op->v2_ok) { set_error("poms_op_set_variant: variant needs pads == pmax"); return 1; }
     if (variant == 5 && op->pmax > 3) variant = 4;  // 32-row tile does not fit LDS at p >= 4
     op->variant = variant;
+    return 0;
+}
+
+int poms_op_kernel_variant(poms_op* op, int epilogue, int* variant) {
+    if (!op || !variant || epilogue < EPI_APPLY || epilogue > EPI_APPLYDOT) {
+        set_error("poms_op_kernel_variant: bad argument");
+        return 1;
+    }
+    *variant = resolve_variant(op, epilogue);
     return 0;
 }
 
@@ -335,7 +349,7 @@ static int auto_chunk(int nz, int tiles, int p, double slots = 512.0) {
 // v5 (variant 10) runs 3D FORM_SUM operators, p <= 3, pads == pmax, arrays < 2 GiB
 static bool v5_ok(const poms_op* o) {
     const int64_t bytes = (int64_t)(o->L.n[0] + 2 * o->L.pads[0]) * row_geom(&o->L).s0 * 8;
-    return o->ndim == 3 && o->form == FORM_SUM && o->v2_ok && o->pmax <= 3 && bytes < 0x7fffffffLL;
+    return o->ndim == 3 && o->form == FORM_SUM && o->v2_ok && o->pmax <= 3 && bytes < 0x7ffffff0LL;
 }
 
 // v5 tiles are line-aligned when the row pitch is a multiple of 16 doubles and
@@ -378,6 +392,22 @@ static int op_geom(poms_op* o, int64_t zb, int64_t ze, KronGeom& g, int v = -1, 
 // variants whose Jacobi epilogue also accumulates x_out . b (v3 and v4 kernels)
 static bool fused_dot_ok(const poms_op* o) { return o->variant >= 4 && o->variant <= 10; }
 
+// The kernel variant one launch of epilogue `epi` runs (see op_run).
+static int resolve_variant(const poms_op* o, int epi) {
+    int v = o->variant;
+    if (v == 8) {
+        const bool plain = epi == EPI_APPLY || epi == EPI_RESID || epi == EPI_JACOBI;
+        if (o->ndim == 3 && v5_ok(o) && epi != EPI_JACOBI0)
+            v = 10;   // v5 (p <= 3): kernel_bench at 515^3, p = 3
+        else if (o->ndim == 3)
+            v = ((epi == EPI_APPLY && o->pmax >= 3) || (plain && o->pmax >= 4)) ? 7 : 9;
+        else
+            v = ((epi == EPI_APPLY || epi == EPI_RESID) && o->pmax <= 3) ? 7 : 9;
+    }
+    if (v == 10 && (!v5_ok(o) || epi == EPI_JACOBI0)) v = 9;
+    return v;
+}
+
 static int op_run(poms_op* o, int epi, double omega, const double* x, double* y, const double* b,
                   int64_t zb, int64_t ze, int want_norm, void* stream, int want_dot = 0) {
     if (!o || !x || !y) { set_error("null operator or vector"); return 1; }
@@ -400,16 +430,11 @@ static int op_run(poms_op* o, int epi, double omega, const double* x, double* y,
     // for every plain epilogue at p >= 4 (VALU-bound there), v3 with whole-array
     // buffer resources (9; falls back to 4 for arrays >= 2 GiB) otherwise; in 2D
     // v4 for apply / residual at p <= 3.  Fused dots and two-sweeps-from-zero: 9.
-    // Variant 10 (v5) runs apply / residual / Jacobi / apply+dot; 9 otherwise.
-    int v = o->variant;
-    if (v == 8) {
-        const bool plain = epi == EPI_APPLY || epi == EPI_RESID || epi == EPI_JACOBI;
-        if (o->ndim == 3)
-            v = ((epi == EPI_APPLY && o->pmax >= 3) || (plain && o->pmax >= 4)) ? 7 : 9;
-        else
-            v = ((epi == EPI_APPLY || epi == EPI_RESID) && o->pmax <= 3) ? 7 : 9;
-    }
-    if (v == 10 && (!v5_ok(o) || epi == EPI_JACOBI0)) v = 9;
+    // Variant 10 (v5) runs apply / residual / Jacobi / apply+dot of 3D p <= 3
+    // operators, and is what 8 picks for them; 9 otherwise.
+    int v = resolve_variant(o, epi);
+    const int v5_diag = (v >= 101 && v <= 108) ? v - 100 : 0;   // v5 diagnostic / tuning builds
+    if (v5_diag) v = 10;
     int v5_h = 0, v5_to = 0;
     if (v == 10) kron_v5_tile(o->pmax, v5_aligned(o, x), &v5_h, &v5_to);
     KronGeom g;
@@ -420,7 +445,7 @@ static int op_run(poms_op* o, int epi, double omega, const double* x, double* y,
     KronPtrs p{x, y, b, o->a0t, o->b0t, o->a1, o->b1, o->a2, o->b2,
                want_norm ? o->ctx->scratch : nullptr, want_dot ? o->ctx->scratch + nblk : nullptr, o->rdiag0};
     const int rc = v == 10
-        ? kron_v5_launch(o->pmax, epi, p, g, o->tc, v5_h, omega, as_stream(stream))
+        ? kron_v5_launch(o->pmax, epi, p, g, o->tc, v5_h, omega, as_stream(stream), v5_diag)
         : v == 0
         ? kron_launch(o->pmax, o->ndim == 3, o->form, epi, p, g, omega, as_stream(stream))
         : (v == 7 || (v >= 92 && v <= 100))
@@ -479,7 +504,7 @@ int poms_op_jacobi_from_zero(poms_op* op, double omega, const double* b, double*
 int poms_op_from_zero_supported(poms_op* op, int* yes) {
     if (!op || !yes) { set_error("poms_op_from_zero_supported: null argument"); return 1; }
     const int64_t bytes = (int64_t)(op->L.n[0] + 2 * op->L.pads[0]) * row_geom(&op->L).s0 * 8;
-    *yes = (op->ndim == 3 && (op->variant == 8 || op->variant == 9 || op->variant == 10) && bytes < 0x7fffffffLL) ? 1 : 0;
+    *yes = (op->ndim == 3 && (op->variant == 8 || op->variant == 9 || op->variant == 10) && bytes < 0x7ffffff0LL) ? 1 : 0;
     return 0;
 }
 

@@ -68,7 +68,7 @@ class TwoLevelVCycle:
 
     def __init__(self, p: int, ncells_fine: int, ncells_coarse: int = 8, ndim: int = 3, *,
                  dist=None, mass_coef: float = 1.0, device=None, knots_fine=None, knots_coarse=None,
-                 tol: float = 1e-6, maxiter: int = 10, chunk: int = 0):
+                 tol: float = 1e-6, maxiter: int = 10, chunk: int = 0, align: bool = True):
         self.p, self.ndim = int(p), int(ndim)
         Tc = uniform_knots(p, ncells_coarse) if knots_coarse is None else np.asarray(knots_coarse, float)
         Tf = uniform_knots(p, ncells_fine) if knots_fine is None else np.asarray(knots_fine, float)
@@ -78,7 +78,9 @@ class TwoLevelVCycle:
         self.n = n
         M, K = assemble_1d(T, p)
         self.M1d, self.K1d = M, K
-        self.space = StencilVectorSpace([n] * ndim, [p] * ndim, dist=dist, device=device)
+        # line-aligned rows (pitch a multiple of 16 doubles): the v5 operator kernel
+        # then stores whole 128-B lines only
+        self.space = StencilVectorSpace([n] * ndim, [p] * ndim, dist=dist, device=device, align=align)
         self.A = KronOperator.laplace(self.space, [M] * ndim, [K] * ndim, mass_coef=mass_coef)
         if chunk:
             self.A.set_chunk(chunk)

@@ -544,6 +544,14 @@ class KronOperator:
         _lib.call("poms_op_get_variant", self._h, C.byref(v))
         return v.value
 
+    EPILOGUES = {"apply": 0, "residual": 1, "jacobi": 2, "jacobi_from_zero": 3, "apply_dot": 4}
+
+    def kernel_variant(self, epilogue: str) -> int:
+        """Variant one launch of ``epilogue`` runs after auto-selection / fall-backs."""
+        v = C.c_int()
+        _lib.call("poms_op_kernel_variant", self._h, self.EPILOGUES[epilogue], C.byref(v))
+        return v.value
+
     def _check(self, *vs):
         for v in vs:
             if not isinstance(v, StencilVector) or v.space is not self.space:

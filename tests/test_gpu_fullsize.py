@@ -34,11 +34,11 @@ def outer(vs):
     return t
 
 
-def setup(ndim, p, N, variant=None):
+def setup(ndim, p, N, variant=None, align=False):
     from poms_amd.stencil import KronOperator, StencilVectorSpace
     M, K = assemble_1d(uniform_knots(p, N), p)
     n = N + p
-    V = StencilVectorSpace([n] * ndim, [p] * ndim)
+    V = StencilVectorSpace([n] * ndim, [p] * ndim, align=align)
     A = KronOperator.laplace(V, [M] * ndim, [K] * ndim)
     if variant is not None:
         A.set_variant(variant)
@@ -60,9 +60,10 @@ def trel(a, b):
 
 
 @pytest.mark.parametrize("cfg", list(CONFIGS))
-def test_separable_apply_residual_jacobi_full_size(gpu, cfg):
+@pytest.mark.parametrize("align", [False, True])
+def test_separable_apply_residual_jacobi_full_size(gpu, cfg, align):
     ndim, p, N = CONFIGS[cfg]
-    V, A, M, K, n = setup(ndim, p, N)
+    V, A, M, K, n = setup(ndim, p, N, align=align)
     rng = np.random.default_rng(N + p)
     us = [rng.uniform(-1, 1, n) for _ in range(ndim)]
     ws = [rng.uniform(-1, 1, n) for _ in range(ndim)]
@@ -99,9 +100,10 @@ def test_separable_apply_residual_jacobi_full_size(gpu, cfg):
 
 
 @pytest.mark.parametrize("cfg", list(CONFIGS))
-def test_symmetry_full_size(gpu, cfg):
+@pytest.mark.parametrize("align", [False, True])
+def test_symmetry_full_size(gpu, cfg, align):
     ndim, p, N = CONFIGS[cfg]
-    V, A, M, K, n = setup(ndim, p, N)
+    V, A, M, K, n = setup(ndim, p, N, align=align)
     x, y = V.zeros(), V.zeros()
     g = torch.Generator(device=gpu).manual_seed(5)
     V.interior(x._data).uniform_(-1, 1, generator=g)

@@ -105,10 +105,12 @@ def test_jacobi_point(gpu):
     assert rel(x.reshape(-1), orc.jacobi(D, b.reshape(-1))) <= 1e-15
 
 
+@pytest.mark.parametrize("align", [True, False])
 @pytest.mark.parametrize("ndim,p,Nf,Nc", [(2, 1, 16, 8), (2, 3, 32, 8), (3, 2, 16, 8), (3, 3, 16, 4)])
-def test_two_level_vcycle(gpu, ndim, p, Nf, Nc):
+def test_two_level_vcycle(gpu, ndim, p, Nf, Nc, align):
     from poms_amd.mg import TwoLevelVCycle
-    mg = TwoLevelVCycle(p, Nf, Nc, ndim=ndim)
+    mg = TwoLevelVCycle(p, Nf, Nc, ndim=ndim, align=align)
+    assert mg.space.aligned == align
     b = mg.rhs_ones()
     x, ipre, ipos = mg.cycle(b)
     Ms, Ks = [mg.M1d] * ndim, [mg.K1d] * ndim

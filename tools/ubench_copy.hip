@@ -45,6 +45,40 @@ __global__ void __launch_bounds__(256) seg_kernel(const d2* x, const d2* b, d2* 
     if (MIX == 2 && acc.x == 1234.5) out[0] = acc.y;
 }
 
+
+// each thread moves 16*V contiguous bytes per step (V x 16-B loads in flight, consecutive)
+template <int V, bool NT>
+__global__ void __launch_bounds__(256) wide_copy(const d2* __restrict__ x, d2* __restrict__ y, long n) {
+    const long st = (long)gridDim.x * blockDim.x * V;
+    for (long i = ((long)blockIdx.x * blockDim.x + threadIdx.x) * V; i + V <= n; i += st) {
+        d2 v[V];
+#pragma unroll
+        for (int u = 0; u < V; ++u) v[u] = NT ? __builtin_nontemporal_load(x + i + u) : x[i + u];
+#pragma unroll
+        for (int u = 0; u < V; ++u) {
+            if (NT) __builtin_nontemporal_store(v[u], y + i + u);
+            else y[i + u] = v[u];
+        }
+    }
+}
+// wave-contiguous: each wave moves U consecutive 1-KiB pieces per step
+template <int U, bool NT>
+__global__ void __launch_bounds__(256) wave_copy(const d2* __restrict__ x, d2* __restrict__ y, long n) {
+    const int lane = threadIdx.x & 63;
+    const long wave = ((long)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+    const long nw = ((long)gridDim.x * blockDim.x) >> 6;
+    for (long base = wave * 64 * U; base + 64 * U <= n; base += nw * 64 * U) {
+        d2 v[U];
+#pragma unroll
+        for (int u = 0; u < U; ++u) v[u] = NT ? __builtin_nontemporal_load(x + base + u * 64 + lane) : x[base + u * 64 + lane];
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            if (NT) __builtin_nontemporal_store(v[u], y + base + u * 64 + lane);
+            else y[base + u * 64 + lane] = v[u];
+        }
+    }
+}
+
 template <typename F>
 static float time_it(F f) {
     hipEvent_t e0, e1;
@@ -80,7 +114,7 @@ int main() {
     printf("gs copy 8192x256: %.1f us %.2f TB/s\n", ms * 1e3, 2 * B / (ms * 1e-3) / 1e12);
     const char* mixn[] = {"copy", "x+b", "read", "write"};
     const double mixb[] = {2, 3, 1, 1};
-    for (int blocks : {1024, 2048, 4096, 8192, 16384}) {
+    for (int blocks : {8192}) {
         const long seg = (n + blocks - 1) / blocks;
         for (int mix = 0; mix < 4; ++mix) {
             for (int u : {2, 4, 8}) {
@@ -95,6 +129,15 @@ int main() {
                 printf("seg %5d blocks U=%d %-5s: %8.1f us %.2f TB/s\n", blocks, u, mixn[mix], ms * 1e3, mixb[mix] * B / (ms * 1e-3) / 1e12);
             }
         }
+    }
+    for (int blocks : {1024, 2048, 4096, 8192}) {
+#define WC(V, NT) { float m2 = time_it([&] { hipLaunchKernelGGL((wide_copy<V, NT>), dim3(blocks), dim3(256), 0, 0, (const d2*)x, (d2*)y, n); }); \
+        printf("wide  %5d blocks V=%d nt=%d: %8.1f us %.2f TB/s\n", blocks, V, (int)NT, m2 * 1e3, 2 * B / (m2 * 1e-3) / 1e12); }
+#define WV(U, NT) { float m2 = time_it([&] { hipLaunchKernelGGL((wave_copy<U, NT>), dim3(blocks), dim3(256), 0, 0, (const d2*)x, (d2*)y, n); }); \
+        printf("wave  %5d blocks U=%d nt=%d: %8.1f us %.2f TB/s\n", blocks, U, (int)NT, m2 * 1e3, 2 * B / (m2 * 1e-3) / 1e12); }
+        WC(2, false) WC(4, false) WC(4, true) WV(4, false) WV(8, false) WV(4, true) WV(8, true)
+#undef WC
+#undef WV
     }
     return 0;
 }
