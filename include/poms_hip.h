@@ -205,6 +205,16 @@ int poms_pcg_r_update(poms_ctx* ctx, const poms_layout* L, double alpha, double*
  * `sources/solvers.py:106` of iteration k and :124 of the same iteration.    */
 int poms_pcg_xp_update(poms_ctx* ctx, const poms_layout* L, double alpha, double beta,
                        double* x, double* p, const double* s, void* stream);
+/* Device-coefficient forms of axpby / pcg_r_update / pcg_xp_update: the kernel
+ * reads (a, b) = ab_dev[0..1] (alpha = alpha_dev[0]) from device memory, so
+ * pcg's alpha = s.r / p.q and beta = s.r / s.r_old are formed on the device and
+ * never synchronise the host (`sources/solvers.py:105,107,123-124`).         */
+int poms_vec_axpby_dev(poms_ctx* ctx, const poms_layout* L, const double* ab_dev, const double* x,
+                       const double* y, double* z, void* stream);
+int poms_pcg_r_update_dev(poms_ctx* ctx, const poms_layout* L, const double* alpha_dev, double* r,
+                          const double* q, double* out_dev, void* stream);
+int poms_pcg_xp_update_dev(poms_ctx* ctx, const poms_layout* L, const double* ab_dev, double* x, double* p,
+                           const double* s, void* stream);
 /* Reduce `count` partials from the context scratch into out_dev[0]. */
 int poms_reduce_partials(poms_ctx* ctx, int64_t count, double* out_dev, void* stream);
 /* Same, starting at scratch[offset]. */

@@ -80,7 +80,9 @@ __device__ __forceinline__ void v5_barrier() {
 // XH: Jacobi x_in from the register history instead of a DMA next to b.
 // ST16: every lane's store address is 16-B aligned (host-checked; always on the
 // aligned layout): one 16-B store per lane, else two 8-B stores.
-template <int P, int EPI, int D, int MODE = 0, int CP = 0, bool XH = false, bool ST16 = true>
+// JDOT: the Jacobi sweep also accumulates x_out . b (only the last sweep of a
+// preconditioner call asks for it).
+template <int P, int EPI, int D, int MODE = 0, int CP = 0, bool XH = false, bool ST16 = true, bool JDOT = true>
 __global__ void __launch_bounds__(1024, 1)
 kron_v5_kernel(const double* __restrict__ x, double* __restrict__ y, const double* __restrict__ bvec,
                const double* __restrict__ a0t, const double* __restrict__ b0t,
@@ -412,7 +414,7 @@ kron_v5_kernel(const double* __restrict__ x, double* __restrict__ y, const doubl
                             const double dr = omega * (bv[e] - vo[e]) * rc[e];
                             outv[e] = xin[e] + dr;
                             nrm = ok[e] ? fma(dr, dr, nrm) : nrm;
-                            dotp = ok[e] ? fma(outv[e], bv[e], dotp) : dotp;
+                            if constexpr (JDOT) dotp = ok[e] ? fma(outv[e], bv[e], dotp) : dotp;
                         }
                     }
                 }
@@ -468,7 +470,7 @@ kron_v5_kernel(const double* __restrict__ x, double* __restrict__ y, const doubl
     }
 }
 
-template <int P, int EPI, int D, int MODE = 0, int CP = 0, bool XH = false, bool ST16 = true>
+template <int P, int EPI, int D, int MODE = 0, int CP = 0, bool XH = false, bool ST16 = true, bool JDOT = true>
 static int v5_launch_t1(const KronPtrs& p, const KronGeom& g, const ToepConst& tc, int H, double omega,
                         hipStream_t st) {
     // the hand-counted vmcnt waits assume the only VMEM ops in the loop are the
@@ -476,7 +478,7 @@ static int v5_launch_t1(const KronPtrs& p, const KronGeom& g, const ToepConst& t
     static int scratch = -1;
     if (scratch < 0) {
         hipFuncAttributes at{};
-        if (hipFuncGetAttributes(&at, reinterpret_cast<const void*>(&kron_v5_kernel<P, EPI, D, MODE, CP, XH, ST16>)) != hipSuccess) {
+        if (hipFuncGetAttributes(&at, reinterpret_cast<const void*>(&kron_v5_kernel<P, EPI, D, MODE, CP, XH, ST16, JDOT>)) != hipSuccess) {
             set_error("v5: hipFuncGetAttributes failed");
             return 1;
         }
@@ -487,7 +489,7 @@ static int v5_launch_t1(const KronPtrs& p, const KronGeom& g, const ToepConst& t
         return 1;
     }
     const int nblk = g.tiles2 * g.tiles1 * g.nchunks;
-    hipLaunchKernelGGL((kron_v5_kernel<P, EPI, D, MODE, CP, XH, ST16>), dim3(nblk), dim3(1024), 0, st, p.x, p.y, p.b, p.a0t, p.b0t,
+    hipLaunchKernelGGL((kron_v5_kernel<P, EPI, D, MODE, CP, XH, ST16, JDOT>), dim3(nblk), dim3(1024), 0, st, p.x, p.y, p.b, p.a0t, p.b0t,
                        p.a1, p.b1, p.a2, p.b2, p.partial, p.partial2, p.rdiag0, g, tc, H, omega);
     return 0;
 }
@@ -501,6 +503,9 @@ static int v5_launch_t(const KronPtrs& p, const KronGeom& g, const ToepConst& tc
     // the Jacobi x_in history does not fit the VGPRs beside the split stores: the
     // unaligned build DMAs x_in next to b instead
     constexpr bool XHU = (EPI == EPI_JACOBI) ? false : XH;
+    if (EPI == EPI_JACOBI && p.partial2 == nullptr)
+        return st16 ? v5_launch_t1<P, EPI, D, MODE, CP, XH, true, false>(p, g, tc, H, omega, st)
+                    : v5_launch_t1<P, EPI, D, MODE, CP, XHU, false, false>(p, g, tc, H, omega, st);
     return st16 ? v5_launch_t1<P, EPI, D, MODE, CP, XH, true>(p, g, tc, H, omega, st)
                 : v5_launch_t1<P, EPI, D, MODE, CP, XHU, false>(p, g, tc, H, omega, st);
 }

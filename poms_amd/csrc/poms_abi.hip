@@ -28,8 +28,11 @@ int kron_tile_rows();
 int kron_tile_cols();
 int vec_launch(int op, const RowGeom& g, double a, double b, const double* x, const double* y,
                double* z, double* w, const double* q, double* partial, hipStream_t st,
-               int* nblk_out);
+               int* nblk_out, const double* ab = nullptr);
 int reduce_launch(const double* partial, int count, double* out, hipStream_t st);
+int vec_flat_launch(int op, int64_t count, double a, double b, const double* x, const double* y,
+                    double* z, double* w, const double* q, double* partial, hipStream_t st,
+                    int* nblk_out, const double* ab = nullptr);
 int diag_scale_launch(bool is3d, int form, const RowGeom& g, int P, int g0, double scale,
                       const double* b, double* x, const double* a0t, const double* b0t,
                       const double* a1, const double* b1, const double* a2, const double* b2,
@@ -607,12 +610,20 @@ int poms_kron_dot_2d(poms_ctx* ctx, const int64_t* starts, const int64_t* ends,
 // ---- vector kernels -----------------------------------------------------------
 static int vec_common(poms_ctx* ctx, const poms_layout* L, int op, double a, double b,
                       const double* x, const double* y, double* z, double* w, const double* q,
-                      double* out_dev, void* stream) {
+                      double* out_dev, void* stream, const double* ab_dev = nullptr) {
     if (!ctx || !layout_ok(L)) { set_error("vector op: bad context or layout"); return 1; }
     const RowGeom g = row_geom(L);
     int nb = 0;
     const bool red = (op == V_DOT || op == V_PCGUPD || op == V_RUPD);
-    if (vec_launch(op, g, a, b, x, y, z, w, q, red ? ctx->scratch : nullptr, as_stream(stream), &nb))
+    // whole interior planes as one flat range (ghost rows / columns are zero in every
+    // vector and stay zero); the per-row kernel for fills and mixed alignments
+    const int64_t off = (int64_t)g.pd0 * g.s0, count = (int64_t)g.n0 * g.s0;
+    auto at = [&](const double* v) { return v ? v + off : nullptr; };
+    const bool flat = vec_flat_launch(op, count, a, b, at(x), at(y), const_cast<double*>(at(z)),
+                                      const_cast<double*>(at(w)), at(q), red ? ctx->scratch : nullptr,
+                                      as_stream(stream), &nb, ab_dev) == 0;
+    if (!flat && vec_launch(op, g, a, b, x, y, z, w, q, red ? ctx->scratch : nullptr, as_stream(stream), &nb,
+                            ab_dev))
         return 1;
     if (red) reduce_launch(ctx->scratch, nb, out_dev, as_stream(stream));
     POMS_HIP_CHECK(hipGetLastError());
@@ -658,6 +669,26 @@ int poms_pcg_xp_update(poms_ctx* ctx, const poms_layout* L, double alpha, double
                        double* p, const double* s, void* stream) {
     if (!x || !p || !s) { set_error("pcg_xp_update: null argument"); return 1; }
     return vec_common(ctx, L, V_XPUPD, alpha, beta, s, nullptr, x, p, nullptr, nullptr, stream);
+}
+
+// Device-coefficient forms: the scalars are read by the kernel from device memory
+// (ab_dev[0], ab_dev[1]), so pcg's alpha / beta never visit the host.
+int poms_vec_axpby_dev(poms_ctx* ctx, const poms_layout* L, const double* ab_dev, const double* x,
+                       const double* y, double* z, void* stream) {
+    if (!x || !y || !z || !ab_dev) { set_error("axpby_dev: null argument"); return 1; }
+    return vec_common(ctx, L, V_AXPBY, 0.0, 0.0, x, y, z, nullptr, nullptr, nullptr, stream, ab_dev);
+}
+
+int poms_pcg_r_update_dev(poms_ctx* ctx, const poms_layout* L, const double* alpha_dev, double* r,
+                          const double* q, double* out_dev, void* stream) {
+    if (!r || !q || !out_dev || !alpha_dev) { set_error("pcg_r_update_dev: null argument"); return 1; }
+    return vec_common(ctx, L, V_RUPD, 0.0, 0.0, nullptr, nullptr, nullptr, r, q, out_dev, stream, alpha_dev);
+}
+
+int poms_pcg_xp_update_dev(poms_ctx* ctx, const poms_layout* L, const double* ab_dev, double* x, double* p,
+                           const double* s, void* stream) {
+    if (!x || !p || !s || !ab_dev) { set_error("pcg_xp_update_dev: null argument"); return 1; }
+    return vec_common(ctx, L, V_XPUPD, 0.0, 0.0, s, nullptr, x, p, nullptr, nullptr, stream, ab_dev);
 }
 
 int poms_reduce_partials(poms_ctx* ctx, int64_t count, double* out_dev, void* stream) {

@@ -15,11 +15,12 @@ constexpr int kMaxPartials = 4096;
 
 template <int OP>
 __global__ void __launch_bounds__(256)
-vec_rows_kernel(const RowGeom g, const double a, const double b,
+vec_rows_kernel(const RowGeom g, double a, double b,
                 const double* __restrict__ x, const double* __restrict__ yv,
                 double* __restrict__ z, double* __restrict__ w, const double* __restrict__ q,
-                double* __restrict__ partial) {
+                double* __restrict__ partial, const double* __restrict__ ab) {
     __shared__ double red[4];
+    if (ab != nullptr) { a = ab[0]; b = ab[1]; }   // coefficients from device memory
     const int lane = threadIdx.x & 63;
     const int wv = threadIdx.x >> 6;
     const int64_t nrows = (int64_t)g.n0 * g.n1;
@@ -53,6 +54,115 @@ vec_rows_kernel(const RowGeom g, const double a, const double b,
                 w[o] = x[o] + b * po;
             }
         }
+    }
+    if constexpr (OP == V_DOT || OP == V_PCGUPD || OP == V_RUPD) {
+        const double t = block_sum_256(s, red);
+        if (threadIdx.x == 0) partial[blockIdx.x] = t;
+    }
+}
+
+// The same element-wise ops over a flat range of whole padded planes (interior
+// planes only): 16-B accesses, U of them in flight per thread, non-temporal
+// stores.  Valid because the ghost rows / columns (and dead pitch columns) of
+// every vector are zero and every op maps zeros to zeros: results there stay
+// zero and add nothing to the reductions.  `head` / `tail` are single leading /
+// trailing elements outside the 16-B aligned middle (done by thread 0).
+template <int OP>
+__device__ __forceinline__ void vec_elem(double a, double b, const double* x, const double* yv, double* z,
+                                         double* w, const double* q, int64_t o, double& s) {
+    if constexpr (OP == V_AXPBY) {
+        z[o] = a * x[o] + b * yv[o];
+    } else if constexpr (OP == V_SCALE) {
+        z[o] = a * x[o];
+    } else if constexpr (OP == V_DOT) {
+        s = fma(x[o], yv[o], s);
+    } else if constexpr (OP == V_PCGUPD) {
+        z[o] = fma(a, yv[o], z[o]);
+        const double rn = fma(-a, q[o], w[o]);
+        w[o] = rn;
+        s = fma(rn, rn, s);
+    } else if constexpr (OP == V_RUPD) {
+        const double rn = fma(-a, q[o], w[o]);
+        w[o] = rn;
+        s = fma(rn, rn, s);
+    } else if constexpr (OP == V_XPUPD) {
+        const double po = w[o];
+        z[o] = fma(a, po, z[o]);
+        w[o] = x[o] + b * po;
+    }
+}
+
+template <int OP>
+__global__ void __launch_bounds__(256)
+vec_flat_kernel(const int head, const int64_t nd2, const int tail, double a, double b,
+                const double* __restrict__ x, const double* __restrict__ yv, double* __restrict__ z,
+                double* __restrict__ w, const double* __restrict__ q, double* __restrict__ partial,
+                const double* __restrict__ ab) {
+    if (ab != nullptr) { a = ab[0]; b = ab[1]; }   // coefficients from device memory
+    typedef double d2 __attribute__((ext_vector_type(2)));
+    constexpr int U = 4;
+    __shared__ double red[4];
+    double s = 0.0;
+    const d2* X = (const d2*)(x + head);
+    const d2* Y = (const d2*)(yv + head);
+    d2* Z = (d2*)(z + head);
+    d2* Wv = (d2*)(w + head);
+    const d2* Q = (const d2*)(q + head);
+    const int64_t step = (int64_t)gridDim.x * 256 * U;
+    for (int64_t base = (int64_t)blockIdx.x * 256 * U + threadIdx.x; base < nd2; base += step) {
+        d2 xa[U], ya[U], za[U], wa[U], qa[U];
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const int64_t i = base + u * 256;
+            if (i < nd2) {
+                if constexpr (OP == V_AXPBY || OP == V_SCALE || OP == V_DOT || OP == V_XPUPD) xa[u] = X[i];
+                if constexpr (OP == V_AXPBY || OP == V_DOT || OP == V_PCGUPD) ya[u] = Y[i];
+                if constexpr (OP == V_PCGUPD || OP == V_XPUPD) za[u] = Z[i];
+                if constexpr (OP == V_PCGUPD || OP == V_RUPD || OP == V_XPUPD) wa[u] = Wv[i];
+                if constexpr (OP == V_PCGUPD || OP == V_RUPD) qa[u] = Q[i];
+            }
+        }
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const int64_t i = base + u * 256;
+            if (i < nd2) {
+                if constexpr (OP == V_AXPBY) {
+                    __builtin_nontemporal_store(a * xa[u] + b * ya[u], Z + i);
+                } else if constexpr (OP == V_SCALE) {
+                    __builtin_nontemporal_store(a * xa[u], Z + i);
+                } else if constexpr (OP == V_DOT) {
+                    s = fma(xa[u].x, ya[u].x, s);
+                    s = fma(xa[u].y, ya[u].y, s);
+                } else if constexpr (OP == V_PCGUPD) {
+                    __builtin_nontemporal_store(a * ya[u] + za[u], Z + i);
+                    d2 rn;
+                    rn.x = fma(-a, qa[u].x, wa[u].x);
+                    rn.y = fma(-a, qa[u].y, wa[u].y);
+                    __builtin_nontemporal_store(rn, Wv + i);
+                    s = fma(rn.x, rn.x, s);
+                    s = fma(rn.y, rn.y, s);
+                } else if constexpr (OP == V_RUPD) {
+                    d2 rn;
+                    rn.x = fma(-a, qa[u].x, wa[u].x);
+                    rn.y = fma(-a, qa[u].y, wa[u].y);
+                    __builtin_nontemporal_store(rn, Wv + i);
+                    s = fma(rn.x, rn.x, s);
+                    s = fma(rn.y, rn.y, s);
+                } else {   // V_XPUPD
+                    d2 zn, wn;
+                    zn.x = fma(a, wa[u].x, za[u].x);
+                    zn.y = fma(a, wa[u].y, za[u].y);
+                    wn.x = xa[u].x + b * wa[u].x;
+                    wn.y = xa[u].y + b * wa[u].y;
+                    __builtin_nontemporal_store(zn, Z + i);
+                    __builtin_nontemporal_store(wn, Wv + i);
+                }
+            }
+        }
+    }
+    if (blockIdx.x == 0 && threadIdx.x == 0) {
+        if (head) vec_elem<OP>(a, b, x, yv, z, w, q, 0, s);
+        if (tail) vec_elem<OP>(a, b, x, yv, z, w, q, head + 2 * nd2, s);
     }
     if constexpr (OP == V_DOT || OP == V_PCGUPD || OP == V_RUPD) {
         const double t = block_sum_256(s, red);
@@ -150,14 +260,14 @@ static int row_blocks(const RowGeom& g) {
 
 int vec_launch(int op, const RowGeom& g, double a, double b, const double* x, const double* y,
                double* z, double* w, const double* q, double* partial, hipStream_t st,
-               int* nblk_out) {
+               int* nblk_out, const double* ab) {
     const int nb = row_blocks(g);
     if (nblk_out) *nblk_out = nb;
     switch (op) {
 #define POMS_VL(OPV)                                                                        \
     case OPV:                                                                               \
         hipLaunchKernelGGL(vec_rows_kernel<OPV>, dim3(nb), dim3(256), 0, st, g, a, b, x, y, z, \
-                           w, q, partial);                                                  \
+                           w, q, partial, ab);                                              \
         return 0;
         POMS_VL(V_AXPBY)
         POMS_VL(V_SCALE)
@@ -169,6 +279,46 @@ int vec_launch(int op, const RowGeom& g, double a, double b, const double* x, co
 #undef POMS_VL
     }
     set_error("unknown vector op");
+    return 1;
+}
+
+// Flat form over `count` doubles starting at each pointer (whole interior planes).
+// The pointers must share their alignment modulo 16 B (same layout): returns 1
+// (nothing launched) otherwise, and for ops without a flat form (V_FILL).
+int vec_flat_launch(int op, int64_t count, double a, double b, const double* x, const double* y,
+                    double* z, double* w, const double* q, double* partial, hipStream_t st,
+                    int* nblk_out, const double* ab) {
+    if (op == V_FILL || count < 4) return 1;
+    int mis = -1;
+    for (const void* ptr : {(const void*)x, (const void*)y, (const void*)z, (const void*)w, (const void*)q}) {
+        if (!ptr) continue;
+        const int m = (int)(reinterpret_cast<uintptr_t>(ptr) & 15);
+        if (m & 7) return 1;
+        if (mis >= 0 && m != mis) return 1;
+        mis = m;
+    }
+    if (mis < 0) return 1;
+    const int head = mis ? 1 : 0;
+    const int64_t nd2 = (count - head) / 2;
+    const int tail = (int)((count - head) - 2 * nd2);
+    int64_t nb = (nd2 + 256 * 4 - 1) / (256 * 4);
+    if (nb > kMaxPartials) nb = kMaxPartials;
+    if (nb < 1) nb = 1;
+    if (nblk_out) *nblk_out = (int)nb;
+    switch (op) {
+#define POMS_VF(OPV)                                                                                  \
+    case OPV:                                                                                         \
+        hipLaunchKernelGGL(vec_flat_kernel<OPV>, dim3((int)nb), dim3(256), 0, st, head, nd2, tail, a, b, x, y, \
+                           z, w, q, partial, ab);                                                     \
+        return 0;
+        POMS_VF(V_AXPBY)
+        POMS_VF(V_SCALE)
+        POMS_VF(V_DOT)
+        POMS_VF(V_PCGUPD)
+        POMS_VF(V_RUPD)
+        POMS_VF(V_XPUPD)
+#undef POMS_VF
+    }
     return 1;
 }
 

@@ -57,6 +57,9 @@ def pcg(A, psolve, b, x0=None, tol=1e-6, maxiter=100, verbose=False):
     """Preconditioned conjugate gradient (`sources/solvers.py:69-135`)."""
     _check(A, b)
     V = b.space
+    if (psolve is damped_jacobi and not verbose and V.lazy_reductions and A.apply_dot_supported
+            and A.fused_dot_supported):
+        return _pcg_device(A, b, x0, tol, maxiter)
     ctx, lay = V.ctx, V.layout
     if x0 is None:
         x = V.zeros()
@@ -103,6 +106,80 @@ def pcg(A, psolve, b, x0=None, tol=1e-6, maxiter=100, verbose=False):
         print("+---------+---------------------+")
     info = {"niter": k, "success": nrmr < tol * nrmr0, "res_norm": sqrt(nrmr)}
     return x, info
+
+
+def _pcg_device(A, b, x0, tol, maxiter):
+    """pcg with damped_jacobi as psolve, scalars on the device.
+
+    Same iterates and stopping rule as the host loop above (`sources/solvers.py:69-135`).
+    alpha = s.r / p.q and beta = s.r / s.r_old are device tensors read by the
+    update kernels (``poms_*_dev``); the host reads only r.r for the stop test,
+    and only after the next preconditioner call is queued, so the device never
+    idles waiting for the host.  If the test fires, that queued psolve(r) is
+    discarded (the reference stops before computing it: results are identical).
+    """
+    import torch
+    V = b.space
+    if x0 is None:
+        x = V.zeros()
+        r = V.empty().assign(b)
+    else:
+        assert x0.shape == (A.shape[0],)
+        x = x0.copy()
+        r = A.residual(b, x)
+    nrmr0 = sqrt(r.dot(r))
+    s, sr = _damped_jacobi(A, r, want_dot=True, device_dot=True)
+    if sr is None:
+        sr = s.dot_device(r)
+    p = s
+    q = V.empty()
+    k = 0
+    nrmr = nrmr0 * nrmr0
+    for k in range(1, maxiter + 1):
+        pq = A.dot_inner(p, q, device=True)
+        alpha = sr / pq
+        nrm_dev = _pcg_r_update_dev(V, alpha, r, q)     # r -= alpha q ; r.r (device)
+        pending = V.lazy_value(nrm_dev)
+        srold = sr
+        s_next, sr = _damped_jacobi(A, r, want_dot=True, device_dot=True)   # queued before the read
+        if sr is None:
+            sr = s_next.dot_device(r)
+        nrmr = pending.value()
+        if nrmr < tol * nrmr0:
+            _vec_dev(V, "poms_vec_axpby_dev", torch.cat([torch.ones_like(alpha), alpha]), x, p, x)
+            k -= 1
+            break
+        beta = sr / srold
+        _pcg_xp_update_dev(V, torch.cat([alpha, beta]), x, p, s_next)
+    info = {"niter": k, "success": nrmr < tol * nrmr0, "res_norm": sqrt(nrmr)}
+    return x, info
+
+
+def _vec_dev(V, name, ab, xv, yv, zv):
+    from . import _lib, runtime as rt
+    import ctypes as C
+    _lib.call(name, V.ctx, C.byref(V.layout), rt.ptr(ab), rt.ptr(xv._data), rt.ptr(yv._data), rt.ptr(zv._data),
+              rt.stream_handle())
+    zv._mark_written()
+
+
+def _pcg_r_update_dev(V, alpha, r, q):
+    from . import _lib, runtime as rt
+    import ctypes as C
+    buf = V.scalar_buffer()
+    _lib.call("poms_pcg_r_update_dev", V.ctx, C.byref(V.layout), rt.ptr(alpha), rt.ptr(r._data), rt.ptr(q._data),
+              rt.ptr(buf), rt.stream_handle())
+    r._mark_written()
+    return V.device_sum(buf[0:1])
+
+
+def _pcg_xp_update_dev(V, ab, x, p, s):
+    from . import _lib, runtime as rt
+    import ctypes as C
+    _lib.call("poms_pcg_xp_update_dev", V.ctx, C.byref(V.layout), rt.ptr(ab), rt.ptr(x._data), rt.ptr(p._data),
+              rt.ptr(s._data), rt.stream_handle())
+    x._mark_written()
+    p._mark_written()
 
 
 def _psolve_dot(A, psolve, r):
@@ -169,9 +246,10 @@ def damped_jacobi(A, b, x0=None, tol=1e-6, maxiter=10, verbose=False):
     return _damped_jacobi(A, b, x0, tol, maxiter, verbose)[0]
 
 
-def _damped_jacobi(A, b, x0=None, tol=1e-6, maxiter=10, verbose=False, want_dot=False):
+def _damped_jacobi(A, b, x0=None, tol=1e-6, maxiter=10, verbose=False, want_dot=False, device_dot=False):
     """damped_jacobi; with ``want_dot`` also returns ``x.b`` accumulated by the final
-    sweep (None when the last sweep was not a full sweep)."""
+    sweep (None when the last sweep was not a full sweep); ``device_dot`` returns it
+    as a device tensor and skips the last sweep's norm (it cannot change the result)."""
     _check(A, b)
     V = b.space
     omega = OMEGA
@@ -240,7 +318,10 @@ def _damped_jacobi(A, b, x0=None, tol=1e-6, maxiter=10, verbose=False, want_dot=
     if maxiter >= k0:
         xn = V.empty()
         for k in range(k0, maxiter + 1):
-            if want_dot and k == maxiter:   # the last sweep also forms x_out . b
+            if want_dot and k == maxiter and device_dot and lazy:
+                # the last sweep's stop test cannot change the result: no norm, dot on device
+                nrmr, dot = A.jacobi_sweep(b, x, xn, omega, want_norm=False, want_dot=True, device_dot=True)
+            elif want_dot and k == maxiter:   # the last sweep also forms x_out . b
                 nrmr, dot = A.jacobi_sweep(b, x, xn, omega, want_norm=need, want_dot=True)
             else:
                 nrmr = A.jacobi_sweep(b, x, xn, omega, want_norm=need, lazy=lazy)
@@ -250,6 +331,8 @@ def _damped_jacobi(A, b, x0=None, tol=1e-6, maxiter=10, verbose=False, want_dot=
                 if done:
                     return xprev, None
             x, xn = xn, x
+            if want_dot and k == maxiter and device_dot and lazy:
+                break
             if lazy and not (want_dot and k == maxiter):
                 pending = (nrmr, x)
                 continue
@@ -257,7 +340,7 @@ def _damped_jacobi(A, b, x0=None, tol=1e-6, maxiter=10, verbose=False, want_dot=
                 break
             if verbose:
                 print(template.format(k, sqrt(nrmr)))
-    if pending is not None:             # the last sweep's test cannot change the result
+    if pending is not None and not device_dot:   # the last sweep's test cannot change the result
         pending[0].value()
     if verbose:
         print("+---------+---------------------+")

@@ -155,6 +155,30 @@ class StencilVectorSpace:
         self._pin_next += k
         return LazyScalar(tot, slot)
 
+    def device_sum(self, *partial_sums: torch.Tensor) -> torch.Tensor:
+        """Global sums of device partial-sum slices as a device tensor (RCCL all-reduce
+        across slabs on the device stream; nothing is read by the host)."""
+        tot = torch.stack([ps.sum() for ps in partial_sums])
+        if self.is_distributed:
+            import torch.distributed as dist
+            dist.all_reduce(tot, group=self.dist.group)
+        return tot
+
+    def lazy_value(self, dev: torch.Tensor) -> "LazyScalar":
+        """Copy a device scalar tensor to pinned host memory without blocking.
+
+        Its own ring (apart from :meth:`lazy_sum`'s), so that the damped-Jacobi
+        norms queued after it cannot overwrite the slot before it is read."""
+        if getattr(self, "_pinned_v", None) is None:
+            self._pinned_v = torch.zeros(8, dtype=F64).pin_memory()
+            self._pinv_next = 0
+        k = dev.numel()
+        if self._pinv_next + k > 8:
+            self._pinv_next = 0
+        slot = self._pinned_v[self._pinv_next:self._pinv_next + k]
+        self._pinv_next += k
+        return LazyScalar(dev, slot)
+
     def global_dot(self, local: float) -> float:
         if self.is_distributed:
             comm = rt.Comm.from_env(self.dist.group)
@@ -287,6 +311,14 @@ class StencilVector:
                   rt.ptr(self._data), rt.ptr(self._data), _stream())
         self._mark_written()
         return self
+
+    def dot_device(self, other: "StencilVector") -> torch.Tensor:
+        """Global inner product as a device tensor of shape (1,) (no host read)."""
+        V = self._space
+        buf = V.scalar_buffer()
+        _lib.call("poms_vec_dot", V.ctx, C.byref(V.layout), rt.ptr(self._data), rt.ptr(other._data),
+                  rt.ptr(buf), _stream())
+        return V.device_sum(buf[0:1])
 
     def dot(self, other: "StencilVector") -> float:
         """Global inner product (RCCL all-reduce across slabs), as spl ``StencilVector.dot``."""
@@ -622,8 +654,9 @@ class KronOperator:
         _lib.call("poms_op_apply_dot_supported", self._h, C.byref(v))
         return bool(v.value)
 
-    def dot_inner(self, x: StencilVector, out: StencilVector) -> float:
-        """``out = A x`` and the global ``x . out`` from the same pass (pcg's q and p.q)."""
+    def dot_inner(self, x: StencilVector, out: StencilVector, device: bool = False):
+        """``out = A x`` and the global ``x . out`` from the same pass (pcg's q and p.q);
+        with ``device`` the dot stays a device tensor of shape (1,)."""
         self._check(x, out)
         if out is x:
             raise ValueError("out must not alias x")
@@ -635,6 +668,8 @@ class KronOperator:
 
         n = self._launch(fn, x, norm_buf=nb, kind="apply", want_dot=True)
         out._mark_written()
+        if device and V.lazy_reductions:
+            return V.device_sum(nb[4:4 + n])
         return V.global_dot(float(nb[4:4 + n].sum().item()))
 
     def residual(self, b: StencilVector, x: StencilVector, out: StencilVector | None = None) -> StencilVector:
@@ -658,7 +693,8 @@ class KronOperator:
         return bool(v.value)
 
     def jacobi_sweep(self, b: StencilVector, x_in: StencilVector, x_out: StencilVector,
-                     omega: float, want_norm: bool = False, want_dot: bool = False, lazy: bool = False):
+                     omega: float, want_norm: bool = False, want_dot: bool = False, lazy: bool = False,
+                     device_dot: bool = False):
         """x_out = x_in + omega (b - A x_in)/diag(A).
 
         Returns the global ``||dr||^2`` (or None); with ``want_dot`` returns
@@ -679,6 +715,8 @@ class KronOperator:
 
         n = self._launch(fn, x_in, want_norm=want_norm, norm_buf=nb, kind="jacobi", want_dot=want_dot)
         x_out._mark_written()
+        if want_dot and device_dot and not want_norm and V.lazy_reductions:
+            return None, V.device_sum(nb[4:4 + n])    # x_out . b as a device tensor (1,)
         if want_dot:
             host = nb.cpu()   # one read for both reductions
             nrm = V.global_dot(float(host[:n].sum())) if want_norm else None
