@@ -138,13 +138,29 @@ class StencilVectorSpace:
         """Global sums can stay on the device stream (single rank, or RCCL)."""
         return not self.is_distributed or self.dist.cuda_transport
 
+    def _side_stream(self) -> torch.cuda.Stream:
+        if getattr(self, "_side", None) is None:
+            self._side = torch.cuda.Stream(device=f"cuda:{self.device}")
+        return self._side
+
     def lazy_sum(self, *partial_sums: torch.Tensor) -> "LazyScalar":
         """Global sums of device partial-sum slices, copied to pinned host memory
-        without blocking the host; ``.value(i)`` waits for that copy only."""
+        without blocking the host; ``.value(i)`` waits for that copy only.
+
+        The local sums are snapshotted on the launch stream (the partial-sum
+        buffer is reused by the next launch); the RCCL all-reduce and the copy run
+        on a side stream, so the next sweep never waits for them."""
         tot = torch.stack([ps.sum() for ps in partial_sums])
-        if self.is_distributed:
-            import torch.distributed as dist
-            dist.all_reduce(tot, group=self.dist.group)
+        side = self._side_stream()
+        side.wait_stream(torch.cuda.current_stream(tot.device))
+        tot.record_stream(side)
+        with torch.cuda.stream(side):
+            if self.is_distributed:
+                import torch.distributed as dist
+                dist.all_reduce(tot, group=self.dist.group)
+            return self._lazy_copy(tot)
+
+    def _lazy_copy(self, tot: torch.Tensor) -> "LazyScalar":
         if self._pinned is None:
             self._pinned = torch.zeros(8, dtype=F64).pin_memory()
             self._pin_next = 0
