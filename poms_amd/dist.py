@@ -39,8 +39,14 @@ class SlabDistribution:
     world: int
     group: object = None
     cuda_transport: bool = True
+    # global sums stay on the device (device tensors all-reduced by the backend);
+    # default: with the RCCL transport.  gloo also reduces CUDA tensors (host
+    # staged), which the 2-rank GPU test uses to run the device-scalar pcg path.
+    device_reductions: bool | None = None
 
     def __post_init__(self):
+        if self.device_reductions is None:
+            self.device_reductions = self.cuda_transport
         self.start, self.end = slab_bounds(self.n0_global, self.world, self.rank)
         if self.end <= self.start:
             raise ValueError(f"rank {self.rank} owns no planes ({self.n0_global} over {self.world})")
@@ -52,11 +58,12 @@ class SlabDistribution:
         return self.end - self.start
 
     @classmethod
-    def from_process_group(cls, n0_global: int, group=None) -> "SlabDistribution":
+    def from_process_group(cls, n0_global: int, group=None, device_reductions: bool | None = None
+                           ) -> "SlabDistribution":
         import torch.distributed as dist
         backend = dist.get_backend(group)
         return cls(n0_global, dist.get_rank(group), dist.get_world_size(group), group,
-                   cuda_transport=(backend == "nccl"))
+                   cuda_transport=(backend == "nccl"), device_reductions=device_reductions)
 
     # ------------------------------------------------------------------
     def start_exchange(self, data: torch.Tensor, width: int, pad: int):

@@ -136,7 +136,7 @@ class StencilVectorSpace:
     @property
     def lazy_reductions(self) -> bool:
         """Global sums can stay on the device stream (single rank, or RCCL)."""
-        return not self.is_distributed or self.dist.cuda_transport
+        return not self.is_distributed or bool(self.dist.device_reductions)
 
     def _side_stream(self) -> torch.cuda.Stream:
         if getattr(self, "_side", None) is None:

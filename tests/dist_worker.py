@@ -157,7 +157,9 @@ def run_gpu():
     pz = np.einsum("ia,jb,kc,abc->ijk", P1, P1, P1, xc.reshape((P1.shape[1],) * 3))
     check(rel(z.to_local_numpy(), pz[sl]) <= 1e-14, "distributed prolongation")
     # two-level V-cycle over the slabs vs the global oracle (p=2: stable smoother)
-    mg = TwoLevelVCycle(2, 16, 4, ndim=3, dist=SlabDistribution.from_process_group(18))
+    devred = os.environ.get("POMS_TEST_DEVRED") == "1"
+    mg = TwoLevelVCycle(2, 16, 4, ndim=3, dist=SlabDistribution.from_process_group(18, device_reductions=devred))
+    assert mg.space.lazy_reductions == devred or not devred
     bf = mg.rhs_ones()
     xf2, ipre, ipos = mg.cycle(bf)
     got = torch.from_numpy(xf2.toarray())

@@ -18,12 +18,12 @@ def _free_port():
         return s.getsockname()[1]
 
 
-def _launch(mode, world=2, timeout=300):
+def _launch(mode, world=2, timeout=300, extra_env=None):
     port = _free_port()
     procs = []
     for r in range(world):
         env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(world),
-                   MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), OMP_NUM_THREADS="2")
+                   MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), OMP_NUM_THREADS="2", **(extra_env or {}))
         procs.append(subprocess.Popen([sys.executable, str(WORKER), mode], env=env,
                                       stdout=subprocess.PIPE, stderr=subprocess.STDOUT, text=True))
     outs = []
@@ -64,9 +64,12 @@ def test_two_rank_halo_exchange_and_slab_apply_cpu():
 
 
 @pytest.mark.gpu
-def test_two_rank_distributed_operator_and_vcycle_gpu():
+@pytest.mark.parametrize("device_reductions", [False, True])
+def test_two_rank_distributed_operator_and_vcycle_gpu(device_reductions):
+    """device_reductions: the global sums stay device tensors (gloo reduces CUDA
+    tensors), which runs the RCCL configuration's device-scalar pcg path."""
     # device_count() does not initialise HIP in this (parent) process: the ranks
     # are the only processes that touch the GPU here
     import torch
     assert torch.cuda.device_count() >= 1, "GPU test selected but no GPU visible"
-    _launch("gpu")
+    _launch("gpu", extra_env={"POMS_TEST_DEVRED": "1" if device_reductions else "0"})
