@@ -109,6 +109,20 @@ int poms_op_get_variant(poms_op* op, int* variant);
  * fall-backs: 0 apply, 1 residual, 2 Jacobi sweep, 3 two sweeps from zero,
  * 4 apply + x.y.                                                              */
 int poms_op_kernel_variant(poms_op* op, int epilogue, int* variant);
+/* One operator launch on planes [z_begin, z_end) and its reductions, in one
+ * call: epilogue as in poms_op_kernel_variant (0 apply y = A x; 1 residual
+ * y = b - A x; 2 Jacobi sweep y = x + omega (b - A x)/diag; 3 sweeps 1-2 from
+ * zero, x = b; 4 apply + x.y).  If norm_out / dot_out (device) are non-null the
+ * per-block partials are reduced into them (accumulate: added to their value),
+ * as poms_op_jacobi_sweep_dot / poms_op_apply_dot + poms_reduce_partials_at
+ * would: Jacobi: norm = ||dr||^2, dot = x_out . b; from zero: norm = ||dr_2||^2,
+ * dot = ||x1||^2; apply + dot: dot = x . y.                                   */
+int poms_op_run_reduce(poms_op* op, int epilogue, double omega, const double* x, double* y,
+                       const double* b, int64_t z_begin, int64_t z_end, double* norm_out,
+                       double* dot_out, int accumulate, void* stream);
+/* hipMemcpyAsync of `count` doubles, device -> (pinned) host, on `stream`. */
+int poms_copy_to_host_async(poms_ctx* ctx, const double* src_dev, double* dst_host, int64_t count,
+                            void* stream);
 
 /* y = A x on output planes [z_begin, z_end) (local axis-0 indices; 2D/1D: 0,1).
  * x must have current ghosts on the planes the range touches.

@@ -76,7 +76,9 @@ __device__ __forceinline__ void v5_barrier() {
 
 // MODE (diagnostic builds, apply only): 1 = memory only (the centre tap is stored,
 // no arithmetic), 2 = arithmetic only (no DMA; the LDS ring is never filled).
-// CP: cache policy bits -- 1: x DMAs nt, 2: b / x_in DMAs nt, 4: y stores nt.
+// CP: cache policy bits -- 1: x DMAs nt, 2: b / x_in DMAs nt, 4: y stores nt,
+// 8: nt on the x rows no other tile reads (x-tile rows 2P .. T1-1; the first and
+// last 2P rows are the neighbouring tiles' halo and keep the default policy).
 // XH: Jacobi x_in from the register history instead of a DMA next to b.
 // ST16: every lane's store address is 16-B aligned (host-checked; always on the
 // aligned layout): one 16-B store per lane, else two 8-B stores.
@@ -195,7 +197,10 @@ kron_v5_kernel(const double* __restrict__ x, double* __restrict__ y, const doubl
         const bool ok = sp >= 0 && sp < nsp;
         const uint32_t so = ok ? (uint32_t)sp * plane8 : 0u;
         // x-tile row q = storage row r0 + q
-        dma16s<XAUX>(rx, lds + XS_OFF + (slot * XR + wv) * TC, ok ? (r0 + wv) * s1 * 8 + colb : 0x7ffffff0, so);
+        if ((CP & 8) && wv >= 2 * P)   // a row only this tile reads: stream it
+            dma16s<2>(rx, lds + XS_OFF + (slot * XR + wv) * TC, ok ? (r0 + wv) * s1 * 8 + colb : 0x7ffffff0, so);
+        else
+            dma16s<XAUX>(rx, lds + XS_OFF + (slot * XR + wv) * TC, ok ? (r0 + wv) * s1 * 8 + colb : 0x7ffffff0, so);
         if (wv < XR - NW)
             dma16s<XAUX>(rx, lds + XS_OFF + (slot * XR + NW + wv) * TC, ok ? (r0 + NW + wv) * s1 * 8 + colb : 0x7ffffff0, so);
     };
@@ -518,7 +523,8 @@ static int v5_launch_p(int epi, const KronPtrs& p, const KronGeom& g, const Toep
         // (tools/kernel_bench.py, variants 103-106 at 515^3: apply 555 -> 534 us,
         // residual 713 -> 672, Jacobi 886 -> 777; nt x DMAs cost 15 %: the halo rows
         // are re-read by the neighbouring tiles)
-        case EPI_APPLY: return v5_launch_t<P, EPI_APPLY, 4, 0, 6>(p, g, tc, H, omega, st);
+        // apply: also nt on the x rows no other tile reads (variant 109: 568 -> 539 us)
+        case EPI_APPLY: return v5_launch_t<P, EPI_APPLY, 4, 0, 14>(p, g, tc, H, omega, st);
         case EPI_RESID: return v5_launch_t<P, EPI_RESID, 3, 0, 6>(p, g, tc, H, omega, st);
         case EPI_JACOBI: return v5_launch_t<P, EPI_JACOBI, 3, 0, 6, true>(p, g, tc, H, omega, st);
         case EPI_APPLYDOT: return v5_launch_t<P, EPI_APPLYDOT, 4, 0, 6>(p, g, tc, H, omega, st);
@@ -569,6 +575,7 @@ int kron_v5_launch(int pmax, int epi, const KronPtrs& p, const KronGeom& g, cons
             case 6: V5CP(4, true)
             case 7: V5CP(0, false)
             case 8: V5CP(2, false)
+            case 9: V5CP(14, true)   // default + nt on the rows no other tile reads
         }
 #undef V5CP
         set_error("v5 diag mode: bad mode / epilogue");

@@ -29,7 +29,7 @@ int kron_tile_cols();
 int vec_launch(int op, const RowGeom& g, double a, double b, const double* x, const double* y,
                double* z, double* w, const double* q, double* partial, hipStream_t st,
                int* nblk_out, const double* ab = nullptr);
-int reduce_launch(const double* partial, int count, double* out, hipStream_t st);
+int reduce_launch(const double* partial, int count, double* out, hipStream_t st, int accumulate = 0);
 int vec_flat_launch(int op, int64_t count, double a, double b, const double* x, const double* y,
                     double* z, double* w, const double* q, double* partial, hipStream_t st,
                     int* nblk_out, const double* ab = nullptr);
@@ -289,7 +289,7 @@ int poms_op_destroy(poms_op* o) {
 }
 
 int poms_op_set_variant(poms_op* op, int variant) {
-    if (!op || variant < 0 || (variant > 10 && (variant < 90 || variant > 108))) { set_error("poms_op_set_variant: bad argument"); return 1; }
+    if (!op || variant < 0 || (variant > 10 && (variant < 90 || variant > 109))) { set_error("poms_op_set_variant: bad argument"); return 1; }
     if (variant > 0 && !op->v2_ok) { set_error("poms_op_set_variant: variant needs pads == pmax"); return 1; }
     if (variant == 5 && op->pmax > 3) variant = 4;  // 32-row tile does not fit LDS at p >= 4
     op->variant = variant;
@@ -436,7 +436,7 @@ static int op_run(poms_op* o, int epi, double omega, const double* x, double* y,
     // Variant 10 (v5) runs apply / residual / Jacobi / apply+dot of 3D p <= 3
     // operators, and is what 8 picks for them; 9 otherwise.
     int v = resolve_variant(o, epi);
-    const int v5_diag = (v >= 101 && v <= 108) ? v - 100 : 0;   // v5 diagnostic / tuning builds
+    const int v5_diag = (v >= 101 && v <= 109) ? v - 100 : 0;   // v5 diagnostic / tuning builds
     if (v5_diag) v = 10;
     int v5_h = 0, v5_to = 0;
     if (v == 10) kron_v5_tile(o->pmax, v5_aligned(o, x), &v5_h, &v5_to);
@@ -545,6 +545,55 @@ int poms_op_profile_phases(poms_op* o, int jacobi, const double* b, const double
     kron_v2_stamps(o->variant, jacobi ? EPI_JACOBI : EPI_APPLY, p, g, o->tc, 2.0 / 3.0,
                    reinterpret_cast<unsigned long long*>(dbg), as_stream(stream));
     POMS_HIP_CHECK(hipGetLastError());
+    return 0;
+}
+
+// One launch plus its reductions (one host call instead of three).
+int poms_op_run_reduce(poms_op* op, int epilogue, double omega, const double* x, double* y,
+                       const double* b, int64_t zb, int64_t ze, double* norm_out, double* dot_out,
+                       int accumulate, void* stream) {
+    if (!op) { set_error("poms_op_run_reduce: null operator"); return 1; }
+    const bool wn = norm_out != nullptr, wd = dot_out != nullptr;
+    switch (epilogue) {
+        case EPI_APPLY:
+            if (wn || wd) { set_error("poms_op_run_reduce: apply has no reductions"); return 1; }
+            if (op_run(op, EPI_APPLY, 0.0, x, y, nullptr, zb, ze, 0, stream)) return 1;
+            break;
+        case EPI_RESID:
+            if (wn || wd) { set_error("poms_op_run_reduce: residual has no reductions"); return 1; }
+            if (op_run(op, EPI_RESID, 0.0, x, y, b, zb, ze, 0, stream)) return 1;
+            break;
+        case EPI_JACOBI:
+            if (x == y) { set_error("jacobi sweep: x_out must not alias x_in"); return 1; }
+            if (op_run(op, EPI_JACOBI, omega, x, y, b, zb, ze, wn ? 1 : 0, stream, wd ? 1 : 0)) return 1;
+            break;
+        case EPI_JACOBI0:   // x = b: norm_out <- ||dr_2||^2, dot_out <- ||x1||^2
+            if (op->ndim != 3) { set_error("jacobi from zero: 3D operators only"); return 1; }
+            if (b == y) { set_error("jacobi from zero: x_out must not alias b"); return 1; }
+            if (wn != wd) { set_error("jacobi from zero: both norms or neither"); return 1; }
+            if (op_run(op, EPI_JACOBI0, omega, b, y, b, zb, ze, wn ? 1 : 0, stream, wn ? 1 : 0)) return 1;
+            break;
+        case EPI_APPLYDOT:
+            if (x == y) { set_error("apply: y must not alias x"); return 1; }
+            if (wn || !wd) { set_error("apply + dot: dot_out only"); return 1; }
+            if (op_run(op, EPI_APPLYDOT, 0.0, x, y, x, zb, ze, 0, stream, 1)) return 1;
+            break;
+        default:
+            set_error("poms_op_run_reduce: bad epilogue");
+            return 1;
+    }
+    const int64_t n = op->last_partials;
+    if (wn) reduce_launch(op->ctx->scratch, (int)n, norm_out, as_stream(stream), accumulate);
+    if (wd) reduce_launch(op->ctx->scratch + n, (int)n, dot_out, as_stream(stream), accumulate);
+    POMS_HIP_CHECK(hipGetLastError());
+    return 0;
+}
+
+// Async copy of `count` doubles from device memory to (pinned) host memory.
+int poms_copy_to_host_async(poms_ctx* ctx, const double* src_dev, double* dst_host, int64_t count, void* stream) {
+    if (!ctx || !src_dev || !dst_host || count < 0) { set_error("poms_copy_to_host_async: bad argument"); return 1; }
+    POMS_HIP_CHECK(hipMemcpyAsync(dst_host, src_dev, count * sizeof(double), hipMemcpyDeviceToHost,
+                                  as_stream(stream)));
     return 0;
 }
 

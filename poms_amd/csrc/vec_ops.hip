@@ -172,12 +172,12 @@ vec_flat_kernel(const int head, const int64_t nd2, const int tail, double a, dou
 
 // Deterministic single-block reduction of `count` partials.
 __global__ void __launch_bounds__(256)
-reduce_partials_kernel(const double* __restrict__ partial, int count, double* __restrict__ out) {
+reduce_partials_kernel(const double* __restrict__ partial, int count, double* __restrict__ out, int accumulate) {
     __shared__ double red[4];
     double s = 0.0;
     for (int i = threadIdx.x; i < count; i += 256) s += partial[i];
     const double t = block_sum_256(s, red);
-    if (threadIdx.x == 0) out[0] = t;
+    if (threadIdx.x == 0) out[0] = accumulate ? out[0] + t : t;
 }
 
 // x = scale * b / diag(A), optional ||x||^2 partials.  diag(A) from the 1D
@@ -322,8 +322,8 @@ int vec_flat_launch(int op, int64_t count, double a, double b, const double* x, 
     return 1;
 }
 
-int reduce_launch(const double* partial, int count, double* out, hipStream_t st) {
-    hipLaunchKernelGGL(reduce_partials_kernel, dim3(1), dim3(256), 0, st, partial, count, out);
+int reduce_launch(const double* partial, int count, double* out, hipStream_t st, int accumulate) {
+    hipLaunchKernelGGL(reduce_partials_kernel, dim3(1), dim3(256), 0, st, partial, count, out, accumulate);
     return 0;
 }
 

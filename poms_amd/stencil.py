@@ -150,7 +150,12 @@ class StencilVectorSpace:
         The local sums are snapshotted on the launch stream (the partial-sum
         buffer is reused by the next launch); the RCCL all-reduce and the copy run
         on a side stream, so the next sweep never waits for them."""
-        tot = torch.stack([ps.sum() for ps in partial_sums])
+        if not self.is_distributed and len(partial_sums) == 1:
+            # one rank, already reduced on the device: one async copy to pinned memory
+            # (no torch ops: this runs ~220 times per V-cycle)
+            src = partial_sums[0]
+            return self._lazy_copy_raw(src)
+        tot = torch.stack([ps.sum() for ps in partial_sums]) if len(partial_sums) > 1 else partial_sums[0].clone()
         side = self._side_stream()
         side.wait_stream(torch.cuda.current_stream(tot.device))
         tot.record_stream(side)
@@ -159,6 +164,20 @@ class StencilVectorSpace:
                 import torch.distributed as dist
                 dist.all_reduce(tot, group=self.dist.group)
             return self._lazy_copy(tot)
+
+    def _lazy_copy_raw(self, src: torch.Tensor) -> "LazyScalar":
+        """hipMemcpyAsync of a (contiguous) device slice into the pinned ring, on the
+        launch stream, and an event after it."""
+        if self._pinned is None:
+            self._pinned = torch.zeros(8, dtype=F64).pin_memory()
+            self._pin_next = 0
+        k = src.numel()
+        if self._pin_next + k > 8:
+            self._pin_next = 0
+        slot = self._pinned[self._pin_next:self._pin_next + k]
+        self._pin_next += k
+        _lib.call("poms_copy_to_host_async", self.ctx, rt.ptr(src), rt.ptr(slot), k, rt.stream_handle())
+        return LazyScalar(None, slot)
 
     def _lazy_copy(self, tot: torch.Tensor) -> "LazyScalar":
         if self._pinned is None:
@@ -208,8 +227,9 @@ class StencilVectorSpace:
 class LazyScalar:
     """A device scalar being copied to pinned host memory on the launch stream."""
 
-    def __init__(self, dev_value: torch.Tensor, host_slot: torch.Tensor):
-        host_slot.copy_(dev_value, non_blocking=True)
+    def __init__(self, dev_value: torch.Tensor | None, host_slot: torch.Tensor):
+        if dev_value is not None:   # else the caller already queued the copy
+            host_slot.copy_(dev_value, non_blocking=True)
         self._ev = torch.cuda.Event()
         self._ev.record()
         self._host = host_slot
@@ -605,24 +625,35 @@ class KronOperator:
             if not isinstance(v, StencilVector) or v.space is not self.space:
                 raise TypeError("vector does not belong to this operator's space")
 
-    def _launch(self, fn, x: StencilVector, *args, want_norm=False, norm_buf=None, kind="apply", want_dot=False):
-        """Run one kernel over all local planes; overlap the RCCL ghost exchange
-        with the interior planes when x's ghosts are stale."""
+    # epilogue codes of poms_op_run_reduce
+    _EPI = {"apply": 0, "residual": 1, "jacobi": 2, "jacobi2": 3, "apply_dot": 4}
+
+    def _run(self, kind: str, x: StencilVector, y: StencilVector, b: StencilVector | None = None,
+             omega: float = 0.0, norm_out: torch.Tensor | None = None, dot_out: torch.Tensor | None = None):
+        """One operator call over all local planes (``poms_op_run_reduce``); with
+        stale ghosts in a slab decomposition the RCCL ghost exchange overlaps the
+        interior planes, and the p boundary planes on each side follow.  The
+        reductions of the launches accumulate into ``norm_out`` / ``dot_out``
+        (device doubles)."""
         V = self.space
         n0 = V.local_npts[0] if V.ndim == 3 else 1
         st = _stream()
-        ranges = [(0, n0)]
+        ranges = ((0, n0),)
         handle = None
         if V.is_distributed and not x._ghost_valid:
             p0 = V.pads[0]
             handle = V.dist.start_exchange(V.planes(x._store), width=p0, pad=p0)
             if handle is not None and n0 > 2 * self.pmax:
-                ranges = [(self.pmax, n0 - self.pmax), (0, self.pmax), (n0 - self.pmax, n0)]
+                ranges = ((self.pmax, n0 - self.pmax), (0, self.pmax), (n0 - self.pmax, n0))
             else:
                 V.dist.finish_exchange(handle)
                 handle = None
-        total = 0
         self._calls += 1
+        epi = self._EPI[kind]
+        xp, yp = rt.ptr(x._data), rt.ptr(y._data)
+        bp = rt.ptr(b._data) if b is not None else None
+        np_ = rt.ptr(norm_out) if norm_out is not None else None
+        dp = rt.ptr(dot_out) if dot_out is not None else None
         for idx, (zb, ze) in enumerate(ranges):
             if idx == 1 and handle is not None:
                 V.dist.finish_exchange(handle)
@@ -630,24 +661,14 @@ class KronOperator:
             if self.timer is not None:
                 e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
                 e0.record()
-                fn(*args, zb, ze, st)
+            _lib.call("poms_op_run_reduce", self._h, epi, float(omega), xp, yp, bp, zb, ze, np_, dp,
+                      1 if idx else 0, st)
+            if self.timer is not None:
                 e1.record()
                 self.timer.append((kind, e0, e1, self._calls))
-            else:
-                fn(*args, zb, ze, st)
-            if want_norm or want_dot:
-                cnt = C.c_int64()
-                _lib.call("poms_op_last_partials", self._h, C.byref(cnt))
-                if want_norm:
-                    _lib.call("poms_reduce_partials", V.ctx, cnt.value, rt.ptr(norm_buf[idx:idx + 1]), st)
-                if want_dot:   # x_out . b partials follow the norm partials (slots 4..)
-                    _lib.call("poms_reduce_partials_at", V.ctx, cnt.value, cnt.value,
-                              rt.ptr(norm_buf[4 + idx:5 + idx]), st)
-                total += 1
         if handle is not None:
             V.dist.finish_exchange(handle)
         x._ghost_valid = True
-        return total
 
     def dot(self, x: StencilVector, out: StencilVector | None = None) -> StencilVector:
         """y = A x (spl ``StencilMatrix.dot``)."""
@@ -657,10 +678,7 @@ class KronOperator:
         if y is x:
             raise ValueError("out must not alias x")
 
-        def fn(zb, ze, st):
-            _lib.call("poms_op_apply", self._h, rt.ptr(x._data), rt.ptr(y._data), zb, ze, st)
-
-        self._launch(fn, x)
+        self._run("apply", x, y)
         y._mark_written()
         return y
 
@@ -678,15 +696,11 @@ class KronOperator:
             raise ValueError("out must not alias x")
         V = self.space
         nb = V.scalar_buffer()
-
-        def fn(zb, ze, st):
-            _lib.call("poms_op_apply_dot", self._h, rt.ptr(x._data), rt.ptr(out._data), zb, ze, st)
-
-        n = self._launch(fn, x, norm_buf=nb, kind="apply", want_dot=True)
+        self._run("apply_dot", x, out, dot_out=nb[4:5])
         out._mark_written()
         if device and V.lazy_reductions:
-            return V.device_sum(nb[4:4 + n])
-        return V.global_dot(float(nb[4:4 + n].sum().item()))
+            return V.device_sum(nb[4:5])
+        return V.global_dot(float(nb[4].item()))
 
     def residual(self, b: StencilVector, x: StencilVector, out: StencilVector | None = None) -> StencilVector:
         """r = b - A x, fused (`sources/solvers.py:85`, `sources/mg_jac.py:93`)."""
@@ -695,10 +709,7 @@ class KronOperator:
         if r is x:
             raise ValueError("out must not alias x")
 
-        def fn(zb, ze, st):
-            _lib.call("poms_op_residual", self._h, rt.ptr(b._data), rt.ptr(x._data), rt.ptr(r._data), zb, ze, st)
-
-        self._launch(fn, x, kind="residual")
+        self._run("residual", x, r, b=b)
         r._mark_written()
         return r
 
@@ -723,25 +734,20 @@ class KronOperator:
             raise ValueError("x_out must not alias x_in")
         V = self.space
         nb = V.scalar_buffer()
-        name = "poms_op_jacobi_sweep_dot" if want_dot else "poms_op_jacobi_sweep"
-
-        def fn(zb, ze, st):
-            _lib.call(name, self._h, float(omega), rt.ptr(b._data), rt.ptr(x_in._data),
-                      rt.ptr(x_out._data), zb, ze, int(want_norm), st)
-
-        n = self._launch(fn, x_in, want_norm=want_norm, norm_buf=nb, kind="jacobi", want_dot=want_dot)
+        self._run("jacobi", x_in, x_out, b=b, omega=omega, norm_out=nb[0:1] if want_norm else None,
+                  dot_out=nb[4:5] if want_dot else None)
         x_out._mark_written()
         if want_dot and device_dot and not want_norm and V.lazy_reductions:
-            return None, V.device_sum(nb[4:4 + n])    # x_out . b as a device tensor (1,)
+            return None, V.device_sum(nb[4:5])    # x_out . b as a device tensor (1,)
         if want_dot:
             host = nb.cpu()   # one read for both reductions
-            nrm = V.global_dot(float(host[:n].sum())) if want_norm else None
-            return nrm, V.global_dot(float(host[4:4 + n].sum()))
+            nrm = V.global_dot(float(host[0])) if want_norm else None
+            return nrm, V.global_dot(float(host[4]))
         if not want_norm:
             return None
         if lazy and V.lazy_reductions:
-            return V.lazy_sum(nb[:n])
-        return V.global_dot(float(nb[:n].sum().item()))
+            return V.lazy_sum(nb[0:1])
+        return V.global_dot(float(nb[0].item()))
 
     @property
     def from_zero_supported(self) -> bool:
@@ -761,19 +767,16 @@ class KronOperator:
             raise ValueError("x_out must not alias b")
         V = self.space
         nb = V.scalar_buffer()
-
-        def fn(zb, ze, st):
-            _lib.call("poms_op_jacobi_from_zero", self._h, float(omega), rt.ptr(b._data), rt.ptr(x_out._data),
-                      zb, ze, int(want_norm), st)
-
-        n = self._launch(fn, b, want_norm=want_norm, norm_buf=nb, kind="jacobi2", want_dot=want_norm)
+        # norm_out <- ||dr_2||^2 (slot 1), dot_out <- ||x1||^2 (slot 0): adjacent, one copy
+        self._run("jacobi2", b, x_out, b=b, omega=omega, norm_out=nb[1:2] if want_norm else None,
+                  dot_out=nb[0:1] if want_norm else None)
         x_out._mark_written()
         if not want_norm:
             return None
         if lazy and V.lazy_reductions:
-            return V.lazy_sum(nb[4:4 + n], nb[:n])
+            return V.lazy_sum(nb[0:2])
         host = nb.cpu()
-        return V.global_dot(float(host[4:4 + n].sum())), V.global_dot(float(host[:n].sum()))
+        return V.global_dot(float(host[0])), V.global_dot(float(host[1]))
 
     def diag_scale(self, b: StencilVector, out: StencilVector, scale: float = 1.0, want_norm: bool = False,
                    lazy: bool = False):
