@@ -102,7 +102,7 @@ def main():
     sec_per_cycle = dt / args.steps
 
     # per-launch kernel durations inside the timed region (events on the launch stream);
-    # one operator call is 1 launch, or 3 when the halo exchange overlaps the interior planes
+    # one operator call is 1 launch, or 2 when the halo exchange overlaps the interior planes
     def per_call(entries, want):
         calls = {}
         for kind, e0, e1, call in entries:

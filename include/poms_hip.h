@@ -43,6 +43,7 @@ extern "C" {
 typedef struct poms_ctx poms_ctx;           /* per-device context + scratch      */
 typedef struct poms_op poms_op;             /* Kronecker(-sum) banded operator   */
 typedef struct poms_transfer poms_transfer; /* knot-insertion R = P^T / P        */
+typedef struct poms_comm poms_comm;         /* RCCL communicator of the slabs    */
 
 /* Grid layout of a (local) padded vector.  ndim in {1,2,3}; unused leading
  * axes have n = 1 and pad = 0.  Axis order is C order: axis 2 is unit-stride. */
@@ -120,6 +121,12 @@ int poms_op_kernel_variant(poms_op* op, int epilogue, int* variant);
 int poms_op_run_reduce(poms_op* op, int epilogue, double omega, const double* x, double* y,
                        const double* b, int64_t z_begin, int64_t z_end, double* norm_out,
                        double* dot_out, int accumulate, void* stream);
+/* The same with a second plane range [z2_begin, z2_end) in the same launch (a
+ * slab's two p-plane boundaries after the ghost exchange: one launch).       */
+int poms_op_run_reduce2(poms_op* op, int epilogue, double omega, const double* x, double* y,
+                        const double* b, int64_t z_begin, int64_t z_end, int64_t z2_begin,
+                        int64_t z2_end, double* norm_out, double* dot_out, int accumulate,
+                        void* stream);
 /* hipMemcpyAsync of `count` doubles, device -> (pinned) host, on `stream`. */
 int poms_copy_to_host_async(poms_ctx* ctx, const double* src_dev, double* dst_host, int64_t count,
                             void* stream);
@@ -259,6 +266,35 @@ int poms_prolong_add(poms_transfer* tr, const double* coarse, double* fine, void
  * `sources/mg_jac.py:98-99`.                                                  */
 int poms_dense_matvec(poms_ctx* ctx, int64_t n, const double* Minv, const double* x,
                       double* y, void* stream);
+
+/* ---- native RCCL communicator (slab ghost exchange, scalar all-reduces) ------ */
+/* Replaces `_update_ghost_regions_parallel` (`pyccel/kron_product.py:21-41`) and
+ * the solvers' `comm.allreduce` (`sources/solvers.py:87-124`, `sources/mg_jac.py:95`).
+ * All RCCL work goes to one communication stream in host issue order, ordered
+ * against the caller's stream with events.                                    */
+int poms_comm_id_bytes(void);
+int poms_comm_unique_id(char* out, int len);          /* rank 0; broadcast it */
+int poms_comm_create(int device, const char* id, int rank, int nranks, poms_comm** out);
+int poms_comm_destroy(poms_comm* comm);
+int poms_comm_stream(poms_comm* comm, void** stream);
+/* data -> plane 0 of the padded local array (first ghost plane); the first /
+ * last `width` owned planes go to prev / next (-1: none), the neighbours'
+ * planes land in the ghost planes.  Starts after the work queued on `stream`;
+ * poms_halo_finish makes `stream` wait for the exchange.                       */
+int poms_halo_start(poms_comm* comm, double* data, int64_t plane_elems, int64_t n_local, int pad,
+                    int width, int prev, int next, void* stream);
+int poms_halo_finish(poms_comm* comm, void* stream);
+/* In-place global sum of `count` doubles after the work queued on `stream`;
+ * wait_back: `stream` waits for the result, else it is ready on the
+ * communication stream only.                                                  */
+int poms_allreduce_sum(poms_comm* comm, double* buf, int64_t count, void* stream, int wait_back);
+/* Lazily read global sums: a ring of device slots (2 doubles each).  A launch
+ * reduces into poms_comm_slot's slot, poms_allreduce_to_host all-reduces it and
+ * copies it to pinned host memory on the communication stream, poms_comm_wait
+ * returns when the host copy is there.                                        */
+int poms_comm_slot(poms_comm* comm, double** dev_slot, int* ticket);
+int poms_allreduce_to_host(poms_comm* comm, int ticket, int count, double* host_dst, void* stream);
+int poms_comm_wait(poms_comm* comm, int ticket);
 
 #ifdef __cplusplus
 }

@@ -62,6 +62,18 @@ _SIGS = {
     "poms_op_kernel_variant": [_vp, _i, C.POINTER(_i)],
     "poms_vec_axpby_dev": [_vp, _LP, _vp, _vp, _vp, _vp, _vp],
     "poms_op_run_reduce": [_vp, _i, _d, _vp, _vp, _vp, _i64, _i64, _vp, _vp, _i, _vp],
+    "poms_op_run_reduce2": [_vp, _i, _d, _vp, _vp, _vp, _i64, _i64, _i64, _i64, _vp, _vp, _i, _vp],
+    "poms_comm_id_bytes": [],
+    "poms_comm_unique_id": [C.c_char_p, _i],
+    "poms_comm_create": [_i, C.c_char_p, _i, _i, _pp],
+    "poms_comm_destroy": [_vp],
+    "poms_comm_stream": [_vp, _pp],
+    "poms_halo_start": [_vp, _vp, _i64, _i64, _i, _i, _i, _i, _vp],
+    "poms_halo_finish": [_vp, _vp],
+    "poms_allreduce_sum": [_vp, _vp, _i64, _vp, _i],
+    "poms_comm_slot": [_vp, _pp, C.POINTER(_i)],
+    "poms_allreduce_to_host": [_vp, _i, _i, _vp, _vp],
+    "poms_comm_wait": [_vp, _i],
     "poms_copy_to_host_async": [_vp, _vp, _vp, _i64, _vp],
     "poms_pcg_r_update_dev": [_vp, _LP, _vp, _vp, _vp, _vp, _vp],
     "poms_pcg_xp_update_dev": [_vp, _LP, _vp, _vp, _vp, _vp, _vp],

@@ -16,7 +16,7 @@ HERE = Path(__file__).resolve().parent
 CSRC = HERE / "csrc"
 LIB = HERE / "libpoms_hip.so"
 OBJ = HERE / "_obj"
-SOURCES = ["kron_fused.hip", "kron_uniform.hip", "kron_dpp.hip", "kron_v4.hip", "kron_v5.hip", "vec_ops.hip", "transfer.hip", "poms_abi.hip"]
+SOURCES = ["kron_fused.hip", "kron_uniform.hip", "kron_dpp.hip", "kron_v4.hip", "kron_v5.hip", "vec_ops.hip", "transfer.hip", "comm.hip", "poms_abi.hip"]
 ARCH = os.environ.get("POMS_OFFLOAD_ARCH", "gfx950")
 
 
@@ -65,7 +65,9 @@ def build(verbose: bool = False, force: bool = False, jobs: int = 4) -> Path:
     objs = [str(OBJ / (s + ".o")) for s in SOURCES]
     if force or todo or not LIB.exists():
         tmp = LIB.with_suffix(".so.tmp")
-        cmd = [hipcc, f"--offload-arch={ARCH}", "-shared", "-fPIC", "-o", str(tmp), *objs]
+        # librccl.so.1: at run time the one torch already loaded (same SONAME)
+        cmd = [hipcc, f"--offload-arch={ARCH}", "-shared", "-fPIC", "-o", str(tmp), *objs,
+               "-L/opt/rocm/lib", "-lrccl"]
         r = subprocess.run(cmd, capture_output=True, text=True)
         if r.returncode != 0:
             raise RuntimeError(f"link failed:\n{r.stdout}\n{r.stderr}")

@@ -22,8 +22,21 @@ struct KronGeom {
     int z_begin, z_end;  // output planes [z_begin, z_end)
     int chunk;           // output planes per workgroup (3D)
     int tiles2, tiles1, nchunks;
+    int nch1;            // chunks of [z_begin, z_end); chunks nch1.. cover [z2_begin, z2_end)
+    int z2_begin, z2_end;  // optional second plane range of the same launch (the other slab boundary)
     int tout;            // output columns per 64-column tile (v3 / v4 kernels; <= 64 - 2P)
 };
+
+// Output planes [z0, z1) of axis-0 chunk `ch` (3D launches may cover two ranges).
+__device__ __forceinline__ void chunk_planes(const KronGeom& g, int ch, int& z0, int& z1) {
+    if (ch < g.nch1) {
+        z0 = g.z_begin + ch * g.chunk;
+        z1 = min(z0 + g.chunk, g.z_end);
+    } else {
+        z0 = g.z2_begin + (ch - g.nch1) * g.chunk;
+        z1 = min(z0 + g.chunk, g.z2_end);
+    }
+}
 
 // Padded row layout used by the row-wise vector kernels.
 struct RowGeom {

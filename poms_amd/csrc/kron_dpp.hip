@@ -139,8 +139,7 @@ kron_v3_kernel(const double* __restrict__ x, double* __restrict__ y,
 
     int z0 = 0, z1 = 1;
     if constexpr (IS3D) {
-        z0 = g.z_begin + ch * g.chunk;
-        z1 = min(z0 + g.chunk, g.z_end);
+        chunk_planes(g, ch, z0, z1);
     }
     const int nplanes = IS3D ? (z1 - z0) + 2 * P : 1;
     const int nsp = g.n0 + 2 * g.pd0;

@@ -174,8 +174,8 @@ kron_v5_kernel(const double* __restrict__ x, double* __restrict__ y, const doubl
         }
     }
 
-    const int z0 = g.z_begin + ch * g.chunk;
-    const int z1 = min(z0 + g.chunk, g.z_end);
+    int z0, z1;
+    chunk_planes(g, ch, z0, z1);
     const int nplanes = (z1 - z0) + 2 * P;
     const int nsp = g.n0 + 2 * g.pd0;
     const int s1 = (int)g.s1;

@@ -362,7 +362,8 @@ static bool v5_aligned(const poms_op* o, const double* x) {
     return pitch % 16 == 0 && (reinterpret_cast<uintptr_t>(x + o->L.pads[2]) & 127) == 0;
 }
 
-static int op_geom(poms_op* o, int64_t zb, int64_t ze, KronGeom& g, int v = -1, int v5_to = 0) {
+static int op_geom(poms_op* o, int64_t zb, int64_t ze, KronGeom& g, int v = -1, int v5_to = 0,
+                   int64_t zb2 = 0, int64_t ze2 = 0) {
     if (v < 0) v = o->variant;
     const bool is3d = o->ndim == 3;
     const RowGeom r = row_geom(&o->L);
@@ -377,18 +378,25 @@ static int op_geom(poms_op* o, int64_t zb, int64_t ze, KronGeom& g, int v = -1, 
     g.tout = v == 10 ? v5_to : (o->tout > 0 ? o->tout : 64 - 2 * o->pmax);
     if (v >= 4) g.tiles2 = (int)((o->L.n[2] + g.tout - 1) / g.tout);
     if (!is3d) {
-        g.z_begin = 0; g.z_end = 1; g.chunk = 1; g.nchunks = 1;
+        g.z_begin = 0; g.z_end = 1; g.chunk = 1; g.nchunks = 1; g.nch1 = 1; g.z2_begin = g.z2_end = 0;
         return 0;
     }
     if (zb < 0 || ze > o->L.n[0] || zb > ze) { set_error("plane range outside the slab"); return 1; }
+    if (zb2 < 0 || ze2 > o->L.n[0] || zb2 > ze2 || (ze2 > zb2 && zb2 < ze && ze2 > zb)) {
+        set_error("second plane range outside the slab or overlapping the first");
+        return 1;
+    }
     g.z_begin = (int)zb;
     g.z_end = (int)ze;
-    const int nz = (int)(ze - zb);
+    g.z2_begin = (int)zb2;
+    g.z2_end = (int)ze2;
+    const int nz = (int)(ze - zb) + (int)(ze2 - zb2);
     int chunk = o->chunk;
     if (chunk <= 0) chunk = auto_chunk(nz, g.tiles2 * g.tiles1, o->pmax, v == 10 ? 256.0 : 512.0);
     chunk = std::max(1, std::min(chunk, std::max(nz, 1)));
     g.chunk = chunk;
-    g.nchunks = nz == 0 ? 0 : (nz + chunk - 1) / chunk;
+    g.nch1 = (int)((ze - zb + chunk - 1) / chunk);
+    g.nchunks = g.nch1 + (int)((ze2 - zb2 + chunk - 1) / chunk);
     return 0;
 }
 
@@ -412,7 +420,8 @@ static int resolve_variant(const poms_op* o, int epi) {
 }
 
 static int op_run(poms_op* o, int epi, double omega, const double* x, double* y, const double* b,
-                  int64_t zb, int64_t ze, int want_norm, void* stream, int want_dot = 0) {
+                  int64_t zb, int64_t ze, int want_norm, void* stream, int want_dot = 0,
+                  int64_t zb2 = 0, int64_t ze2 = 0) {
     if (!o || !x || !y) { set_error("null operator or vector"); return 1; }
     if (epi != EPI_APPLY && !b) { set_error("null right-hand side"); return 1; }
     if (epi == EPI_APPLYDOT && !(o->variant == 4 || o->variant == 5 || o->variant == 6 || o->variant == 8 ||
@@ -441,7 +450,7 @@ static int op_run(poms_op* o, int epi, double omega, const double* x, double* y,
     int v5_h = 0, v5_to = 0;
     if (v == 10) kron_v5_tile(o->pmax, v5_aligned(o, x), &v5_h, &v5_to);
     KronGeom g;
-    if (op_geom(o, zb, ze, g, v, v5_to)) return 1;
+    if (op_geom(o, zb, ze, g, v, v5_to, zb2, ze2)) return 1;
     const int64_t nblk = (int64_t)g.tiles2 * g.tiles1 * g.nchunks;
     if (nblk == 0) { o->last_partials = 0; return 0; }
     if ((want_norm || want_dot) && 2 * nblk > kScratch) { set_error("too many blocks for the partial-sum scratch"); return 1; }
@@ -548,35 +557,36 @@ int poms_op_profile_phases(poms_op* o, int jacobi, const double* b, const double
     return 0;
 }
 
-// One launch plus its reductions (one host call instead of three).
-int poms_op_run_reduce(poms_op* op, int epilogue, double omega, const double* x, double* y,
-                       const double* b, int64_t zb, int64_t ze, double* norm_out, double* dot_out,
-                       int accumulate, void* stream) {
+// One launch plus its reductions (one host call instead of three); the launch
+// may cover a second plane range [zb2, ze2) (the slab's other boundary).
+int poms_op_run_reduce2(poms_op* op, int epilogue, double omega, const double* x, double* y,
+                        const double* b, int64_t zb, int64_t ze, int64_t zb2, int64_t ze2,
+                        double* norm_out, double* dot_out, int accumulate, void* stream) {
     if (!op) { set_error("poms_op_run_reduce: null operator"); return 1; }
     const bool wn = norm_out != nullptr, wd = dot_out != nullptr;
     switch (epilogue) {
         case EPI_APPLY:
             if (wn || wd) { set_error("poms_op_run_reduce: apply has no reductions"); return 1; }
-            if (op_run(op, EPI_APPLY, 0.0, x, y, nullptr, zb, ze, 0, stream)) return 1;
+            if (op_run(op, EPI_APPLY, 0.0, x, y, nullptr, zb, ze, 0, stream, 0, zb2, ze2)) return 1;
             break;
         case EPI_RESID:
             if (wn || wd) { set_error("poms_op_run_reduce: residual has no reductions"); return 1; }
-            if (op_run(op, EPI_RESID, 0.0, x, y, b, zb, ze, 0, stream)) return 1;
+            if (op_run(op, EPI_RESID, 0.0, x, y, b, zb, ze, 0, stream, 0, zb2, ze2)) return 1;
             break;
         case EPI_JACOBI:
             if (x == y) { set_error("jacobi sweep: x_out must not alias x_in"); return 1; }
-            if (op_run(op, EPI_JACOBI, omega, x, y, b, zb, ze, wn ? 1 : 0, stream, wd ? 1 : 0)) return 1;
+            if (op_run(op, EPI_JACOBI, omega, x, y, b, zb, ze, wn ? 1 : 0, stream, wd ? 1 : 0, zb2, ze2)) return 1;
             break;
         case EPI_JACOBI0:   // x = b: norm_out <- ||dr_2||^2, dot_out <- ||x1||^2
             if (op->ndim != 3) { set_error("jacobi from zero: 3D operators only"); return 1; }
             if (b == y) { set_error("jacobi from zero: x_out must not alias b"); return 1; }
             if (wn != wd) { set_error("jacobi from zero: both norms or neither"); return 1; }
-            if (op_run(op, EPI_JACOBI0, omega, b, y, b, zb, ze, wn ? 1 : 0, stream, wn ? 1 : 0)) return 1;
+            if (op_run(op, EPI_JACOBI0, omega, b, y, b, zb, ze, wn ? 1 : 0, stream, wn ? 1 : 0, zb2, ze2)) return 1;
             break;
         case EPI_APPLYDOT:
             if (x == y) { set_error("apply: y must not alias x"); return 1; }
             if (wn || !wd) { set_error("apply + dot: dot_out only"); return 1; }
-            if (op_run(op, EPI_APPLYDOT, 0.0, x, y, x, zb, ze, 0, stream, 1)) return 1;
+            if (op_run(op, EPI_APPLYDOT, 0.0, x, y, x, zb, ze, 0, stream, 1, zb2, ze2)) return 1;
             break;
         default:
             set_error("poms_op_run_reduce: bad epilogue");
@@ -587,6 +597,12 @@ int poms_op_run_reduce(poms_op* op, int epilogue, double omega, const double* x,
     if (wd) reduce_launch(op->ctx->scratch + n, (int)n, dot_out, as_stream(stream), accumulate);
     POMS_HIP_CHECK(hipGetLastError());
     return 0;
+}
+
+int poms_op_run_reduce(poms_op* op, int epilogue, double omega, const double* x, double* y,
+                       const double* b, int64_t zb, int64_t ze, double* norm_out, double* dot_out,
+                       int accumulate, void* stream) {
+    return poms_op_run_reduce2(op, epilogue, omega, x, y, b, zb, ze, 0, 0, norm_out, dot_out, accumulate, stream);
 }
 
 // Async copy of `count` doubles from device memory to (pinned) host memory.

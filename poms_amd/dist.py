@@ -15,6 +15,8 @@ the first ``n % w`` ranks get one extra plane (515 = 3x65 + 5x64).
 """
 from __future__ import annotations
 
+import os
+import warnings
 from dataclasses import dataclass
 
 import torch
@@ -47,6 +49,7 @@ class SlabDistribution:
     def __post_init__(self):
         if self.device_reductions is None:
             self.device_reductions = self.cuda_transport
+        self.native = None   # poms_comm handle (NativeComm) when the RCCL path is native
         self.start, self.end = slab_bounds(self.n0_global, self.world, self.rank)
         if self.end <= self.start:
             raise ValueError(f"rank {self.rank} owns no planes ({self.n0_global} over {self.world})")
@@ -62,8 +65,11 @@ class SlabDistribution:
                            ) -> "SlabDistribution":
         import torch.distributed as dist
         backend = dist.get_backend(group)
-        return cls(n0_global, dist.get_rank(group), dist.get_world_size(group), group,
-                   cuda_transport=(backend == "nccl"), device_reductions=device_reductions)
+        d = cls(n0_global, dist.get_rank(group), dist.get_world_size(group), group,
+                cuda_transport=(backend == "nccl"), device_reductions=device_reductions)
+        if backend == "nccl" and d.world > 1 and os.environ.get("POMS_NATIVE_COMM", "1") != "0":
+            d.native = NativeComm.create(group)
+        return d
 
     # ------------------------------------------------------------------
     def start_exchange(self, data: torch.Tensor, width: int, pad: int):
@@ -83,6 +89,12 @@ class SlabDistribution:
         n = self.n_local
         if n < width:
             raise ValueError(f"slab of {n} planes is thinner than the ghost width {width}")
+        if self.native is not None:
+            from . import runtime as rt
+            # ranks of the native communicator are the group's ranks
+            self.native.halo_start(data, n, pad, width, -1 if self.prev is None else self.prev,
+                                   -1 if self.next is None else self.next, rt.stream_handle())
+            return ("native",)
         staged = not self.cuda_transport and data.device.type != "cpu"
         buf = data.cpu() if staged else data
         ops, recv_views = [], []
@@ -106,6 +118,10 @@ class SlabDistribution:
     def finish_exchange(self, handle) -> None:
         if handle is None:
             return
+        if handle[0] == "native":
+            from . import runtime as rt
+            self.native.halo_finish(rt.stream_handle())
+            return
         works, staged, data, recv_views = handle
         for w in works:
             w.wait()
@@ -121,3 +137,131 @@ class SlabDistribution:
             return r
         import torch.distributed as dist
         return dist.get_global_rank(self.group, r)
+
+
+class NativeComm:
+    """The library's own RCCL communicator over the process group's ranks
+    (``poms_comm_*``, ``csrc/comm.hip``): ghost exchanges and scalar all-reduces
+    cost the host one C call each instead of a torch.distributed round trip.
+
+    :meth:`create` runs a self-test (an all-reduce and a ghost exchange checked
+    against their known results) and returns None -- the torch.distributed path
+    is used -- if anything fails."""
+
+    def __init__(self, handle, device: int):
+        import ctypes as C
+        from . import _lib
+        self.h = handle
+        self.device = device
+        s = C.c_void_p()
+        _lib.call("poms_comm_stream", self.h, C.byref(s))
+        self.stream = torch.cuda.ExternalStream(s.value, device=torch.device("cuda", device))
+
+    @classmethod
+    def create(cls, group=None):
+        import ctypes as C
+        import torch.distributed as dist
+        from . import _lib
+        try:
+            dev = torch.cuda.current_device()
+            nb = _lib.lib.poms_comm_id_bytes()
+            obj = [None]
+            if dist.get_rank(group) == 0:
+                buf = C.create_string_buffer(nb)
+                _lib.call("poms_comm_unique_id", buf, nb)
+                obj[0] = bytes(buf.raw[:nb])
+            dist.broadcast_object_list(obj, src=dist.get_global_rank(group, 0) if group is not None else 0,
+                                       group=group)
+            h = C.c_void_p()
+            _lib.call("poms_comm_create", dev, C.c_char_p(obj[0]), dist.get_rank(group),
+                      dist.get_world_size(group), C.byref(h))
+            comm = cls(h, dev)
+            ok = comm._self_test(dist.get_rank(group), dist.get_world_size(group))
+        except Exception as e:   # fall back to torch.distributed
+            warnings.warn(f"native RCCL communicator unavailable ({e!r}); using torch.distributed")
+            return None
+        oks = torch.tensor([1.0 if ok else 0.0], dtype=torch.float64, device=f"cuda:{dev}")
+        dist.all_reduce(oks, op=dist.ReduceOp.MIN, group=group)
+        if float(oks.item()) < 1.0:
+            warnings.warn("native RCCL communicator failed its self-test; using torch.distributed")
+            return None
+        return comm
+
+    def _self_test(self, rank: int, world: int) -> bool:
+        from . import runtime as rt
+        dev = f"cuda:{self.device}"
+        t = torch.full((2,), float(rank + 1), dtype=torch.float64, device=dev)
+        self.allreduce(t, rt.stream_handle(), wait_back=True)
+        if not torch.allclose(t.cpu(), torch.full((2,), world * (world + 1) / 2.0, dtype=torch.float64)):
+            return False
+        pad, width, n_loc, pe = 2, 2, 3, 8
+        data = torch.zeros((n_loc + 2 * pad, pe), dtype=torch.float64, device=dev)
+        for i in range(n_loc):
+            data[pad + i] = 1000.0 * rank + i
+        prev = rank - 1 if rank > 0 else -1
+        nxt = rank + 1 if rank + 1 < world else -1
+        self.halo_start(data, n_loc, pad, width, prev, nxt, rt.stream_handle())
+        self.halo_finish(rt.stream_handle())
+        h = data.cpu()
+        for j in range(width):
+            lo = h[pad - width + j]   # planes n_loc-width+j of rank-1
+            hi = h[pad + n_loc + j]   # planes j of rank+1
+            if prev >= 0 and not bool((lo == 1000.0 * prev + (n_loc - width + j)).all()):
+                return False
+            if prev < 0 and bool(lo.any()):
+                return False
+            if nxt >= 0 and not bool((hi == 1000.0 * nxt + j).all()):
+                return False
+            if nxt < 0 and bool(hi.any()):
+                return False
+        return True
+
+    def halo_start(self, data: torch.Tensor, n_local: int, pad: int, width: int, prev: int, nxt: int, stream):
+        from . import _lib
+        import ctypes as C
+        _lib.call("poms_halo_start", self.h, C.c_void_p(data.data_ptr()), int(data.stride(0)), int(n_local),
+                  int(pad), int(width), int(prev), int(nxt), stream)
+
+    def halo_finish(self, stream):
+        from . import _lib
+        _lib.call("poms_halo_finish", self.h, stream)
+
+    def slot(self):
+        """(device address, ticket) of the next ring slot (2 doubles) for a lazily
+        read global sum."""
+        from . import _lib
+        import ctypes as C
+        p, t = C.c_void_p(), C.c_int()
+        _lib.call("poms_comm_slot", self.h, C.byref(p), C.byref(t))
+        return p.value, t.value
+
+    def to_host(self, ticket: int, count: int, host_slot: torch.Tensor, stream) -> "LazyNative":
+        """All-reduce ring slot ``ticket`` and copy it to ``host_slot`` (pinned) on the
+        communication stream; the returned object's ``value(i)`` waits for it."""
+        from . import _lib
+        import ctypes as C
+        _lib.call("poms_allreduce_to_host", self.h, int(ticket), int(count), C.c_void_p(host_slot.data_ptr()),
+                  stream)
+        return LazyNative(self, ticket, host_slot)
+
+    def allreduce(self, t: torch.Tensor, stream, wait_back: bool):
+        from . import _lib
+        import ctypes as C
+        _lib.call("poms_allreduce_sum", self.h, C.c_void_p(t.data_ptr()), int(t.numel()), stream,
+                  1 if wait_back else 0)
+
+
+class LazyNative:
+    """A global sum being all-reduced and copied to pinned memory on the native
+    communicator's stream (the LazyScalar interface)."""
+
+    def __init__(self, comm: NativeComm, ticket: int, host_slot: torch.Tensor):
+        self._comm, self._ticket, self._host = comm, ticket, host_slot
+        self._done = False
+
+    def value(self, i: int = 0) -> float:
+        if not self._done:
+            from . import _lib
+            _lib.call("poms_comm_wait", self._comm.h, self._ticket)
+            self._done = True
+        return float(self._host[i])

@@ -156,6 +156,14 @@ class StencilVectorSpace:
             src = partial_sums[0]
             return self._lazy_copy_raw(src)
         tot = torch.stack([ps.sum() for ps in partial_sums]) if len(partial_sums) > 1 else partial_sums[0].clone()
+        if self.is_distributed and self.dist.native is not None:
+            # native RCCL: all-reduce and the copy to pinned memory both on the
+            # communication stream; the launch stream never waits for them
+            nc = self.dist.native
+            nc.allreduce(tot, rt.stream_handle(), wait_back=False)
+            tot.record_stream(nc.stream)
+            with torch.cuda.stream(nc.stream):
+                return self._lazy_copy(tot)
         side = self._side_stream()
         side.wait_stream(torch.cuda.current_stream(tot.device))
         tot.record_stream(side)
@@ -164,6 +172,17 @@ class StencilVectorSpace:
                 import torch.distributed as dist
                 dist.all_reduce(tot, group=self.dist.group)
             return self._lazy_copy(tot)
+
+    def pinned_slots(self, k: int) -> torch.Tensor:
+        """k doubles of the pinned host ring (each use is read within a few sweeps)."""
+        if self._pinned is None:
+            self._pinned = torch.zeros(8, dtype=F64).pin_memory()
+            self._pin_next = 0
+        if self._pin_next + k > 8:
+            self._pin_next = 0
+        slot = self._pinned[self._pin_next:self._pin_next + k]
+        self._pin_next += k
+        return slot
 
     def _lazy_copy_raw(self, src: torch.Tensor) -> "LazyScalar":
         """hipMemcpyAsync of a (contiguous) device slice into the pinned ring, on the
@@ -193,10 +212,13 @@ class StencilVectorSpace:
     def device_sum(self, *partial_sums: torch.Tensor) -> torch.Tensor:
         """Global sums of device partial-sum slices as a device tensor (RCCL all-reduce
         across slabs on the device stream; nothing is read by the host)."""
-        tot = torch.stack([ps.sum() for ps in partial_sums])
+        tot = torch.stack([ps.sum() for ps in partial_sums]) if len(partial_sums) > 1 else partial_sums[0].clone()
         if self.is_distributed:
-            import torch.distributed as dist
-            dist.all_reduce(tot, group=self.dist.group)
+            if self.dist.native is not None:
+                self.dist.native.allreduce(tot, rt.stream_handle(), wait_back=True)
+            else:
+                import torch.distributed as dist
+                dist.all_reduce(tot, group=self.dist.group)
         return tot
 
     def lazy_value(self, dev: torch.Tensor) -> "LazyScalar":
@@ -531,7 +553,7 @@ class KronOperator:
         _lib.call("poms_op_create", V.ctx, 3 if nd == 3 else 2, C.byref(V.layout), cform, self.pmax,
                   farr, g0, n0g, C.byref(self._h))
         self.timer = None  # list -> (kind, start_event, end_event, call) per kernel launch
-        self._calls = 0    # operator calls (one call = 1 launch, or 3 when a halo exchange is overlapped)
+        self._calls = 0    # operator calls (one call = 1 launch, or 2 when a halo exchange is overlapped)
 
     # -- constructors ------------------------------------------------------------
     @classmethod
@@ -630,21 +652,22 @@ class KronOperator:
 
     def _run(self, kind: str, x: StencilVector, y: StencilVector, b: StencilVector | None = None,
              omega: float = 0.0, norm_out: torch.Tensor | None = None, dot_out: torch.Tensor | None = None):
-        """One operator call over all local planes (``poms_op_run_reduce``); with
+        """One operator call over all local planes (``poms_op_run_reduce2``); with
         stale ghosts in a slab decomposition the RCCL ghost exchange overlaps the
-        interior planes, and the p boundary planes on each side follow.  The
+        interior planes, and the p boundary planes on both sides follow in one launch.  The
         reductions of the launches accumulate into ``norm_out`` / ``dot_out``
         (device doubles)."""
         V = self.space
         n0 = V.local_npts[0] if V.ndim == 3 else 1
         st = _stream()
-        ranges = ((0, n0),)
+        ranges = ((0, n0, 0, 0),)
         handle = None
         if V.is_distributed and not x._ghost_valid:
             p0 = V.pads[0]
             handle = V.dist.start_exchange(V.planes(x._store), width=p0, pad=p0)
             if handle is not None and n0 > 2 * self.pmax:
-                ranges = ((self.pmax, n0 - self.pmax), (0, self.pmax), (n0 - self.pmax, n0))
+                # interior planes meanwhile, then both p-plane boundaries in one launch
+                ranges = ((self.pmax, n0 - self.pmax, 0, 0), (0, self.pmax, n0 - self.pmax, n0))
             else:
                 V.dist.finish_exchange(handle)
                 handle = None
@@ -652,16 +675,20 @@ class KronOperator:
         epi = self._EPI[kind]
         xp, yp = rt.ptr(x._data), rt.ptr(y._data)
         bp = rt.ptr(b._data) if b is not None else None
-        np_ = rt.ptr(norm_out) if norm_out is not None else None
-        dp = rt.ptr(dot_out) if dot_out is not None else None
-        for idx, (zb, ze) in enumerate(ranges):
+        def _p(v):   # device tensor, raw device address (int) or None
+            if v is None:
+                return None
+            return rt.ptr(v) if isinstance(v, torch.Tensor) else C.c_void_p(v)
+
+        np_, dp = _p(norm_out), _p(dot_out)
+        for idx, (zb, ze, zb2, ze2) in enumerate(ranges):
             if idx == 1 and handle is not None:
                 V.dist.finish_exchange(handle)
                 handle = None
             if self.timer is not None:
                 e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
                 e0.record()
-            _lib.call("poms_op_run_reduce", self._h, epi, float(omega), xp, yp, bp, zb, ze, np_, dp,
+            _lib.call("poms_op_run_reduce2", self._h, epi, float(omega), xp, yp, bp, zb, ze, zb2, ze2, np_, dp,
                       1 if idx else 0, st)
             if self.timer is not None:
                 e1.record()
@@ -734,6 +761,13 @@ class KronOperator:
             raise ValueError("x_out must not alias x_in")
         V = self.space
         nb = V.scalar_buffer()
+        if lazy and want_norm and not want_dot and V.is_distributed and V.dist.native is not None:
+            # native RCCL: reduce into a ring slot, all-reduce + copy on the comm stream
+            nc = V.dist.native
+            slot, ticket = nc.slot()
+            self._run("jacobi", x_in, x_out, b=b, omega=omega, norm_out=slot)
+            x_out._mark_written()
+            return nc.to_host(ticket, 1, V.pinned_slots(1), rt.stream_handle())
         self._run("jacobi", x_in, x_out, b=b, omega=omega, norm_out=nb[0:1] if want_norm else None,
                   dot_out=nb[4:5] if want_dot else None)
         x_out._mark_written()
@@ -767,6 +801,12 @@ class KronOperator:
             raise ValueError("x_out must not alias b")
         V = self.space
         nb = V.scalar_buffer()
+        if lazy and want_norm and V.is_distributed and V.dist.native is not None:
+            nc = V.dist.native
+            slot, ticket = nc.slot()
+            self._run("jacobi2", b, x_out, b=b, omega=omega, norm_out=slot + 8, dot_out=slot)
+            x_out._mark_written()
+            return nc.to_host(ticket, 2, V.pinned_slots(2), rt.stream_handle())
         # norm_out <- ||dr_2||^2 (slot 1), dot_out <- ||x1||^2 (slot 0): adjacent, one copy
         self._run("jacobi2", b, x_out, b=b, omega=omega, norm_out=nb[1:2] if want_norm else None,
                   dot_out=nb[0:1] if want_norm else None)

@@ -287,3 +287,98 @@ def test_aligned_layout_and_tile_cols(gpu, p, cells, variant, tile_cols):
     for k in range(3):
         assert rel(out[True][k], out[False][k]) <= 1e-14, k
     assert abs(out[True][3] - out[False][3]) <= 1e-12 * abs(out[False][3])
+
+
+@pytest.mark.gpu
+def test_native_comm_single_rank(gpu):
+    """poms_comm_* on a one-rank RCCL communicator: the all-reduce is the identity,
+    a ghost exchange without neighbours is a no-op, the streams stay ordered."""
+    import ctypes as C
+    import torch
+    from poms_amd import _lib
+    from poms_amd.dist import NativeComm
+    from poms_amd import runtime as rt
+    nb = _lib.lib.poms_comm_id_bytes()
+    buf = C.create_string_buffer(nb)
+    _lib.call("poms_comm_unique_id", buf, nb)
+    h = C.c_void_p()
+    _lib.call("poms_comm_create", 0, C.c_char_p(bytes(buf.raw[:nb])), 0, 1, C.byref(h))
+    try:
+        nc = NativeComm(h, 0)
+        t = torch.arange(5, dtype=torch.float64, device=gpu) + 0.5
+        nc.allreduce(t, rt.stream_handle(), wait_back=True)
+        assert torch.equal(t.cpu(), torch.arange(5, dtype=torch.float64) + 0.5)
+        assert nc._self_test(0, 1)
+        # result ready on the communication stream only (wait_back = False)
+        u = torch.full((3,), 2.0, dtype=torch.float64, device=gpu)
+        nc.allreduce(u, rt.stream_handle(), wait_back=False)
+        nc.stream.synchronize()
+        assert torch.equal(u.cpu(), torch.full((3,), 2.0, dtype=torch.float64))
+    finally:
+        _lib.call("poms_comm_destroy", h)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("variant", [9, 10])
+def test_two_range_launch(gpu, variant):
+    """poms_op_run_reduce2: interior planes, then both p-plane boundaries in ONE launch
+    (the overlapped slab schedule) == one launch over all planes, norms included."""
+    import torch
+    from poms_amd import _lib, runtime as rt
+    from poms_amd.stencil import KronOperator
+    p, cells = 3, (20, 18, 70)
+    F = [assemble_1d(uniform_knots(p, N), p) for N in cells]
+    n = [N + p for N in cells]
+    V = _space(n, [p] * 3)
+    A = KronOperator.laplace(V, [f[0] for f in F], [f[1] for f in F])
+    A.set_variant(variant)
+    rng = np.random.default_rng(21)
+    x, b = V.zeros().from_numpy(rng.standard_normal(n)), V.zeros().from_numpy(rng.standard_normal(n))
+    y1, y2 = V.zeros(), V.zeros()
+    nb = torch.zeros(8, dtype=torch.float64, device=gpu)
+    st = rt.stream_handle()
+    n0 = n[0]
+    for kind, epi in (("apply", 0), ("jacobi", 2)):
+        wn = epi == 2
+        _lib.call("poms_op_run_reduce2", A._h, epi, 2.0 / 3.0, rt.ptr(x._data), rt.ptr(y1._data), rt.ptr(b._data),
+                  0, n0, 0, 0, rt.ptr(nb[0:1]) if wn else None, None, 0, st)
+        _lib.call("poms_op_run_reduce2", A._h, epi, 2.0 / 3.0, rt.ptr(x._data), rt.ptr(y2._data), rt.ptr(b._data),
+                  p, n0 - p, 0, 0, rt.ptr(nb[1:2]) if wn else None, None, 0, st)
+        _lib.call("poms_op_run_reduce2", A._h, epi, 2.0 / 3.0, rt.ptr(x._data), rt.ptr(y2._data), rt.ptr(b._data),
+                  0, p, n0 - p, n0, rt.ptr(nb[1:2]) if wn else None, None, 1, st)
+        np.testing.assert_array_equal(y1.to_local_numpy(), y2.to_local_numpy())
+        if wn:
+            h = nb.cpu()
+            assert abs(float(h[0]) - float(h[1])) <= 1e-13 * abs(float(h[0])), kind
+
+
+@pytest.mark.gpu
+def test_native_comm_lazy_slot(gpu):
+    """The native ring slot path of a lazily read norm (one rank): the sweep reduces
+    into the slot, poms_allreduce_to_host copies it, value() waits for it."""
+    import ctypes as C
+    from poms_amd import _lib, runtime as rt
+    from poms_amd.dist import NativeComm
+    from poms_amd.stencil import KronOperator
+    nbytes = _lib.lib.poms_comm_id_bytes()
+    buf = C.create_string_buffer(nbytes)
+    _lib.call("poms_comm_unique_id", buf, nbytes)
+    h = C.c_void_p()
+    _lib.call("poms_comm_create", 0, C.c_char_p(bytes(buf.raw[:nbytes])), 0, 1, C.byref(h))
+    try:
+        nc = NativeComm(h, 0)
+        p, cells = 3, (12, 14, 40)
+        F = [assemble_1d(uniform_knots(p, N), p) for N in cells]
+        n = [N + p for N in cells]
+        V = _space(n, [p] * 3)
+        A = KronOperator.laplace(V, [f[0] for f in F], [f[1] for f in F])
+        rng = np.random.default_rng(5)
+        x, b = V.zeros().from_numpy(rng.standard_normal(n)), V.zeros().from_numpy(rng.standard_normal(n))
+        ref = A.jacobi_sweep(b, x, V.zeros(), 2.0 / 3.0, want_norm=True)
+        for _ in range(20):   # wraps the 16-slot ring
+            slot, ticket = nc.slot()
+            A._run("jacobi", x, V.zeros(), b=b, omega=2.0 / 3.0, norm_out=slot)
+            lz = nc.to_host(ticket, 1, V.pinned_slots(1), rt.stream_handle())
+            assert abs(lz.value() - ref) <= 1e-13 * ref
+    finally:
+        _lib.call("poms_comm_destroy", h)
