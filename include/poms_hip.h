@@ -295,6 +295,17 @@ int poms_allreduce_sum(poms_comm* comm, double* buf, int64_t count, void* stream
 int poms_comm_slot(poms_comm* comm, double** dev_slot, int* ticket);
 int poms_allreduce_to_host(poms_comm* comm, int ticket, int count, double* host_dst, void* stream);
 int poms_comm_wait(poms_comm* comm, int ticket);
+/* One distributed operator call (epilogue as poms_op_run_reduce2) from one host
+ * call: with `exchange` the p-plane ghost exchange of x (xplanes = plane 0 of its
+ * padded array) overlaps the interior planes and both boundaries follow in one
+ * launch.  Reductions go to norm_dev / dot_dev (device, local sums), or with
+ * lazy_count > 0 to a ring slot all-reduced and copied to host_dst on the
+ * communication stream ([dot, norm] with both; *ticket for poms_comm_wait).   */
+int poms_op_run_dist(poms_op* op, poms_comm* comm, int epilogue, double omega, const double* x,
+                     double* y, const double* b, double* xplanes, int64_t plane_elems,
+                     int64_t n_local, int pad, int pmax, int prev, int next, int exchange,
+                     int want_norm, int want_dot, double* norm_dev, double* dot_dev,
+                     int lazy_count, double* host_dst, int* ticket, void* stream);
 
 #ifdef __cplusplus
 }

@@ -74,6 +74,8 @@ _SIGS = {
     "poms_comm_slot": [_vp, _pp, C.POINTER(_i)],
     "poms_allreduce_to_host": [_vp, _i, _i, _vp, _vp],
     "poms_comm_wait": [_vp, _i],
+    "poms_op_run_dist": [_vp, _vp, _i, _d, _vp, _vp, _vp, _vp, _i64, _i64, _i, _i, _i, _i, _i, _i, _i, _vp, _vp,
+                         _i, _vp, C.POINTER(_i), _vp],
     "poms_copy_to_host_async": [_vp, _vp, _vp, _i64, _vp],
     "poms_pcg_r_update_dev": [_vp, _LP, _vp, _vp, _vp, _vp, _vp],
     "poms_pcg_xp_update_dev": [_vp, _LP, _vp, _vp, _vp, _vp, _vp],

@@ -199,6 +199,52 @@ int poms_allreduce_to_host(poms_comm* c, int ticket, int count, double* host_dst
     return 0;
 }
 
+// One distributed operator call from a single host call: with `exchange` the
+// ghost exchange of x starts, the interior planes [p, n_local - p) run meanwhile,
+// then both p-plane boundaries in one launch after the exchange; otherwise one
+// launch over all planes.  Reductions (as poms_op_run_reduce2) go to norm_dev /
+// dot_dev, or -- lazy_count > 0 -- to a ring slot that is all-reduced and copied
+// to host_dst on the communication stream (*ticket for poms_comm_wait; lazy
+// order in the slot: [dot, norm] with both, else the one asked for).
+int poms_op_run_dist(poms_op* op, poms_comm* c, int epilogue, double omega, const double* x, double* y,
+                     const double* b, double* xplanes, int64_t plane_elems, int64_t n_local, int pad, int pmax,
+                     int prev, int next, int exchange, int want_norm, int want_dot, double* norm_dev,
+                     double* dot_dev, int lazy_count, double* host_dst, int* ticket, void* stream) {
+    if (!op || !c) { set_error("poms_op_run_dist: null argument"); return 1; }
+    double *nout = want_norm ? norm_dev : nullptr, *dout = want_dot ? dot_dev : nullptr;
+    int t = -1;
+    if (lazy_count > 0) {
+        if (!host_dst || !ticket || lazy_count != (want_norm ? 1 : 0) + (want_dot ? 1 : 0)) {
+            set_error("poms_op_run_dist: bad lazy request");
+            return 1;
+        }
+        double* slot = nullptr;
+        if (poms_comm_slot(c, &slot, &t)) return 1;
+        dout = want_dot ? slot : nullptr;
+        nout = want_norm ? slot + (want_dot ? 1 : 0) : nullptr;
+    }
+    if (exchange && n_local > 2 * pmax) {
+        if (poms_halo_start(c, xplanes, plane_elems, n_local, pad, pmax, prev, next, stream)) return 1;
+        if (poms_op_run_reduce2(op, epilogue, omega, x, y, b, pmax, n_local - pmax, 0, 0, nout, dout, 0, stream))
+            return 1;
+        if (poms_halo_finish(c, stream)) return 1;
+        if (poms_op_run_reduce2(op, epilogue, omega, x, y, b, 0, pmax, n_local - pmax, n_local, nout, dout, 1,
+                                stream))
+            return 1;
+    } else {
+        if (exchange) {
+            if (poms_halo_start(c, xplanes, plane_elems, n_local, pad, pmax, prev, next, stream)) return 1;
+            if (poms_halo_finish(c, stream)) return 1;
+        }
+        if (poms_op_run_reduce2(op, epilogue, omega, x, y, b, 0, n_local, 0, 0, nout, dout, 0, stream)) return 1;
+    }
+    if (lazy_count > 0) {
+        if (poms_allreduce_to_host(c, t, lazy_count, host_dst, stream)) return 1;
+        *ticket = t;
+    }
+    return 0;
+}
+
 int poms_comm_wait(poms_comm* c, int ticket) {
     if (!c || ticket < 0 || ticket >= poms_comm::kRing) { set_error("poms_comm_wait: bad argument"); return 1; }
     POMS_HIP_CHECK(hipEventSynchronize(c->ring_ev[ticket]));

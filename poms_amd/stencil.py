@@ -658,6 +658,9 @@ class KronOperator:
         reductions of the launches accumulate into ``norm_out`` / ``dot_out``
         (device doubles)."""
         V = self.space
+        if V.is_distributed and V.dist.native is not None:
+            self._run_native(kind, x, y, b, omega, norm_out, dot_out)
+            return
         n0 = V.local_npts[0] if V.ndim == 3 else 1
         st = _stream()
         ranges = ((0, n0, 0, 0),)
@@ -696,6 +699,40 @@ class KronOperator:
         if handle is not None:
             V.dist.finish_exchange(handle)
         x._ghost_valid = True
+
+    def _run_native(self, kind, x, y, b=None, omega=0.0, norm_out=None, dot_out=None, lazy_count=0,
+                    host_dst=None):
+        """The distributed call through the native communicator: exchange (if x's
+        ghosts are stale), interior, both boundaries and the reductions in ONE host
+        call (``poms_op_run_dist``).  With ``lazy_count`` returns the ticket of the
+        all-reduced values being copied to ``host_dst``."""
+        V = self.space
+        d = V.dist
+        st = _stream()
+        self._calls += 1
+
+        def _p(v):
+            if v is None:
+                return None
+            return rt.ptr(v) if isinstance(v, torch.Tensor) else C.c_void_p(v)
+
+        tk = C.c_int(-1)
+        if self.timer is not None:   # per call: includes the wait for the exchange
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record()
+        _lib.call("poms_op_run_dist", self._h, d.native.h, self._EPI[kind], float(omega), rt.ptr(x._data),
+                  rt.ptr(y._data), rt.ptr(b._data) if b is not None else None,
+                  C.c_void_p(V.planes(x._store).data_ptr()), V.plane_elems, V.local_npts[0], V.pads[0],
+                  self.pmax, -1 if d.prev is None else d.prev, -1 if d.next is None else d.next,
+                  0 if x._ghost_valid else 1, 1 if (norm_out is not None or (lazy_count and kind != "apply_dot"))
+                  else 0, 1 if (dot_out is not None or (lazy_count == 2)) else 0, _p(norm_out), _p(dot_out),
+                  int(lazy_count), C.c_void_p(host_dst.data_ptr()) if host_dst is not None else None,
+                  C.byref(tk), st)
+        if self.timer is not None:
+            e1.record()
+            self.timer.append((kind, e0, e1, self._calls))
+        x._ghost_valid = True
+        return tk.value
 
     def dot(self, x: StencilVector, out: StencilVector | None = None) -> StencilVector:
         """y = A x (spl ``StencilMatrix.dot``)."""
@@ -763,11 +800,11 @@ class KronOperator:
         nb = V.scalar_buffer()
         if lazy and want_norm and not want_dot and V.is_distributed and V.dist.native is not None:
             # native RCCL: reduce into a ring slot, all-reduce + copy on the comm stream
-            nc = V.dist.native
-            slot, ticket = nc.slot()
-            self._run("jacobi", x_in, x_out, b=b, omega=omega, norm_out=slot)
+            from .dist import LazyNative
+            host = V.pinned_slots(1)
+            ticket = self._run_native("jacobi", x_in, x_out, b, omega, lazy_count=1, host_dst=host)
             x_out._mark_written()
-            return nc.to_host(ticket, 1, V.pinned_slots(1), rt.stream_handle())
+            return LazyNative(V.dist.native, ticket, host)
         self._run("jacobi", x_in, x_out, b=b, omega=omega, norm_out=nb[0:1] if want_norm else None,
                   dot_out=nb[4:5] if want_dot else None)
         x_out._mark_written()
@@ -802,11 +839,11 @@ class KronOperator:
         V = self.space
         nb = V.scalar_buffer()
         if lazy and want_norm and V.is_distributed and V.dist.native is not None:
-            nc = V.dist.native
-            slot, ticket = nc.slot()
-            self._run("jacobi2", b, x_out, b=b, omega=omega, norm_out=slot + 8, dot_out=slot)
+            from .dist import LazyNative
+            host = V.pinned_slots(2)   # [||x1||^2, ||dr_2||^2]
+            ticket = self._run_native("jacobi2", b, x_out, b, omega, lazy_count=2, host_dst=host)
             x_out._mark_written()
-            return nc.to_host(ticket, 2, V.pinned_slots(2), rt.stream_handle())
+            return LazyNative(V.dist.native, ticket, host)
         # norm_out <- ||dr_2||^2 (slot 1), dot_out <- ||x1||^2 (slot 0): adjacent, one copy
         self._run("jacobi2", b, x_out, b=b, omega=omega, norm_out=nb[1:2] if want_norm else None,
                   dot_out=nb[0:1] if want_norm else None)

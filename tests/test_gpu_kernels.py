@@ -382,3 +382,45 @@ def test_native_comm_lazy_slot(gpu):
             assert abs(lz.value() - ref) <= 1e-13 * ref
     finally:
         _lib.call("poms_comm_destroy", h)
+
+
+@pytest.mark.gpu
+def test_native_run_dist_single_rank(gpu):
+    """poms_op_run_dist on a one-rank communicator (no neighbours): the overlapped
+    schedule (interior, then both boundaries) and its device / lazy reductions equal
+    one plain launch."""
+    import ctypes as C
+    import torch
+    from poms_amd import _lib, runtime as rt
+    from poms_amd.dist import LazyNative, NativeComm
+    from poms_amd.stencil import KronOperator
+    nbytes = _lib.lib.poms_comm_id_bytes()
+    buf = C.create_string_buffer(nbytes)
+    _lib.call("poms_comm_unique_id", buf, nbytes)
+    h = C.c_void_p()
+    _lib.call("poms_comm_create", 0, C.c_char_p(bytes(buf.raw[:nbytes])), 0, 1, C.byref(h))
+    try:
+        nc = NativeComm(h, 0)
+        p, cells = 3, (21, 14, 40)
+        F = [assemble_1d(uniform_knots(p, N), p) for N in cells]
+        n = [N + p for N in cells]
+        V = _space(n, [p] * 3)
+        A = KronOperator.laplace(V, [f[0] for f in F], [f[1] for f in F])
+        rng = np.random.default_rng(6)
+        x, b = V.zeros().from_numpy(rng.standard_normal(n)), V.zeros().from_numpy(rng.standard_normal(n))
+        y_ref = V.zeros()
+        ref = A.jacobi_sweep(b, x, y_ref, 2.0 / 3.0, want_norm=True)
+        dev = torch.zeros(2, dtype=torch.float64, device=gpu)
+        for lazy in (0, 1):
+            y = V.zeros()
+            host = V.pinned_slots(1)
+            tk = C.c_int(-1)
+            _lib.call("poms_op_run_dist", A._h, nc.h, 2, 2.0 / 3.0, rt.ptr(x._data), rt.ptr(y._data), rt.ptr(b._data),
+                      C.c_void_p(V.planes(x._store).data_ptr()), V.plane_elems, V.local_npts[0], V.pads[0], p,
+                      -1, -1, 1, 1, 0, None if lazy else rt.ptr(dev[0:1]), None, lazy,
+                      C.c_void_p(host.data_ptr()) if lazy else None, C.byref(tk), rt.stream_handle())
+            np.testing.assert_array_equal(y.to_local_numpy(), y_ref.to_local_numpy())
+            got = LazyNative(nc, tk.value, host).value() if lazy else float(dev[0].item())
+            assert abs(got - ref) <= 1e-13 * ref, lazy
+    finally:
+        _lib.call("poms_comm_destroy", h)
