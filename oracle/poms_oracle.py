@@ -245,3 +245,52 @@ def vcycle_two_level(M, K, P1, b, c=1.0, tol=1e-6, maxiter=10, x0=None, reorder=
     xf = xf + P @ xc
     xf2, info_pos = pcg(apply, psolve, bf, x0=xf, tol=tol, maxiter=maxiter)
     return xf2.reshape(b.shape), info_pre, info_pos
+
+
+def vcycle_multilevel(Ms, Ks, P1s, b, c=1.0, tol=1e-6, maxiters=None, x0=None, reorder=False):
+    """Recursive V-cycle over L levels (the reference's
+    two-level cycle `sources/mg_jac.py:84-119` applied at every level).
+
+    Level 0 is the finest.  ``Ms[l]``, ``Ks[l]``: per-axis band factors of level
+    l (used on level 0 only: coarser operators are the materialised Galerkin
+    products R A P, as in the reference); ``P1s[l]``: 1D prolongation from level
+    l+1 to level l.  ``maxiters[l]``: pcg iterations of the pre / post smoothing
+    on level l (default 10, the reference's).  The coarsest level is solved with
+    ``splu``.  Returns ``(x, infos)`` with ``infos[l] = (info_pre, info_post)``
+    of the first visit of level l.
+    """
+    L = len(P1s) + 1
+    nd = b.ndim
+    maxiters = [10] * (L - 1) if maxiters is None else list(maxiters)
+    A0 = kron_sum_csr(Ms[0], Ks[0], c)
+    As, Ps = [A0], []
+    for l in range(L - 1):
+        Pm = sp.csr_matrix(P1s[l])
+        P = Pm
+        for _ in range(nd - 1):
+            P = sp.kron(P, Pm, format="csr")
+        Ps.append(P)
+        As.append((P.T @ As[l] @ P).tocsr())
+    infos = [None] * (L - 1)
+
+    def cycle(l, bl, xl0):
+        if l == L - 1:
+            return splu(As[l].tocsc()).solve(bl)
+        A = As[l]
+        D = A.diagonal().copy()
+        if l == 0 and reorder:
+            apply = lambda v: kron_sum_apply(v.reshape(b.shape), Ms[0], Ks[0], c).reshape(-1)
+        else:
+            apply = lambda v: A @ v
+        psolve = lambda r: damped_jacobi(apply, D, r)
+        x, ipre = pcg(apply, psolve, bl, x0=xl0, tol=tol, maxiter=maxiters[l])
+        rc = Ps[l].T @ (bl - apply(x))
+        ec = cycle(l + 1, rc, None)
+        x = x + Ps[l] @ ec
+        x, ipos = pcg(apply, psolve, bl, x0=x, tol=tol, maxiter=maxiters[l])
+        if infos[l] is None:
+            infos[l] = (ipre, ipos)
+        return x
+
+    x = cycle(0, b.reshape(-1), None if x0 is None else x0.reshape(-1))
+    return x.reshape(b.shape), infos

@@ -40,6 +40,8 @@ int diag_scale_launch(bool is3d, int form, const RowGeom& g, int P, int g0, doub
 int dense_matvec_launch(int n, const double* M, const double* x, double* y, hipStream_t st);
 int transfer_pass_launch(bool restrict_dir, int ncm, const AxisPass& ps, const double* Pm,
                          const double* in, double* out, hipStream_t st);
+int transfer_band_launch(bool restrict_dir, const AxisPass& ps, const double* band, const int* lo, int w,
+                         const double* in, double* out, hipStream_t st);
 
 enum { V_AXPBY = 0, V_SCALE = 1, V_FILL = 2, V_DOT = 3, V_PCGUPD = 4, V_RUPD = 5, V_XPUPD = 6 };
 constexpr int64_t kScratch = 1 << 16;
@@ -110,6 +112,11 @@ struct poms_transfer {
     int64_t g0 = 0;
     int64_t nf[3]{}, nc[3]{};
     double* Pm[3]{};
+    // banded form (coarse extent > 32): rows of P (Pb, jlo, wP) and of P^T (Rb, ilo, wR)
+    bool banded = false;
+    double *Pb[3]{}, *Rb[3]{};
+    int *jlo[3]{}, *ilo[3]{};
+    int wP[3]{}, wR[3]{};
     double *t0 = nullptr, *t1 = nullptr;
 };
 
@@ -786,7 +793,6 @@ int poms_transfer_create(poms_ctx* ctx, int ndim, const poms_layout* fine, int64
         if (!P[d] || nc[d] < 1 || nf_global[d] < 1) { set_error("poms_transfer_create: bad axis"); return 1; }
         ncmax = std::max(ncmax, nc[d]);
     }
-    if (ncmax > 32) { set_error("poms_transfer_create: coarse extent > 32"); return 1; }
     if (!is3d && (fine->n[0] != 1 || fine->pads[0] != 0)) {
         set_error("poms_transfer_create: 1D/2D layouts need n[0]=1, pads[0]=0");
         return 1;
@@ -799,6 +805,7 @@ int poms_transfer_create(poms_ctx* ctx, int ndim, const poms_layout* fine, int64
     t->ctx = ctx;
     t->ndim = ndim;
     t->ncm = ncmax <= 16 ? 16 : 32;
+    t->banded = ncmax > 32;
     t->L = *fine;
     t->g0 = is3d ? g0 : 0;
     int rc = 0;
@@ -806,10 +813,46 @@ int poms_transfer_create(poms_ctx* ctx, int ndim, const poms_layout* fine, int64
         t->nf[d] = (d < d0) ? 1 : nf_global[d];
         t->nc[d] = (d < d0) ? 1 : nc[d];
         if (d < d0) continue;
-        std::vector<double> pm(t->nf[d] * t->ncm, 0.0);
-        for (int64_t i = 0; i < t->nf[d]; ++i)
-            for (int64_t j = 0; j < t->nc[d]; ++j) pm[i * t->ncm + j] = P[d][i * t->nc[d] + j];
-        rc |= upload(pm.data(), pm.size(), &t->Pm[d]);
+        if (!t->banded) {
+            std::vector<double> pm(t->nf[d] * t->ncm, 0.0);
+            for (int64_t i = 0; i < t->nf[d]; ++i)
+                for (int64_t j = 0; j < t->nc[d]; ++j) pm[i * t->ncm + j] = P[d][i * t->nc[d] + j];
+            rc |= upload(pm.data(), pm.size(), &t->Pm[d]);
+            continue;
+        }
+        // banded: non-zero span of every row of P and of every column
+        const int64_t nfd = t->nf[d], ncd = t->nc[d];
+        const double* Pd = P[d];
+        std::vector<int> jl(nfd, 0), il(ncd, 0);
+        int wp = 1, wr = 1;
+        for (int64_t i = 0; i < nfd; ++i) {
+            int64_t a = -1, b = -1;
+            for (int64_t j = 0; j < ncd; ++j)
+                if (Pd[i * ncd + j] != 0.0) { if (a < 0) a = j; b = j; }
+            jl[i] = a < 0 ? 0 : (int)a;
+            wp = std::max(wp, a < 0 ? 1 : (int)(b - a + 1));
+        }
+        for (int64_t j = 0; j < ncd; ++j) {
+            int64_t a = -1, b = -1;
+            for (int64_t i = 0; i < nfd; ++i)
+                if (Pd[i * ncd + j] != 0.0) { if (a < 0) a = i; b = i; }
+            il[j] = a < 0 ? 0 : (int)a;
+            wr = std::max(wr, a < 0 ? 1 : (int)(b - a + 1));
+        }
+        if (wp > 64 || wr > 256) { set_error("poms_transfer_create: prolongation is not banded"); rc = 1; break; }
+        std::vector<double> pb(nfd * wp, 0.0), rb(ncd * wr, 0.0);
+        for (int64_t i = 0; i < nfd; ++i)
+            for (int k = 0; k < wp && jl[i] + k < ncd; ++k) pb[i * wp + k] = Pd[i * ncd + jl[i] + k];
+        for (int64_t j = 0; j < ncd; ++j)
+            for (int k = 0; k < wr && il[j] + k < nfd; ++k) rb[j * wr + k] = Pd[(il[j] + k) * ncd + j];
+        t->wP[d] = wp;
+        t->wR[d] = wr;
+        rc |= upload(pb.data(), pb.size(), &t->Pb[d]);
+        rc |= upload(rb.data(), rb.size(), &t->Rb[d]);
+        if (!rc && hipMalloc(reinterpret_cast<void**>(&t->jlo[d]), nfd * sizeof(int)) != hipSuccess) rc = 1;
+        if (!rc && hipMalloc(reinterpret_cast<void**>(&t->ilo[d]), ncd * sizeof(int)) != hipSuccess) rc = 1;
+        if (!rc && hipMemcpy(t->jlo[d], jl.data(), nfd * sizeof(int), hipMemcpyHostToDevice) != hipSuccess) rc = 1;
+        if (!rc && hipMemcpy(t->ilo[d], il.data(), ncd * sizeof(int), hipMemcpyHostToDevice) != hipSuccess) rc = 1;
     }
     const int64_t n1 = fine->n[1], n2 = fine->n[2];
     const size_t sz0 = (size_t)t->nc[0] * n1 * n2;
@@ -827,10 +870,22 @@ int poms_transfer_create(poms_ctx* ctx, int ndim, const poms_layout* fine, int64
 
 int poms_transfer_destroy(poms_transfer* t) {
     if (!t) return 0;
-    for (double* p : {t->Pm[0], t->Pm[1], t->Pm[2], t->t0, t->t1})
+    for (double* p : {t->Pm[0], t->Pm[1], t->Pm[2], t->t0, t->t1, t->Pb[0], t->Pb[1], t->Pb[2], t->Rb[0],
+                      t->Rb[1], t->Rb[2]})
+        if (p) (void)hipFree(p);
+    for (int* p : {t->jlo[0], t->jlo[1], t->jlo[2], t->ilo[0], t->ilo[1], t->ilo[2]})
         if (p) (void)hipFree(p);
     delete t;
     return 0;
+}
+
+// one axis pass of a transfer: dense-P kernels for small coarse extents, banded
+// gather kernels otherwise
+static int tpass(const poms_transfer* t, bool restrict_dir, int d, const AxisPass& ps, const double* in,
+                 double* out, hipStream_t st) {
+    if (!t->banded) return transfer_pass_launch(restrict_dir, t->ncm, ps, t->Pm[d], in, out, st);
+    return restrict_dir ? transfer_band_launch(true, ps, t->Rb[d], t->ilo[d], t->wR[d], in, out, st)
+                        : transfer_band_launch(false, ps, t->Pb[d], t->jlo[d], t->wP[d], in, out, st);
 }
 
 int poms_restrict(poms_transfer* t, const double* fine, double* coarse, void* stream) {
@@ -848,7 +903,7 @@ int poms_restrict(poms_transfer* t, const double* fine, double* coarse, void* st
         a0.in_base = fbase; a0.in_sb1 = g.s1; a0.in_sb2 = 1; a0.in_si = g.s0;
         a0.out_sb1 = n2; a0.out_sb2 = 1; a0.out_si = n1 * n2;
         a0.nI = (int)n0; a0.nJ = (int)c0; a0.goff = (int)t->g0;
-        if (transfer_pass_launch(true, t->ncm, a0, t->Pm[0], fine, t->t0, st)) return 1;
+        if (tpass(t, true, 0, a0, fine, t->t0, st)) return 1;
         src1 = t->t0;
         a1.nA = c0; a1.nB1 = 1; a1.nB2 = n2;
         a1.in_base = 0; a1.in_sa = n1 * n2; a1.in_sb2 = 1; a1.in_si = n2;
@@ -859,13 +914,13 @@ int poms_restrict(poms_transfer* t, const double* fine, double* coarse, void* st
     }
     a1.out_sa = c1 * n2; a1.out_sb2 = 1; a1.out_si = n2;
     a1.nI = (int)n1; a1.nJ = (int)c1; a1.goff = 0;
-    if (transfer_pass_launch(true, t->ncm, a1, t->Pm[1], src1, t->t1, st)) return 1;
+    if (tpass(t, true, 1, a1, src1, t->t1, st)) return 1;
     AxisPass a2{};
     a2.nA = c0 * c1; a2.nB1 = 1; a2.nB2 = 1;
     a2.in_sa = n2; a2.in_si = 1;
     a2.out_sa = c2; a2.out_si = 1;
     a2.nI = (int)n2; a2.nJ = (int)c2; a2.goff = 0;
-    if (transfer_pass_launch(true, t->ncm, a2, t->Pm[2], t->t1, coarse, st)) return 1;
+    if (tpass(t, true, 2, a2, t->t1, coarse, st)) return 1;
     POMS_HIP_CHECK(hipGetLastError());
     return 0;
 }
@@ -882,7 +937,7 @@ int poms_prolong_add(poms_transfer* t, const double* coarse, double* fine, void*
     a2.nA = c0 * c1; a2.nB1 = 1; a2.nB2 = 1;
     a2.in_sa = c2; a2.in_si = 1; a2.nJ = (int)c2;
     a2.out_sa = n2; a2.out_si = 1; a2.nI = (int)n2; a2.goff = 0; a2.accumulate = 0;
-    if (transfer_pass_launch(false, t->ncm, a2, t->Pm[2], coarse, t->t1, st)) return 1;
+    if (tpass(t, false, 2, a2, coarse, t->t1, st)) return 1;
     // axis 1: t1 [c0][c1][n2] -> t0 [c0][n1][n2] (3D) or fine (2D, accumulate)
     AxisPass a1{};
     a1.nA = c0; a1.nB1 = 1; a1.nB2 = n2;
@@ -890,16 +945,16 @@ int poms_prolong_add(poms_transfer* t, const double* coarse, double* fine, void*
     a1.nI = (int)n1; a1.goff = 0;
     if (t->ndim == 3) {
         a1.out_sa = n1 * n2; a1.out_sb2 = 1; a1.out_si = n2; a1.accumulate = 0;
-        if (transfer_pass_launch(false, t->ncm, a1, t->Pm[1], t->t1, t->t0, st)) return 1;
+        if (tpass(t, false, 1, a1, t->t1, t->t0, st)) return 1;
         AxisPass a0{};
         a0.nA = 1; a0.nB1 = n1; a0.nB2 = n2;
         a0.in_sb1 = n2; a0.in_sb2 = 1; a0.in_si = n1 * n2; a0.nJ = (int)c0;
         a0.out_base = fbase; a0.out_sb1 = g.s1; a0.out_sb2 = 1; a0.out_si = g.s0;
         a0.nI = (int)n0; a0.goff = (int)t->g0; a0.accumulate = 1;
-        if (transfer_pass_launch(false, t->ncm, a0, t->Pm[0], t->t0, fine, st)) return 1;
+        if (tpass(t, false, 0, a0, t->t0, fine, st)) return 1;
     } else {
         a1.out_base = fbase; a1.out_sb2 = 1; a1.out_si = g.s1; a1.accumulate = 1;
-        if (transfer_pass_launch(false, t->ncm, a1, t->Pm[1], t->t1, fine, st)) return 1;
+        if (tpass(t, false, 1, a1, t->t1, fine, st)) return 1;
     }
     POMS_HIP_CHECK(hipGetLastError());
     return 0;

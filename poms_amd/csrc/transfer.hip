@@ -9,6 +9,7 @@
 // wave-uniform (scalar) rows of P (P is stored fine-row-major, padded to NCM
 // columns with zeros).  The dominant pass (axis 0 of the fine slab) streams the
 // fine vector once: 8 B/DOF for restriction, 16 B/DOF for prolong-add.
+// Coarse extents > 32 (multilevel hierarchies) use the banded gather kernels.
 #include "common.hpp"
 
 namespace poms {
@@ -65,6 +66,70 @@ prolong_pass_kernel(const AxisPass ps, const double* __restrict__ Pm,
         if (ps.accumulate) *o += s;
         else *o = s;
     }
+}
+
+// Banded gather form for large coarse extents (multilevel hierarchies, where P
+// is the dyadic knot-insertion matrix with a few non-zeros per row / column):
+// one thread per OUTPUT element, the fastest index (b2) on consecutive lanes.
+//   restrict: out[a][J][b] = sum_k Rb[J][k] in[a][ilo[J] + k - goff][b]  (local rows only)
+//   prolong : out[a][i][b] (+)= sum_k Pb[goff+i][k] in[a][jlo[goff+i] + k][b]
+__global__ void __launch_bounds__(256)
+restrict_band_kernel(const AxisPass ps, const double* __restrict__ Rb, const int* __restrict__ ilo, int wR,
+                     const double* __restrict__ in, double* __restrict__ out) {
+    const int64_t tid = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    const int64_t nout = ps.nA * ps.nJ * ps.nB1 * ps.nB2;
+    if (tid >= nout) return;
+    const int64_t b2 = tid % ps.nB2;
+    int64_t t = tid / ps.nB2;
+    const int64_t b1 = t % ps.nB1;
+    t /= ps.nB1;
+    const int J = (int)(t % ps.nJ);
+    const int64_t a = t / ps.nJ;
+    const double* src = in + ps.in_base + a * ps.in_sa + b1 * ps.in_sb1 + b2 * ps.in_sb2;
+    double s = 0.0;
+    const int i0 = ilo[J] - ps.goff;
+    for (int k = 0; k < wR; ++k) {
+        const int i = i0 + k;
+        if (i >= 0 && i < ps.nI) s = fma(Rb[(int64_t)J * wR + k], src[(int64_t)i * ps.in_si], s);
+    }
+    out[ps.out_base + a * ps.out_sa + b1 * ps.out_sb1 + b2 * ps.out_sb2 + (int64_t)J * ps.out_si] = s;
+}
+
+__global__ void __launch_bounds__(256)
+prolong_band_kernel(const AxisPass ps, const double* __restrict__ Pb, const int* __restrict__ jlo, int wP,
+                    const double* __restrict__ in, double* __restrict__ out) {
+    const int64_t tid = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    const int64_t nout = ps.nA * (int64_t)ps.nI * ps.nB1 * ps.nB2;
+    if (tid >= nout) return;
+    const int64_t b2 = tid % ps.nB2;
+    int64_t t = tid / ps.nB2;
+    const int64_t b1 = t % ps.nB1;
+    t /= ps.nB1;
+    const int i = (int)(t % ps.nI);
+    const int64_t a = t / ps.nI;
+    const double* src = in + ps.in_base + a * ps.in_sa + b1 * ps.in_sb1 + b2 * ps.in_sb2;
+    const int gi = ps.goff + i;
+    const int j0 = jlo[gi];
+    double s = 0.0;
+    for (int k = 0; k < wP; ++k) {
+        const int j = j0 + k;
+        if (j < ps.nJ) s = fma(Pb[(int64_t)gi * wP + k], src[(int64_t)j * ps.in_si], s);
+    }
+    double* o = out + ps.out_base + a * ps.out_sa + b1 * ps.out_sb1 + b2 * ps.out_sb2 + (int64_t)i * ps.out_si;
+    if (ps.accumulate) *o += s;
+    else *o = s;
+}
+
+int transfer_band_launch(bool restrict_dir, const AxisPass& ps, const double* band, const int* lo, int w,
+                         const double* in, double* out, hipStream_t st) {
+    const int64_t nout = ps.nA * (int64_t)(restrict_dir ? ps.nJ : ps.nI) * ps.nB1 * ps.nB2;
+    const int64_t nb = (nout + 255) / 256;
+    if (nb == 0) return 0;
+    if (restrict_dir)
+        hipLaunchKernelGGL(restrict_band_kernel, dim3((unsigned)nb), dim3(256), 0, st, ps, band, lo, w, in, out);
+    else
+        hipLaunchKernelGGL(prolong_band_kernel, dim3((unsigned)nb), dim3(256), 0, st, ps, band, lo, w, in, out);
+    return 0;
 }
 
 int transfer_pass_launch(bool restrict_dir, int ncm, const AxisPass& ps, const double* Pm,

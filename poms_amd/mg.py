@@ -127,3 +127,123 @@ class TwoLevelVCycle:
         xf.update_ghost_regions()
         xf2, info_pos = pcg(A, damped_jacobi, bf, x0=xf, tol=self.tol, maxiter=self.maxiter)
         return xf2, info_pre, info_pos
+
+
+class MultilevelVCycle:
+    """V-cycle over a hierarchy of nested uniform B-spline spaces (SURVEY §8f
+    rank 1: the reference's two-level cycle `sources/mg_jac.py:84-119` applied
+    recursively, with every level's operator, smoothing and transfers on the
+    device and a dense device solve on the coarsest level).
+
+    Level 0 has ``ncells_fine`` cells per axis; each coarser level halves the
+    cells (dyadic knot insertion, ``P1 = matrix_multi_stages``) down to
+    ``ncells_coarsest``.  Level operators are assembled on their own knots; for
+    nested spaces with exact quadrature that IS the Galerkin product R A P of
+    the reference (pinned by tests/test_splines.py and the oracle parity test).
+    Each level is smoothed by ``pcg(A_l, damped_jacobi, b_l, tol, maxiters[l])``
+    before and after the coarse correction, as the reference smooths its fine
+    level.  With ``dist`` the finest level is slab-decomposed; the restriction
+    to level 1 is all-reduced and the coarser levels are replicated on every
+    rank (their work is 1/8, 1/64, ... of the finest level's).
+    """
+
+    def __init__(self, p: int, ncells_fine: int, ncells_coarsest: int = 8, ndim: int = 3, *,
+                 dist=None, mass_coef: float = 1.0, device=None, tol: float = 1e-6, maxiters=None,
+                 align: bool = True, chunk: int = 0):
+        if ncells_fine < ncells_coarsest or ncells_coarsest < 1:
+            raise ValueError("need ncells_fine >= ncells_coarsest >= 1")
+        self.p, self.ndim, self.tol = int(p), int(ndim), tol
+        cells = [int(ncells_fine)]
+        while cells[-1] // 2 >= ncells_coarsest and cells[-1] % 2 == 0:
+            cells.append(cells[-1] // 2)
+        if len(cells) < 2:
+            raise ValueError("the hierarchy needs at least two levels (even cell counts)")
+        self.cells = cells
+        self.nlevels = L = len(cells)
+        self.maxiters = [10] * (L - 1) if maxiters is None else [int(m) for m in maxiters]
+        if len(self.maxiters) != L - 1:
+            raise ValueError(f"maxiters needs {L - 1} entries")
+        knots = [uniform_knots(p, N) for N in cells]
+        self.knots = knots
+        self.P1 = []
+        self.M1d, self.K1d, self.spaces, self.ops, self.transfers = [], [], [], [], []
+        for l in range(L):
+            n = len(knots[l]) - p - 1
+            M, K = assemble_1d(knots[l], p)
+            self.M1d.append(M)
+            self.K1d.append(K)
+            if l < L - 1:
+                _, _, P1 = two_level_setup_1d(p, knots[l], knots[l + 1])
+                self.P1.append(P1)
+            if l == L - 1:
+                break
+            V = StencilVectorSpace([n] * ndim, [p] * ndim, dist=dist if l == 0 else None, device=device,
+                                   align=align)
+            A = KronOperator.laplace(V, [M] * ndim, [K] * ndim, mass_coef=mass_coef)
+            if chunk:
+                A.set_chunk(chunk)
+            self.spaces.append(V)
+            self.ops.append(A)
+            self.transfers.append(KronTransfer(V, [self.P1[l]] * ndim))
+        # coarsest level: dense inverse of its operator (assembled = Galerkin, nested)
+        from .splines import band_to_dense
+        Mc, Kc = band_to_dense(self.M1d[-1]), band_to_dense(self.K1d[-1])
+        Ac = galerkin_coarse_dense(Mc, Kc, ndim, mass_coef)
+        self.Ac = Ac
+        Ainv = sla.lu_solve(sla.lu_factor(Ac), np.eye(Ac.shape[0]))
+        dev = f"cuda:{self.spaces[0].device}"
+        self.Ainv = torch.from_numpy(np.ascontiguousarray(Ainv)).to(dev)
+        self.rcs = [torch.empty(tr.ncoarse, dtype=F64, device=dev) for tr in self.transfers]
+        self.xc = torch.empty(Ac.shape[0], dtype=F64, device=dev)
+        self.infos = [None] * (L - 1)
+
+    @property
+    def ndof(self) -> int:
+        return self.spaces[0].dimension
+
+    @property
+    def space(self) -> StencilVectorSpace:
+        return self.spaces[0]
+
+    @property
+    def A(self) -> KronOperator:
+        return self.ops[0]
+
+    def rhs_ones(self) -> StencilVector:
+        b = self.spaces[0].empty()
+        _lib.call("poms_vec_fill", self.spaces[0].ctx, C.byref(self.spaces[0].layout), 1.0, rt.ptr(b._data),
+                  rt.stream_handle())
+        b._mark_written()
+        b.update_ghost_regions()
+        return b
+
+    def _level(self, l: int, b: StencilVector, x0: StencilVector | None) -> StencilVector:
+        A, tr = self.ops[l], self.transfers[l]
+        x, ipre = pcg(A, damped_jacobi, b, x0=x0, tol=self.tol, maxiter=self.maxiters[l])
+        r = A.residual(b, x)
+        rc = tr.restrict(r, out=self.rcs[l])
+        if l + 1 == self.nlevels - 1:
+            ec = self.xc
+            _lib.call("poms_dense_matvec", self.spaces[0].ctx, rc.numel(), rt.ptr(self.Ainv), rt.ptr(rc),
+                      rt.ptr(ec), rt.stream_handle())
+        else:
+            Vc = self.spaces[l + 1]
+            bc = Vc.empty()
+            Vc.interior(bc._data).copy_(rc.view(Vc.local_npts))
+            bc._mark_written()
+            bc.update_ghost_regions()
+            ecv = self._level(l + 1, bc, None)
+            ec = Vc.interior(ecv._data).contiguous().view(-1)
+        tr.prolong_add(ec, x)
+        x.update_ghost_regions()
+        x, ipos = pcg(A, damped_jacobi, b, x0=x, tol=self.tol, maxiter=self.maxiters[l])
+        if self.infos[l] is None:
+            self.infos[l] = (ipre, ipos)
+        return x
+
+    def cycle(self, b: StencilVector, x0: StencilVector | None = None):
+        """One V-cycle from level 0; returns ``(x, infos)``, ``infos[l] = (info_pre,
+        info_post)`` of level l's first visit in this cycle."""
+        self.infos = [None] * (self.nlevels - 1)
+        x = self._level(0, b, x0)
+        return x, list(self.infos)

@@ -137,3 +137,73 @@ def test_transfer_restrict_prolong(gpu):
     mg.transfer.prolong_add(torch.from_numpy(xc).cuda(), out)
     ref2 = f + np.einsum("ia,jb,kc,abc->ijk", P, P, P, xc.reshape((P.shape[1],) * 3))
     assert rel(out.to_local_numpy(), ref2) <= 1e-13
+
+
+@pytest.mark.parametrize("ndim,p,Nf,Nc,maxiters", [(2, 1, 32, 4, None), (2, 3, 32, 8, [4, 6]),
+                                                   (3, 2, 16, 4, [3, 10])])
+def test_multilevel_vcycle(gpu, ndim, p, Nf, Nc, maxiters):
+    """MultilevelVCycle against the oracle's recursive cycle with
+    materialised Galerkin operators R A P on every level: same iteration counts,
+    iterates within the parity bound."""
+    from poms_amd.mg import MultilevelVCycle
+    mg = MultilevelVCycle(p, Nf, Nc, ndim=ndim, maxiters=maxiters)
+    assert mg.nlevels >= 3
+    b = mg.rhs_ones()
+    x, infos = mg.cycle(b)
+    ones = np.ones((mg.spaces[0].npts[0],) * ndim)
+    Ms, Ks = [[mg.M1d[0]] * ndim], [[mg.K1d[0]] * ndim]
+    xr, rinfos = orc.vcycle_multilevel(Ms, Ks, mg.P1, ones, maxiters=mg.maxiters)
+    xr2, _ = orc.vcycle_multilevel(Ms, Ks, mg.P1, ones, maxiters=mg.maxiters, reorder=True)
+    tol = max(1e-9, 20.0 * rel(xr2, xr))
+    for l in range(mg.nlevels - 1):
+        assert infos[l][0]["niter"] == rinfos[l][0]["niter"] and infos[l][1]["niter"] == rinfos[l][1]["niter"], l
+    assert rel(x.to_local_numpy(), xr) <= tol
+
+
+def test_multilevel_converges_h_independently(gpu):
+    """Repeated multilevel cycles solve -Δu+u = 1 (2D, p = 2) with a contraction per
+    cycle that does not degrade as the grid is refined (the O(n) claim of
+    `slides/content.tex:42` that motivates SURVEY §8f rank 1)."""
+    from poms_amd.mg import MultilevelVCycle
+    rates = []
+    for N in (32, 128):
+        mg = MultilevelVCycle(2, N, 4, ndim=2)
+        mg.maxiters = [2] * (mg.nlevels - 1)
+        b = mg.rhs_ones()
+        x = None
+        res = []
+        for _ in range(4):
+            x, _ = mg.cycle(b, x0=x)
+            r = mg.A.residual(b, x)
+            res.append(np.sqrt(r.dot(r)))
+        rates.append((res[-1] / res[0]) ** (1.0 / 3))
+        assert res[-1] < 1e-3 * res[0]
+    assert rates[1] <= 2.0 * rates[0] + 0.05
+
+
+@pytest.mark.parametrize("ndim,p,Nf", [(2, 3, 80), (3, 2, 72)])
+def test_transfer_banded(gpu, ndim, p, Nf):
+    """Restriction / prolongation with coarse extents > 32 (the banded gather kernels
+    of the multilevel hierarchy) against dense einsum."""
+    import torch
+    from poms_amd.mg import two_level_setup_1d
+    from poms_amd.multilevels import KronTransfer
+    from poms_amd.splines import uniform_knots
+    from poms_amd.stencil import StencilVectorSpace
+    _, _, P1 = two_level_setup_1d(p, uniform_knots(p, Nf), uniform_knots(p, Nf // 2))
+    n = P1.shape[0]
+    assert P1.shape[1] > 32
+    V = StencilVectorSpace([n] * ndim, [p] * ndim, align=True)
+    tr = KronTransfer(V, [P1] * ndim)
+    rng = np.random.default_rng(4)
+    f = rng.uniform(-1, 1, (n,) * ndim)
+    rc = tr.restrict(V.zeros().from_numpy(f)).cpu().numpy()
+    sub = "ia,jb,kc,ijk->abc" if ndim == 3 else "ia,jb,ij->ab"
+    ref = np.einsum(sub, *([P1] * ndim), f).reshape(-1)
+    assert rel(rc, ref) <= 1e-13
+    xc = rng.uniform(-1, 1, rc.shape)
+    out = V.zeros().from_numpy(f)
+    tr.prolong_add(torch.from_numpy(xc).cuda(), out)
+    sub2 = "ia,jb,kc,abc->ijk" if ndim == 3 else "ia,jb,ab->ij"
+    ref2 = f + np.einsum(sub2, *([P1] * ndim), xc.reshape((P1.shape[1],) * ndim))
+    assert rel(out.to_local_numpy(), ref2) <= 1e-13
