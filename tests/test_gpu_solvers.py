@@ -199,11 +199,11 @@ def test_transfer_banded(gpu, ndim, p, Nf):
     f = rng.uniform(-1, 1, (n,) * ndim)
     rc = tr.restrict(V.zeros().from_numpy(f)).cpu().numpy()
     sub = "ia,jb,kc,ijk->abc" if ndim == 3 else "ia,jb,ij->ab"
-    ref = np.einsum(sub, *([P1] * ndim), f).reshape(-1)
+    ref = np.einsum(sub, *([P1] * ndim), f, optimize=True).reshape(-1)
     assert rel(rc, ref) <= 1e-13
     xc = rng.uniform(-1, 1, rc.shape)
     out = V.zeros().from_numpy(f)
     tr.prolong_add(torch.from_numpy(xc).cuda(), out)
     sub2 = "ia,jb,kc,abc->ijk" if ndim == 3 else "ia,jb,ab->ij"
-    ref2 = f + np.einsum(sub2, *([P1] * ndim), xc.reshape((P1.shape[1],) * ndim))
+    ref2 = f + np.einsum(sub2, *([P1] * ndim), xc.reshape((P1.shape[1],) * ndim), optimize=True)
     assert rel(out.to_local_numpy(), ref2) <= 1e-13
