@@ -44,6 +44,7 @@ typedef struct poms_ctx poms_ctx;           /* per-device context + scratch     
 typedef struct poms_op poms_op;             /* Kronecker(-sum) banded operator   */
 typedef struct poms_transfer poms_transfer; /* knot-insertion R = P^T / P        */
 typedef struct poms_comm poms_comm;         /* RCCL communicator of the slabs    */
+typedef struct poms_ksolve poms_ksolve;     /* factorised Kronecker direct solve */
 
 /* Grid layout of a (local) padded vector.  ndim in {1,2,3}; unused leading
  * axes have n = 1 and pad = 0.  Axis order is C order: axis 2 is unit-stride. */
@@ -266,6 +267,48 @@ int poms_prolong_add(poms_transfer* tr, const double* coarse, double* fine, void
  * `sources/mg_jac.py:98-99`.                                                  */
 int poms_dense_matvec(poms_ctx* ctx, int64_t n, const double* Minv, const double* x,
                       double* y, void* stream);
+
+/* ---- Kronecker direct solve (GLT post-smoother preconditioner) --------------- */
+/* X = (A0^-1 (x) A1^-1 (x) A2^-1) Y by banded LU line solves along each axis
+ * (axis 0 first, as the reference).  ab[d] is a HOST column-major (ldab[d] x n_d)
+ * array in LAPACK band storage of the UNFACTORED matrix of axis d, with kl[d]
+ * spare rows for fill-in: a(i, j) at ab[(kl+ku+i-j) + j*ldab], ldab >= 2kl+ku+1
+ * -- the layout `to_bnd` builds (`sources/kron_product.py:179-191`,
+ * `pyccel/test_kron_solve.py:37-44`).  Each is factorised once on the host with
+ * partial pivoting (LAPACK dgbtf2, as scipy's dgbtrf for kl < 32); axis-0 rows are
+ * global (n0_global).  2D/1D: leading unused axes have n = 1, pads = 0 and a NULL
+ * band.  kl + ku <= 16.
+ * Replaces: `dgbtrf` + the per-line `dgbtrs` loops of `kron_solve_par_bnd_pyccel_2d`
+ * / `_3d` (`pyccel/pyccel_functions.py:114-248`) and `kron_solve_par` /
+ * `kron_solve_serial` (`sources/kron_product.py:93-158`, dense dgetrf there).     */
+int poms_ksolve_create(poms_ctx* ctx, int ndim, const poms_layout* layout, int64_t n0_global,
+                       const double* const* ab, const int64_t* ldab, const int* kl, const int* ku,
+                       poms_ksolve** ks);
+int poms_ksolve_destroy(poms_ksolve* ks);
+/* dgbtrf info per axis (0 = ok, j+1 = u(j,j) is exactly zero; solves then fail). */
+int poms_ksolve_info(poms_ksolve* ks, int* info3);
+/* Absolute 0-based pivot rows of axis `axis` (n_d ints, host). */
+int poms_ksolve_pivots(poms_ksolve* ks, int axis, int* ipiv);
+/* x = solve(y) on the interior of padded device arrays (x may alias y; ghosts
+ * untouched).  All axes must be local (n0 == n0_global).                      */
+int poms_kron_solve(poms_ksolve* ks, const double* y, double* x, void* stream);
+/* One axis only (axis 0 needs n0 == n0_global). */
+int poms_kron_solve_axis(poms_ksolve* ks, int axis, const double* in, double* out, void* stream);
+/* Axis-0 solve of a dense C-order (n0_global, m) device buffer (the all-to-all
+ * transposed slab of a distributed solve; replaces the per-line `Allgatherv` +
+ * `dgbtrs` of `pyccel/pyccel_functions.py:150-155`).  out may alias in.         */
+int poms_kron_solve_axis0_dense(poms_ksolve* ks, const double* in, double* out, int64_t m, void* stream);
+/* Host-pointer drop-ins of `kron_solve_par_bnd_pyccel_2d(A_bnd, la, ua, B_bnd, lb,
+ * ub, X, Y, points, pads, ...)` / `_3d` on one rank: X, Y are padded C-order
+ * host arrays ((n_d + 2 pads_d) per axis); X's interior is overwritten, its
+ * ghosts are kept.  Synchronous.                                               */
+int poms_kron_solve_bnd_2d(poms_ctx* ctx, const double* A_bnd, int64_t lda, int la, int ua,
+                           const double* B_bnd, int64_t ldb, int lb, int ub, double* X, const double* Y,
+                           const int64_t* points, const int64_t* pads);
+int poms_kron_solve_bnd_3d(poms_ctx* ctx, const double* A_bnd, int64_t lda, int la, int ua,
+                           const double* B_bnd, int64_t ldb, int lb, int ub, const double* C_bnd,
+                           int64_t ldc, int lc, int uc, double* X, const double* Y,
+                           const int64_t* points, const int64_t* pads);
 
 /* ---- native RCCL communicator (slab ghost exchange, scalar all-reduces) ------ */
 /* Replaces `_update_ghost_regions_parallel` (`pyccel/kron_product.py:21-41`) and

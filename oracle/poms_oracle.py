@@ -26,7 +26,8 @@ from scipy.sparse.linalg import splu
 __all__ = [
     "band_dense", "band_csr", "kron_dot_pyccel_2d", "kron_product_apply", "kron_sum_apply",
     "kron_sum_csr", "kron_sum_diag", "residual", "damped_jacobi", "jacobi", "pcg",
-    "vcycle_two_level", "knots_to_insert",
+    "vcycle_two_level", "knots_to_insert", "to_bnd", "gbtrf", "gbtrs", "kron_solve", "pcg_glt",
+    "cardinal_bspline", "collocation_cardinal_splines",
 ]
 
 
@@ -200,6 +201,113 @@ def pcg(apply, psolve, b, x0=None, tol=1e-6, maxiter=100):
         beta = sr / srold
         p = s + beta * p
     return x, {"niter": k, "success": nrmr < tol * nrmr0, "res_norm": sqrt(nrmr)}
+
+
+# ---------------------------------------------------------------------------
+# Kronecker direct solve (GLT preconditioner): sources/kron_product.py:93-238,
+# pyccel/pyccel_functions.py:26-248.  LAPACK band storage, dgbtf2 / dgbtrs.
+# ---------------------------------------------------------------------------
+def to_bnd(A: np.ndarray):
+    """`sources/kron_product.py:179-191`: ``A_bnd[la+ua+i-j, j] = A[i, j]`` with ``la``
+    spare rows for fill-in."""
+    A = np.asarray(A, dtype=np.float64)
+    ii, jj = np.nonzero(A)
+    la = int(max(0, (ii - jj).max())) if ii.size else 0
+    ua = int(max(0, (jj - ii).max())) if ii.size else 0
+    ab = np.zeros((1 + ua + 2 * la, A.shape[0]), order="F")
+    ab[la + ua + ii - jj, jj] = A[ii, jj]
+    return ab, la, ua
+
+
+def gbtrf(ab: np.ndarray, kl: int, ku: int):
+    """LAPACK dgbtf2 (partial pivoting, the path scipy's dgbtrf takes for kl < 32),
+    0-based: returns (factorised copy, ipiv, info).  Pure-Python loops: small n."""
+    ab = np.array(ab, dtype=np.float64, order="F", copy=True)
+    n = ab.shape[1]
+    kv = kl + ku
+    for j in range(ku + 1, min(kv, n)):
+        ab[kv - j:kl, j] = 0.0
+    ipiv = np.zeros(n, dtype=np.int64)
+    ju, info = 0, 0
+    for j in range(n):
+        if j + kv < n:
+            ab[:kl, j + kv] = 0.0
+        km = min(kl, n - 1 - j)
+        jp = int(np.argmax(np.abs(ab[kv:kv + km + 1, j])))   # first maximum (idamax)
+        ipiv[j] = j + jp
+        if ab[kv + jp, j] != 0.0:
+            ju = max(ju, min(j + ku + jp, n - 1))
+            if jp != 0:
+                for c in range(ju - j + 1):
+                    ab[kv + jp - c, j + c], ab[kv - c, j + c] = ab[kv - c, j + c], ab[kv + jp - c, j + c]
+            if km > 0:
+                ab[kv + 1:kv + km + 1, j] *= 1.0 / ab[kv, j]
+                for k in range(1, ju - j + 1):
+                    y = ab[kv - k, j + k]
+                    if y != 0.0:
+                        ab[kv + 1 - k:kv + km + 1 - k, j + k] -= ab[kv + 1:kv + km + 1, j] * y
+        elif info == 0:
+            info = j + 1
+    return ab, ipiv, info
+
+
+def gbtrs(ab: np.ndarray, kl: int, ku: int, ipiv: np.ndarray, b: np.ndarray) -> np.ndarray:
+    """LAPACK dgbtrs (no transpose) on the leading axis of ``b`` (any trailing shape)."""
+    x = np.array(b, dtype=np.float64, copy=True)
+    n = ab.shape[1]
+    kd = kl + ku
+    for j in range(n - 1):
+        lm = min(kl, n - 1 - j)
+        l = int(ipiv[j])
+        if l != j:
+            x[[l, j]] = x[[j, l]]
+        if lm:
+            x[j + 1:j + 1 + lm] -= np.multiply.outer(ab[kd + 1:kd + 1 + lm, j], x[j])
+    for j in range(n - 1, -1, -1):        # dtbsv, upper, column form
+        x[j] = x[j] / ab[kd, j]
+        i0 = max(0, j - kd)
+        if j > i0:
+            x[i0:j] -= np.multiply.outer(ab[kd - (j - i0):kd, j], x[j])
+    return x
+
+
+def kron_solve(F: list, Y: np.ndarray) -> np.ndarray:
+    """``X = (F0^-1 ⊗ F1^-1 [⊗ F2^-1]) Y`` on a global interior array, axis 0 first
+    (`pyccel/pyccel_functions.py:150-171,216-246`)."""
+    X = np.array(Y, dtype=np.float64, copy=True)
+    for d, Fd in enumerate(F):
+        ab, kl, ku = to_bnd(Fd)
+        lu, ipiv, info = gbtrf(ab, kl, ku)
+        if info:
+            raise np.linalg.LinAlgError(f"factor {d} is singular (info {info})")
+        X = np.moveaxis(gbtrs(lu, kl, ku, ipiv, np.moveaxis(X, d, 0)), 0, d)
+    return X
+
+
+def pcg_glt(apply, F: list, b, x0=None, tol=1e-6, maxiter=100):
+    """`sources/solvers.py:239-306`: pcg with ``psolve = kron_solve_par(M2, M1, .)``
+    (here ``F[d]`` acts on axis ``d``; the reference passes ``(M2, M1)``)."""
+    shape = tuple(np.asarray(f).shape[0] for f in F)
+    return pcg(apply, lambda r: kron_solve(F, r.reshape(shape)).reshape(r.shape), b, x0=x0, tol=tol,
+               maxiter=maxiter)
+
+
+def cardinal_bspline(p: int, x):
+    """Cardinal B-spline of degree p on the knots 0, 1, ..., p+1 (truncated-power form)."""
+    from math import comb, factorial
+    x = np.asarray(x, dtype=np.float64)
+    s = np.zeros_like(x)
+    for k in range(p + 2):
+        s += (-1) ** k * comb(p + 1, k) * np.where(x > k, (x - k) ** p, 0.0)
+    return np.where((x > 0) & (x < p + 1), s / factorial(p), 0.0)
+
+
+def collocation_cardinal_splines(p: int, n: int) -> np.ndarray:
+    """spl's ``collocation_cardinal_splines(p, n)`` (spl absent, restated, UNPINNED):
+    the n x n symmetric Toeplitz matrix ``C[i, j] = N_p((p+1)/2 + i - j)`` of the centred
+    cardinal B-spline sampled at the integers."""
+    i = np.arange(n)
+    return cardinal_bspline(p, (p + 1) / 2.0 + i[:, None] - i[None, :])
 
 
 # ---------------------------------------------------------------------------

@@ -33,12 +33,26 @@ import scipy.sparse as sp
 
 
 # ---------------------------------------------------------------------------
+class _SubComm:
+    """Single-rank sub-communicator: ``Allgatherv`` copies the local block into the
+    receive buffer (``recv`` or ``[recv, sizes, displs(, type)]``)."""
+
+    def Allgatherv(self, send, recv):
+        buf = recv[0] if isinstance(recv, (list, tuple)) else recv
+        send = np.asarray(send)
+        buf[:send.size] = send.reshape(-1)
+
+    def py2f(self):
+        return 0
+
+
 class _Cart:
     def __init__(self, ndim):
         self._rank = 0
         self._size = 1
         self.nprocs = [1] * ndim
         self.coords = [0] * ndim
+        self.subcomm = [_SubComm() for _ in range(ndim)]
 
 
 class StencilVectorSpace:
@@ -340,6 +354,7 @@ def install():
     MPI = types.ModuleType("mpi4py.MPI")
     MPI.COMM_WORLD = _Comm()
     MPI.SUM = "sum"
+    MPI.DOUBLE = "double"
     import time as _t
     MPI.Wtime = _t.perf_counter
     mpi4py.MPI = MPI

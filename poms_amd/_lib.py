@@ -106,6 +106,17 @@ _SIGS = {
     "poms_restrict": [_vp, _vp, _vp, _vp],
     "poms_prolong_add": [_vp, _vp, _vp, _vp],
     "poms_dense_matvec": [_vp, _i64, _vp, _vp, _vp, _vp],
+    "poms_ksolve_create": [_vp, _i, _LP, _i64, C.POINTER(C.c_void_p), C.POINTER(_i64), C.POINTER(_i),
+                           C.POINTER(_i), _pp],
+    "poms_ksolve_destroy": [_vp],
+    "poms_ksolve_info": [_vp, C.POINTER(_i)],
+    "poms_ksolve_pivots": [_vp, _i, C.POINTER(_i)],
+    "poms_kron_solve": [_vp, _vp, _vp, _vp],
+    "poms_kron_solve_axis": [_vp, _i, _vp, _vp, _vp],
+    "poms_kron_solve_axis0_dense": [_vp, _vp, _vp, _i64, _vp],
+    "poms_kron_solve_bnd_2d": [_vp, _vp, _i64, _i, _i, _vp, _i64, _i, _i, _vp, _vp, _vp, _vp],
+    "poms_kron_solve_bnd_3d": [_vp, _vp, _i64, _i, _i, _vp, _i64, _i, _i, _vp, _i64, _i, _i, _vp, _vp, _vp,
+                               _vp],
 }
 _RESTYPES = {"poms_last_error": C.c_char_p}
 

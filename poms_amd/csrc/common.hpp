@@ -77,6 +77,26 @@ struct KronPtrs {
     const double* rdiag0 = nullptr;  // 1/diag(A) per global plane inside the axis-1/2 Toeplitz interior
 };
 
+// Banded LU factors of one axis of a Kronecker solve (kron_solve.hip).
+struct BandLU {
+    const double* L;  // n * kl   : L[j*kl + t-1] = l(j+t, j), t = 1..kl (0 past the end)
+    const double* U;  // n * (K+1): U[j*(K+1) + t] = u(j-t, j), t = 0..K (0 before the start)
+    const int* piv;   // n        : ipiv(j) - j in [0, kl]
+    int n, kl, K;     // K = kl + ku (fill-in widens U by kl)
+};
+
+// element (io, i2, j) of a line set at base + io*so + i2 + j*sa
+struct LineGeom {
+    int64_t base, so, sa;
+    int64_t no, n2;
+};
+
+// rows r in [0, nrows): row start base + (r / n1)*s0 + (r % n1)*s1, line along +1
+struct RowLines {
+    int64_t base, s0, s1;
+    int64_t n1, nrows;
+};
+
 void set_error(const std::string& msg);
 
 // Block-wide (256 threads) sum; result valid in thread 0.

@@ -43,6 +43,12 @@ int transfer_pass_launch(bool restrict_dir, int ncm, const AxisPass& ps, const d
 int transfer_band_launch(bool restrict_dir, const AxisPass& ps, const double* band, const int* lo, int w,
                          const double* in, double* out, hipStream_t st);
 
+int ksolve_strided_launch(const LineGeom& g, const BandLU& f, const double* in, double* out, hipStream_t st);
+int ksolve_rows_launch(const RowLines& g, const BandLU& f, const double* in, double* out, hipStream_t st);
+int band_lu(int64_t n, int kl, int ku, double* ab, int64_t ldab, int* ipiv);
+void band_lu_tables(int64_t n, int kl, int ku, const double* ab, int64_t ldab, const int* ipiv,
+                    std::vector<double>& L, std::vector<double>& U, std::vector<int>& piv);
+
 enum { V_AXPBY = 0, V_SCALE = 1, V_FILL = 2, V_DOT = 3, V_PCGUPD = 4, V_RUPD = 5, V_XPUPD = 6 };
 constexpr int64_t kScratch = 1 << 16;
 
@@ -118,6 +124,19 @@ struct poms_transfer {
     int *jlo[3]{}, *ilo[3]{};
     int wP[3]{}, wR[3]{};
     double *t0 = nullptr, *t1 = nullptr;
+};
+
+struct poms_ksolve {
+    poms_ctx* ctx = nullptr;
+    int ndim = 3;
+    poms_layout L{};
+    int64_t n0g = 1;
+    int info[3]{};
+    int kl[3]{}, ku[3]{};
+    std::vector<int> ipiv[3];   // absolute 0-based pivot rows (host copy, for callers)
+    double *Ld[3]{}, *Ud[3]{};
+    int* pivd[3]{};
+    BandLU f[3]{};
 };
 
 static hipStream_t as_stream(void* s) { return reinterpret_cast<hipStream_t>(s); }
@@ -966,6 +985,195 @@ int poms_dense_matvec(poms_ctx* ctx, int64_t n, const double* Minv, const double
     dense_matvec_launch((int)n, Minv, x, y, as_stream(stream));
     POMS_HIP_CHECK(hipGetLastError());
     return 0;
+}
+
+// ---- Kronecker direct solve (banded LU line solves) ---------------------------
+int poms_ksolve_destroy(poms_ksolve* ks) {
+    if (!ks) return 0;
+    for (int d = 0; d < 3; ++d) {
+        if (ks->Ld[d]) (void)hipFree(ks->Ld[d]);
+        if (ks->Ud[d]) (void)hipFree(ks->Ud[d]);
+        if (ks->pivd[d]) (void)hipFree(ks->pivd[d]);
+    }
+    delete ks;
+    return 0;
+}
+
+int poms_ksolve_create(poms_ctx* ctx, int ndim, const poms_layout* layout, int64_t n0_global,
+                       const double* const* ab, const int64_t* ldab, const int* kl, const int* ku,
+                       poms_ksolve** out) {
+    if (!ctx || !out || !ab || !ldab || !kl || !ku || !layout_ok(layout)) {
+        set_error("poms_ksolve_create: bad argument");
+        return 1;
+    }
+    if (ndim < 1 || ndim > 3) { set_error("poms_ksolve_create: ndim 1..3"); return 1; }
+    const int d0 = 3 - ndim;
+    for (int d = 0; d < d0; ++d)
+        if (layout->n[d] != 1 || layout->pads[d] != 0) {
+            set_error("poms_ksolve_create: unused leading axes need n = 1, pads = 0");
+            return 1;
+        }
+    if (ndim == 3 && n0_global < layout->n[0]) { set_error("poms_ksolve_create: n0_global < local n0"); return 1; }
+    for (int d = d0; d < 3; ++d) {
+        if (!ab[d] || kl[d] < 0 || ku[d] < 0 || ldab[d] < 2 * kl[d] + ku[d] + 1) {
+            set_error("poms_ksolve_create: bad band of axis " + std::to_string(d));
+            return 1;
+        }
+        if (kl[d] + ku[d] > 16) { set_error("poms_ksolve_create: kl + ku must be <= 16"); return 1; }
+    }
+    POMS_HIP_CHECK(hipSetDevice(ctx->device));
+    auto* ks = new poms_ksolve();
+    ks->ctx = ctx;
+    ks->ndim = ndim;
+    ks->L = *layout;
+    ks->n0g = ndim == 3 ? n0_global : 1;
+    int rc = 0;
+    for (int d = d0; d < 3 && !rc; ++d) {
+        const int64_t n = d == 0 ? ks->n0g : layout->n[d];
+        std::vector<double> band(ab[d], ab[d] + ldab[d] * n);
+        ks->ipiv[d].assign((size_t)n, 0);
+        ks->info[d] = band_lu(n, kl[d], ku[d], band.data(), ldab[d], ks->ipiv[d].data());
+        ks->kl[d] = kl[d];
+        ks->ku[d] = ku[d];
+        std::vector<double> Lt, Ut;
+        std::vector<int> pt;
+        band_lu_tables(n, kl[d], ku[d], band.data(), ldab[d], ks->ipiv[d].data(), Lt, Ut, pt);
+        rc |= upload(Lt.data(), Lt.size(), &ks->Ld[d]);
+        rc |= upload(Ut.data(), Ut.size(), &ks->Ud[d]);
+        if (!rc && hipMalloc(reinterpret_cast<void**>(&ks->pivd[d]), pt.size() * sizeof(int)) != hipSuccess) rc = 1;
+        if (!rc && hipMemcpy(ks->pivd[d], pt.data(), pt.size() * sizeof(int), hipMemcpyHostToDevice) != hipSuccess)
+            rc = 1;
+        ks->f[d] = BandLU{ks->Ld[d], ks->Ud[d], ks->pivd[d], (int)n, kl[d], kl[d] + ku[d]};
+    }
+    if (rc) {
+        if (g_err.empty()) set_error("poms_ksolve_create: allocation failed");
+        poms_ksolve_destroy(ks);
+        return 1;
+    }
+    *out = ks;
+    return 0;
+}
+
+int poms_ksolve_info(poms_ksolve* ks, int* info) {
+    if (!ks || !info) { set_error("poms_ksolve_info: bad argument"); return 1; }
+    for (int d = 0; d < 3; ++d) info[d] = ks->info[d];
+    return 0;
+}
+
+int poms_ksolve_pivots(poms_ksolve* ks, int axis, int* ipiv) {
+    if (!ks || !ipiv || axis < 3 - ks->ndim || axis > 2) { set_error("poms_ksolve_pivots: bad argument"); return 1; }
+    std::copy(ks->ipiv[axis].begin(), ks->ipiv[axis].end(), ipiv);
+    return 0;
+}
+
+static int ksolve_axis(poms_ksolve* ks, int axis, const double* in, double* out, hipStream_t st) {
+    if (ks->info[axis] != 0) {
+        set_error("kron solve: factor of axis " + std::to_string(axis) + " is singular (info " +
+                  std::to_string(ks->info[axis]) + ")");
+        return 1;
+    }
+    const RowGeom g = row_geom(&ks->L);
+    const int64_t base = g.pd0 * g.s0 + g.pd1 * g.s1 + g.pd2;
+    int rc = 0;
+    if (axis == 2) {
+        RowLines r{base, g.s0, g.s1, g.n1, (int64_t)g.n0 * g.n1};
+        rc = ksolve_rows_launch(r, ks->f[2], in, out, st);
+    } else if (axis == 1) {
+        LineGeom lg{base, g.s0, g.s1, g.n0, g.n2};
+        rc = ksolve_strided_launch(lg, ks->f[1], in, out, st);
+    } else {
+        if (ks->L.n[0] != ks->n0g) {
+            set_error("kron solve: axis 0 is distributed; use poms_kron_solve_axis0_dense on transposed data");
+            return 1;
+        }
+        LineGeom lg{base, g.s1, g.s0, g.n1, g.n2};
+        rc = ksolve_strided_launch(lg, ks->f[0], in, out, st);
+    }
+    if (rc) return rc;
+    POMS_HIP_CHECK(hipGetLastError());
+    return 0;
+}
+
+int poms_kron_solve_axis(poms_ksolve* ks, int axis, const double* in, double* out, void* stream) {
+    if (!ks || !in || !out || axis < 3 - ks->ndim || axis > 2) { set_error("poms_kron_solve_axis: bad argument"); return 1; }
+    return ksolve_axis(ks, axis, in, out, as_stream(stream));
+}
+
+int poms_kron_solve(poms_ksolve* ks, const double* y, double* x, void* stream) {
+    if (!ks || !y || !x) { set_error("poms_kron_solve: bad argument"); return 1; }
+    const double* src = y;
+    for (int d = 3 - ks->ndim; d < 3; ++d) {
+        if (ksolve_axis(ks, d, src, x, as_stream(stream))) return 1;
+        src = x;
+    }
+    return 0;
+}
+
+int poms_kron_solve_axis0_dense(poms_ksolve* ks, const double* in, double* out, int64_t m, void* stream) {
+    if (!ks || !in || !out || ks->ndim != 3 || m < 0) { set_error("poms_kron_solve_axis0_dense: bad argument"); return 1; }
+    if (ks->info[0] != 0) { set_error("kron solve: factor of axis 0 is singular"); return 1; }
+    LineGeom lg{0, 0, m, 1, m};
+    if (ksolve_strided_launch(lg, ks->f[0], in, out, as_stream(stream))) return 1;
+    POMS_HIP_CHECK(hipGetLastError());
+    return 0;
+}
+
+// host drop-in of kron_solve_par_bnd_pyccel_2d / _3d on one rank
+static int kron_solve_bnd_host(poms_ctx* ctx, int ndim, const double* const* bands, const int64_t* ld,
+                               const int* kl, const int* ku, double* X, const double* Y,
+                               const int64_t* points, const int64_t* pads) {
+    if (!ctx || !X || !Y || !points || !pads) { set_error("poms_kron_solve_bnd: null argument"); return 1; }
+    const int d0 = 3 - ndim;
+    poms_layout L{{1, 1, 1}, {0, 0, 0}, 0};
+    for (int d = d0; d < 3; ++d) {
+        L.n[d] = points[d - d0];
+        L.pads[d] = pads[d - d0];
+        if (!bands[d]) { set_error("poms_kron_solve_bnd: null band"); return 1; }
+    }
+    poms_ksolve* ks = nullptr;
+    if (poms_ksolve_create(ctx, ndim, &L, L.n[0], bands, ld, kl, ku, &ks)) return 1;
+    const RowGeom g = row_geom(&L);
+    const size_t nel = (size_t)(L.n[0] + 2 * L.pads[0]) * g.s0;
+    double *dx = nullptr, *dy = nullptr;
+    int rc = 0;
+    if (hipMalloc(reinterpret_cast<void**>(&dx), nel * sizeof(double)) != hipSuccess ||
+        hipMalloc(reinterpret_cast<void**>(&dy), nel * sizeof(double)) != hipSuccess) {
+        set_error("poms_kron_solve_bnd: hipMalloc failed");
+        rc = 1;
+    }
+    if (!rc && (hipMemcpy(dx, X, nel * sizeof(double), hipMemcpyHostToDevice) != hipSuccess ||
+                hipMemcpy(dy, Y, nel * sizeof(double), hipMemcpyHostToDevice) != hipSuccess)) {
+        set_error("poms_kron_solve_bnd: upload failed");
+        rc = 1;
+    }
+    if (!rc) rc = poms_kron_solve(ks, dy, dx, nullptr);
+    if (!rc && hipMemcpy(X, dx, nel * sizeof(double), hipMemcpyDeviceToHost) != hipSuccess) {
+        set_error("poms_kron_solve_bnd: download failed");
+        rc = 1;
+    }
+    if (dx) (void)hipFree(dx);
+    if (dy) (void)hipFree(dy);
+    poms_ksolve_destroy(ks);
+    return rc;
+}
+
+int poms_kron_solve_bnd_2d(poms_ctx* ctx, const double* A_bnd, int64_t lda, int la, int ua,
+                           const double* B_bnd, int64_t ldb, int lb, int ub, double* X, const double* Y,
+                           const int64_t* points, const int64_t* pads) {
+    const double* bands[3] = {nullptr, A_bnd, B_bnd};
+    const int64_t ld[3] = {1, lda, ldb};
+    const int kl[3] = {0, la, lb}, ku[3] = {0, ua, ub};
+    return kron_solve_bnd_host(ctx, 2, bands, ld, kl, ku, X, Y, points, pads);
+}
+
+int poms_kron_solve_bnd_3d(poms_ctx* ctx, const double* A_bnd, int64_t lda, int la, int ua,
+                           const double* B_bnd, int64_t ldb, int lb, int ub, const double* C_bnd,
+                           int64_t ldc, int lc, int uc, double* X, const double* Y,
+                           const int64_t* points, const int64_t* pads) {
+    const double* bands[3] = {A_bnd, B_bnd, C_bnd};
+    const int64_t ld[3] = {lda, ldb, ldc};
+    const int kl[3] = {la, lb, lc}, ku[3] = {ua, ub, uc};
+    return kron_solve_bnd_host(ctx, 3, bands, ld, kl, ku, X, Y, points, pads);
 }
 
 }  // extern "C"

@@ -1,0 +1,266 @@
+"""Kronecker direct solve and the GLT post-smoother's preconditioner.
+
+``X = (F0^-1 ⊗ F1^-1 [⊗ F2^-1]) Y`` by banded LU line solves along each axis
+(axis 0 first, as the reference): the ``kron_solve_*`` family of
+`sources/kron_product.py:93-238` and `pyccel/kron_product.py:93-200`, whose
+native kernels are `pyccel/pyccel_functions.py:26-248`.
+
+Each 1D factor is converted to LAPACK band storage (:func:`to_bnd`,
+`sources/kron_product.py:179-191`) and factorised ONCE on the host with partial
+pivoting inside ``poms_ksolve_create`` (dgbtf2, what scipy's ``dgbtrf`` runs for
+these bandwidths; pivots are identical).  Every solve then runs only the
+``dgbtrs`` sweeps on the GPU (``csrc/kron_solve.hip``).  The reference's dense
+``dgetrf``/``dgetrs`` variants (`sources/kron_product.py:93-158`) factorise the
+same banded matrices: partial pivoting never picks an entry outside the band, so
+the pivots and the factors agree.
+
+Slab-distributed 3D spaces: axes 1 and 2 are local; axis 0 is transposed by an
+all-to-all (the slab's interior, split along axis 1, one block per rank), solved
+as dense columns and transposed back.  That replaces the per-line
+``Allgatherv`` of `pyccel/pyccel_functions.py:150-155` (one collective per
+line) by two collectives per solve.
+"""
+from __future__ import annotations
+
+import ctypes as C
+
+import numpy as np
+import torch
+
+from . import _lib
+from . import runtime as rt
+from .stencil import StencilVector, StencilVectorSpace, _stream
+
+F64 = torch.float64
+
+
+def _dense(F) -> np.ndarray:
+    if isinstance(F, np.ndarray) and F.ndim == 2 and F.shape[0] == F.shape[1]:
+        return np.asarray(F, dtype=np.float64)
+    if hasattr(F, "toarray"):
+        return np.asarray(F.toarray(), dtype=np.float64)
+    raise TypeError("1D factor must be a square ndarray or have .toarray()")
+
+
+def to_bnd(A) -> tuple[np.ndarray, int, int]:
+    """``(A_bnd, la, ua)``: LAPACK band storage (column-major, ``2 la + ua + 1`` rows,
+    ``la`` spare rows for fill-in) of a dense / 1D-stencil matrix, ``A_bnd[la+ua+i-j, j]
+    = A[i, j]`` (`sources/kron_product.py:179-191`)."""
+    D = _dense(A)
+    n = D.shape[0]
+    ii, jj = np.nonzero(D)
+    la = int(max(0, (ii - jj).max())) if ii.size else 0
+    ua = int(max(0, (jj - ii).max())) if ii.size else 0
+    ab = np.zeros((1 + ua + 2 * la, n), order="F")
+    ab[la + ua + ii - jj, jj] = D[ii, jj]
+    return ab, la, ua
+
+
+def _as_band(F):
+    """(F-order band array, la, ua) from a matrix or an (A_bnd, la, ua) triple."""
+    if isinstance(F, tuple) and len(F) == 3:
+        ab, la, ua = F
+        return np.asfortranarray(np.asarray(ab, dtype=np.float64)), int(la), int(ua)
+    return to_bnd(F)
+
+
+class KronSolver:
+    """Factorised ``F0 ⊗ F1 [⊗ F2]`` on a :class:`StencilVectorSpace`; ``factors[d]`` acts on
+    axis ``d`` (a square ndarray, anything with ``toarray()``, or ``(A_bnd, la, ua)``)."""
+
+    def __init__(self, V: StencilVectorSpace, factors):
+        if len(factors) != V.ndim:
+            raise ValueError(f"{V.ndim}D space needs {V.ndim} factors")
+        self.V = V
+        lead = 3 - V.ndim
+        bands = [None] * 3
+        kl, ku, ld = (C.c_int * 3)(), (C.c_int * 3)(), (C.c_int64 * 3)()
+        for d in range(3):
+            ld[d] = 1
+        self._keep = []
+        for k, F in enumerate(factors):
+            d = lead + k
+            ab, la, ua = _as_band(F)
+            if ab.shape[1] != V.npts[k]:
+                raise ValueError(f"factor {k} has {ab.shape[1]} columns, axis has {V.npts[k]} points")
+            if ab.shape[0] < 2 * la + ua + 1:
+                raise ValueError(f"factor {k}: band array needs 2*la+ua+1 = {2 * la + ua + 1} rows")
+            self._keep.append(ab)
+            bands[d] = ab
+            kl[d], ku[d], ld[d] = la, ua, ab.shape[0]
+        ptrs = (C.c_void_p * 3)(*[None if b is None else b.ctypes.data for b in bands])
+        self.kl, self.ku = tuple(kl), tuple(ku)
+        h = C.c_void_p()
+        _lib.call("poms_ksolve_create", V.ctx, V.ndim, C.byref(V.layout), int(V.npts[0]) if V.ndim == 3 else 1,
+                  ptrs, ld, kl, ku, C.byref(h))
+        self._h = h
+        info = (C.c_int * 3)()
+        _lib.call("poms_ksolve_info", h, info)
+        self.info = tuple(info)[lead:]
+
+    def __del__(self):
+        h = getattr(self, "_h", None)
+        if h is not None and h.value:
+            try:
+                _lib.lib.poms_ksolve_destroy(h)
+            except Exception:
+                pass
+            self._h = None
+
+    def pivots(self, axis: int) -> np.ndarray:
+        """0-based pivot rows (dgbtrf ``ipiv - 1``) of factor ``axis``."""
+        d = 3 - self.V.ndim + axis
+        n = self.V.npts[axis]
+        out = np.zeros(n, dtype=np.int32)
+        _lib.call("poms_ksolve_pivots", self._h, d, out.ctypes.data_as(C.POINTER(C.c_int)))
+        return out
+
+    # ------------------------------------------------------------------
+    def solve(self, Y: StencilVector, out: StencilVector | None = None) -> StencilVector:
+        V = self.V
+        if Y.space is not V and (Y.space.npts != V.npts or Y.space.pads != V.pads
+                                 or Y.space.layout.pitch != V.layout.pitch):
+            raise ValueError("vector is not in the solver's space")
+        X = V.empty() if out is None else out
+        st = rt.stream_handle()
+        if not V.is_distributed:
+            _lib.call("poms_kron_solve", self._h, rt.ptr(Y._data), rt.ptr(X._data), st)
+        else:
+            self._axis0_distributed(Y, X)
+            for d in (1, 2):
+                _lib.call("poms_kron_solve_axis", self._h, d, rt.ptr(X._data), rt.ptr(X._data), st)
+        X._mark_written()
+        return X
+
+    def _axis0_distributed(self, Y: StencilVector, X: StencilVector) -> None:
+        """Axis-0 line solves of a slab-distributed vector: all-to-all transpose
+        (slab -> axis-1 columns), dense column solve, all-to-all back."""
+        import torch.distributed as dist
+        from .dist import slab_bounds
+        V, D = self.V, self.V.dist
+        w, me = D.world, D.rank
+        n0l, n1, n2 = V.local_npts
+        cols = [slab_bounds(n1, w, r) if n1 >= w else (min(r, n1), min(r + 1, n1)) for r in range(w)]
+        n0s = [slab_bounds(V.npts[0], w, r) for r in range(w)]
+        Yi = V.interior(Y._data)
+        send = torch.cat([Yi[:, a:b, :].reshape(-1) for a, b in cols])
+        m_me = cols[me][1] - cols[me][0]
+        recv_sizes = [(e - s) * m_me * n2 for s, e in n0s]
+        send_sizes = [n0l * (b - a) * n2 for a, b in cols]
+        recv = torch.empty(sum(recv_sizes), dtype=F64, device=send.device)
+        self._a2a(recv, send, recv_sizes, send_sizes)
+        if m_me * n2 > 0:
+            _lib.call("poms_kron_solve_axis0_dense", self._h, rt.ptr(recv), rt.ptr(recv), m_me * n2,
+                      rt.stream_handle())
+        back = torch.empty(sum(send_sizes), dtype=F64, device=send.device)
+        self._a2a(back, recv, send_sizes, recv_sizes)
+        Xi = V.interior(X._data)
+        off = 0
+        for a, b in cols:
+            k = n0l * (b - a) * n2
+            Xi[:, a:b, :].copy_(back[off:off + k].view(n0l, b - a, n2))
+            off += k
+
+    def _a2a(self, out: torch.Tensor, inp: torch.Tensor, out_sizes, in_sizes) -> None:
+        import torch.distributed as dist
+        D = self.V.dist
+        if D.cuda_transport or out.device.type == "cpu":
+            dist.all_to_all_single(out, inp, out_sizes, in_sizes, group=D.group)
+            return
+        oc = torch.empty(out.numel(), dtype=out.dtype)
+        dist.all_to_all_single(oc, inp.cpu(), out_sizes, in_sizes, group=D.group)
+        out.copy_(oc)
+
+
+_CACHE: dict = {}
+
+
+def solver_for(V: StencilVectorSpace, factors) -> KronSolver:
+    """Cached :class:`KronSolver` (keyed on the space and the factors' contents)."""
+    key = (id(V), tuple(id(f) for f in factors))
+    dense = [None if isinstance(f, tuple) else _dense(f) for f in factors]
+    ent = _CACHE.get(key)
+    if ent is not None and all((a is None and b is None) or (a is not None and b is not None and np.array_equal(a, b))
+                               for a, b in zip(ent[1], dense)):
+        return ent[0]
+    ks = KronSolver(V, factors)
+    _CACHE.clear()
+    _CACHE[key] = (ks, dense)
+    return ks
+
+
+# ---- the reference's entry points -------------------------------------------
+def kron_solve_serial(A, B, Y: StencilVector) -> StencilVector:
+    """``X`` with ``(A ⊗ B) X = Y`` (`sources/kron_product.py:93-115`); A acts on axis 0."""
+    return solver_for(Y.space, (A, B)).solve(Y)
+
+
+def kron_solve_par(A, B, Y: StencilVector) -> StencilVector:
+    """Distributed form of :func:`kron_solve_serial` (`sources/kron_product.py:119-158`)."""
+    return solver_for(Y.space, (A, B)).solve(Y)
+
+
+def kron_solve_3d(A, B, Cf, Y: StencilVector) -> StencilVector:
+    """``X`` with ``(A ⊗ B ⊗ C) X = Y`` (3D analogue of the above)."""
+    return solver_for(Y.space, (A, B, Cf)).solve(Y)
+
+
+def kron_solve_par_bnd_2d(A_bnd, la, ua, B_bnd, lb, ub, Y: StencilVector, X: StencilVector,
+                          with_pycc: bool = False) -> StencilVector:
+    """Band-storage form (`pyccel/kron_product.py:135-164`): writes ``X`` and returns it."""
+    return solver_for(Y.space, ((A_bnd, la, ua), (B_bnd, lb, ub))).solve(Y, out=X)
+
+
+def kron_solve_par_bnd_3d(A_bnd, la, ua, B_bnd, lb, ub, C_bnd, lc, uc, Y: StencilVector,
+                          X: StencilVector) -> StencilVector:
+    """`pyccel/kron_product.py:166-200`."""
+    return solver_for(Y.space, ((A_bnd, la, ua), (B_bnd, lb, ub), (C_bnd, lc, uc))).solve(Y, out=X)
+
+
+# ---- host-array drop-ins of the native kernels --------------------------------
+def _host_args(X, Y, points, pads, nd):
+    for name, arr in (("X", X), ("Y", Y)):
+        if not (isinstance(arr, np.ndarray) and arr.dtype == np.float64 and arr.flags.c_contiguous):
+            raise TypeError(f"{name} must be a C-contiguous float64 numpy array")
+    points = np.ascontiguousarray(points, dtype=np.int64)
+    pads = np.ascontiguousarray(pads, dtype=np.int64)
+    if points.shape != (nd,) or pads.shape != (nd,):
+        raise ValueError(f"points/pads need {nd} entries")
+    shape = tuple(int(n + 2 * p) for n, p in zip(points, pads))
+    if X.shape != shape or Y.shape != shape:
+        raise ValueError(f"X/Y must have the padded shape {shape}")
+    return points, pads
+
+
+def kron_solve_par_bnd_pyccel_2d(A_bnd, la, ua, B_bnd, lb, ub, X, Y, points, pads):
+    """Host drop-in of `pyccel/pyccel_functions.py:114-171` on one rank (no
+    sub-communicators): X's interior is overwritten with the solution, X returned."""
+    points, pads = _host_args(X, Y, points, pads, 2)
+    a = np.asfortranarray(A_bnd, dtype=np.float64)
+    b = np.asfortranarray(B_bnd, dtype=np.float64)
+    ctx = rt.ctx(rt.device_index())
+    _lib.call("poms_kron_solve_bnd_2d", ctx, a.ctypes.data_as(C.c_void_p), a.shape[0], int(la), int(ua),
+              b.ctypes.data_as(C.c_void_p), b.shape[0], int(lb), int(ub), X.ctypes.data_as(C.c_void_p),
+              Y.ctypes.data_as(C.c_void_p), points.ctypes.data_as(C.c_void_p), pads.ctypes.data_as(C.c_void_p))
+    return X
+
+
+def kron_solve_par_bnd_pyccel_3d(A_bnd, la, ua, B_bnd, lb, ub, C_bnd, lc, uc, X, Y, points, pads):
+    """Host drop-in of `pyccel/pyccel_functions.py:174-248` on one rank."""
+    points, pads = _host_args(X, Y, points, pads, 3)
+    a = np.asfortranarray(A_bnd, dtype=np.float64)
+    b = np.asfortranarray(B_bnd, dtype=np.float64)
+    c = np.asfortranarray(C_bnd, dtype=np.float64)
+    ctx = rt.ctx(rt.device_index())
+    _lib.call("poms_kron_solve_bnd_3d", ctx, a.ctypes.data_as(C.c_void_p), a.shape[0], int(la), int(ua),
+              b.ctypes.data_as(C.c_void_p), b.shape[0], int(lb), int(ub), c.ctypes.data_as(C.c_void_p),
+              c.shape[0], int(lc), int(uc), X.ctypes.data_as(C.c_void_p), Y.ctypes.data_as(C.c_void_p),
+              points.ctypes.data_as(C.c_void_p), pads.ctypes.data_as(C.c_void_p))
+    return X
+
+
+def kron_solve_serial_pyccel_2d(A, B, X, Y, points, pads):
+    """Host drop-in of `pyccel/pyccel_functions.py:26-56` (dense A, B): A acts on axis 0."""
+    a, la, ua = to_bnd(A)
+    b, lb, ub = to_bnd(B)
+    return kron_solve_par_bnd_pyccel_2d(a, la, ua, b, lb, ub, X, Y, points, pads)

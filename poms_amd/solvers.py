@@ -10,6 +10,10 @@ Signatures, defaults, return conventions and stopping rules are those of
 * ``damped_jacobi(A, b, x0=None, tol=1e-6, maxiter=10, verbose=False) -> x``
   (:167-235), omega = 2/3, stop when ``dr.dr < tol**2`` *after* the update.
 * ``jacobi(A, b) -> x`` (:139-163).
+* ``pcg_glt(A, M1, M2, b, x0=None, tol=1e-6, maxiter=100, verbose=False) -> (x, info)``
+  (:239-306): the same PCG with the Kronecker direct solve
+  ``kron_solve_par(M2, M1, r)`` as preconditioner (:258, :290), factorised once
+  per (M2, M1) pair (``poms_amd.kron_solve``); :func:`pcg_kron` is its n-D form.
 
 Differences that do not change results:
 * the reference's discarded ``s = A.dot(r)`` (:109) is not computed;
@@ -345,3 +349,19 @@ def _damped_jacobi(A, b, x0=None, tol=1e-6, maxiter=10, verbose=False, want_dot=
     if verbose:
         print("+---------+---------------------+")
     return x, dot
+
+
+def pcg_kron(A, factors, b, x0=None, tol=1e-6, maxiter=100, verbose=False):
+    """PCG preconditioned by ``X = (F0^-1 ⊗ F1^-1 [⊗ F2^-1]) R`` (``factors[d]`` acts on
+    axis ``d``): the body of `sources/solvers.py:239-306` for any dimension."""
+    from .kron_solve import solver_for
+    ks = solver_for(b.space, tuple(factors))
+    return pcg(A, lambda _A, r: ks.solve(r), b, x0=x0, tol=tol, maxiter=maxiter, verbose=verbose)
+
+
+def pcg_glt(A, M1, M2, b, x0=None, tol=1e-6, maxiter=100, verbose=False):
+    """GLT-preconditioned CG (`sources/solvers.py:239-306`).  As the reference, the
+    preconditioner is ``kron_solve_par(M2, M1, r)`` (:258, :290): M2 acts on axis 0."""
+    if b.space.ndim != 2:
+        raise ValueError("pcg_glt is the 2D solver of the reference; use pcg_kron for other dimensions")
+    return pcg_kron(A, (M2, M1), b, x0=x0, tol=tol, maxiter=maxiter, verbose=verbose)

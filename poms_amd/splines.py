@@ -274,3 +274,29 @@ def greville(T: np.ndarray, p: int) -> np.ndarray:
     """Greville abscissae (knot averages) -- used by the spline-reproduction tests."""
     n = len(T) - p - 1
     return np.array([np.mean(T[i + 1:i + p + 1]) if p > 0 else T[i] for i in range(n)])
+
+
+def cardinal_bspline(p: int, x):
+    """Cardinal B-spline of degree p on the integer knots 0..p+1 (truncated-power form)."""
+    from math import comb, factorial
+    x = np.asarray(x, dtype=np.float64)
+    s = np.zeros_like(x)
+    for k in range(p + 2):
+        s += (-1) ** k * comb(p + 1, k) * np.where(x > k, (x - k) ** p, 0.0)
+    return np.where((x > 0) & (x < p + 1), s / factorial(p), 0.0)
+
+
+def collocation_cardinal_splines(p: int, n: int) -> np.ndarray:
+    """The GLT preconditioner's 1D matrix (`sources/mg_glt.py:115-116`): spl's
+    ``collocation_cardinal_splines(p, n)``, restated because spl is absent (parity
+    UNPINNED): the symmetric Toeplitz ``C[i, j] = N_p((p+1)/2 + i - j)`` of the centred
+    cardinal B-spline sampled at the integers (p=3: [1, 4, 1]/6; p=1: identity)."""
+    i = np.arange(int(n))
+    return cardinal_bspline(int(p), (p + 1) / 2.0 + i[:, None] - i[None, :])
+
+
+def array_to_mat_stencil(n: int, p: int, C: np.ndarray):
+    """`sources/utils.py:104-133`: the entries of C within the 2p+1 band as a 1D
+    stencil matrix (host band rows)."""
+    from .stencil import StencilMatrix1D
+    return StencilMatrix1D(n, p, dense_to_band(np.asarray(C, dtype=np.float64), p))

@@ -73,3 +73,11 @@ def test_two_rank_distributed_operator_and_vcycle_gpu(device_reductions):
     import torch
     assert torch.cuda.device_count() >= 1, "GPU test selected but no GPU visible"
     _launch("gpu", extra_env={"POMS_TEST_DEVRED": "1" if device_reductions else "0"})
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("world", [2, 3])
+def test_distributed_kron_solve_gpu(world):
+    import torch
+    assert torch.cuda.device_count() >= 1, "GPU test selected but no GPU visible"
+    _launch("gpu_ksolve", world=world)
