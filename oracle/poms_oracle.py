@@ -324,8 +324,12 @@ def knots_to_insert(Tf, nf, pf, Tc, nc, pc):
     return np.array([t for t in Tf[pf + 1:nf] if float(t) not in coarse], dtype=np.float64)
 
 
-def vcycle_two_level(M, K, P1, b, c=1.0, tol=1e-6, maxiter=10, x0=None, reorder=False):
+def vcycle_two_level(M, K, P1, b, c=1.0, tol=1e-6, maxiter=10, x0=None, reorder=False, glt=None):
     """`sources/mg_jac.py:84-119` on global arrays with materialised R, P, Ac, splu.
+
+    ``glt`` (list of per-axis 1D matrices): the post-smoother is instead
+    `sources/mg_glt.py:113-123`, ``pcg_glt`` with ``maxiter = p + 1``, whose
+    preconditioner solves with ``glt[d]`` on axis ``d``.
 
     ``reorder=True`` applies the fine operator term by term instead of through
     the assembled CSR matrix: same arithmetic, different summation order (used
@@ -351,7 +355,11 @@ def vcycle_two_level(M, K, P1, b, c=1.0, tol=1e-6, maxiter=10, x0=None, reorder=
     rc = R @ rf
     xc = splu(Ac).solve(rc)
     xf = xf + P @ xc
-    xf2, info_pos = pcg(apply, psolve, bf, x0=xf, tol=tol, maxiter=maxiter)
+    if glt is not None:
+        p = (M[0].shape[1] - 1) // 2
+        xf2, info_pos = pcg_glt(apply, glt, bf, x0=xf, tol=tol, maxiter=p + 1)
+    else:
+        xf2, info_pos = pcg(apply, psolve, bf, x0=xf, tol=tol, maxiter=maxiter)
     return xf2.reshape(b.shape), info_pre, info_pos
 
 

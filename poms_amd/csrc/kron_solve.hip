@@ -43,8 +43,10 @@ __device__ __forceinline__ void feed(double (&w)[MW + 1], int S, double v) {
 
 // dgbtrs forward step j: w[t] = b(j + t).  Interchange b(j) <-> b(ipiv(j)),
 // then b(j+t) -= l(j+t, j) b(j) (the DGER of dgbtrs, column form).
-template <int MW>
+// CKL / CK >= 0: kl / K known at compile time (the predicates fold away).
+template <int MW, int CKL = -1>
 __device__ __forceinline__ double step_fwd(double (&w)[MW + 1], const BandLU& f, int j) {
+    const int kl = CKL >= 0 ? CKL : f.kl;
     const int l = f.piv[j];
     if (l != 0) {
 #pragma unroll
@@ -56,29 +58,30 @@ __device__ __forceinline__ double step_fwd(double (&w)[MW + 1], const BandLU& f,
             }
     }
     const double b0 = w[0];
-    const double* Lj = f.L + (int64_t)j * f.kl;
+    const double* Lj = f.L + (int64_t)j * kl;
 #pragma unroll
     for (int t = 1; t <= MW; ++t)
-        if (t <= f.kl) w[t] = fma(-Lj[t - 1], b0, w[t]);
+        if (t <= kl) w[t] = fma(-Lj[t - 1], b0, w[t]);
     return b0;
 }
 
 // dtbsv (upper, no transpose, non-unit) step j: w[t] = b(j - t).
 // x(j) = b(j) / u(j,j), then b(j-t) -= x(j) u(j-t, j).
-template <int MW>
+template <int MW, int CK = -1>
 __device__ __forceinline__ double step_bwd(double (&w)[MW + 1], const BandLU& f, int j) {
-    const double* Uj = f.U + (int64_t)j * (f.K + 1);
+    const int K = CK >= 0 ? CK : f.K;
+    const double* Uj = f.U + (int64_t)j * (K + 1);
     const double x = w[0] / Uj[0];
 #pragma unroll
     for (int t = 1; t <= MW; ++t)
-        if (t <= f.K) w[t] = fma(-Uj[t], x, w[t]);
+        if (t <= K) w[t] = fma(-Uj[t], x, w[t]);
     return x;
 }
 
 // One line per thread.  `in` may alias `out`: every position is loaded before
 // it is stored (forward: stores trail the loads by kl; backward runs downward
 // and stores trail by K), and the backward re-reads only this thread's stores.
-template <int MW>
+template <int MW, int CKL, int CK>
 __global__ void __launch_bounds__(256)
 ksolve_strided_kernel(const LineGeom g, const BandLU f, const double* in, double* out) {
     const int64_t tid = (int64_t)blockIdx.x * 256 + threadIdx.x;
@@ -87,8 +90,8 @@ ksolve_strided_kernel(const LineGeom g, const BandLU f, const double* in, double
     const int64_t off = g.base + io * g.so + i2;
     const double* src = in + off;
     double* dst = out + off;
-    const int n = f.n, kl = f.kl, K = f.K;
-    constexpr int D = 8;
+    const int n = f.n, kl = CKL >= 0 ? CKL : f.kl, K = CK >= 0 ? CK : f.K;
+    constexpr int D = MW <= 4 ? 16 : 8;   // loads in flight per thread
     double w[MW + 1];
 #pragma unroll
     for (int t = 0; t <= MW; ++t) w[t] = 0.0;
@@ -105,7 +108,7 @@ ksolve_strided_kernel(const LineGeom g, const BandLU f, const double* in, double
             if (m >= n + kl) break;
             feed<MW>(w, kl, v[d]);
             const int j = m - kl;
-            if (j >= 0) dst[(int64_t)j * g.sa] = step_fwd<MW>(w, f, j);
+            if (j >= 0) dst[(int64_t)j * g.sa] = step_fwd<MW, CKL>(w, f, j);
         }
     }
 #pragma unroll
@@ -123,7 +126,7 @@ ksolve_strided_kernel(const LineGeom g, const BandLU f, const double* in, double
             if (m < -K) break;
             feed<MW>(w, K, v[d]);
             const int j = m + K;
-            if (j <= n - 1) dst[(int64_t)j * g.sa] = step_bwd<MW>(w, f, j);
+            if (j <= n - 1) dst[(int64_t)j * g.sa] = step_bwd<MW, CK>(w, f, j);
         }
     }
 }
@@ -139,16 +142,16 @@ __device__ __forceinline__ void wave_sync() {
 // One sweep (BWD = 0 forward, 1 backward) over rows along the unit-stride axis.
 // Forward feeds columns m = 0, 1, ... and emits y(m - kl); backward feeds
 // m = n-1, n-2, ... and emits x(m + K).  in may alias out.
-template <int MW, int BWD>
+template <int MW, int BWD, int CKL, int CK>
 __global__ void __launch_bounds__(64 * kRowWaves)
 ksolve_rows_kernel(const RowLines g, const BandLU f, const double* in, double* out) {
     constexpr int C = kChunk, RPI = 64 / C;
+    // one tile: a lane reads column c of its own row before it writes its output there
     __shared__ double s_in[kRowWaves][64][C + 1];
-    __shared__ double s_out[kRowWaves][64][C + 1];
     const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
     const int64_t row0 = ((int64_t)blockIdx.x * kRowWaves + wv) * 64;
     if (row0 >= g.nrows) return;  // the whole wave leaves; no block barriers below
-    const int n = f.n, S = BWD ? f.K : f.kl;
+    const int n = f.n, S = BWD ? (CK >= 0 ? CK : f.K) : (CKL >= 0 ? CKL : f.kl);
     const int ccol = lane % C, crow0 = lane / C;
     int64_t ra[C];   // row start of coop element i (row crow0 + i*RPI of the wave)
     bool rv[C];
@@ -182,8 +185,8 @@ ksolve_rows_kernel(const RowLines g, const BandLU f, const double* in, double* o
             feed<MW>(w, S, s_in[wv][lane][c]);
             const int j = BWD ? m + S : m - S;
             double o = 0.0;
-            if (j >= 0 && j < n) o = BWD ? step_bwd<MW>(w, f, j) : step_fwd<MW>(w, f, j);
-            s_out[wv][lane][c] = o;
+            if (j >= 0 && j < n) o = BWD ? step_bwd<MW, CK>(w, f, j) : step_fwd<MW, CKL>(w, f, j);
+            s_in[wv][lane][c] = o;
         }
         wave_sync();
         {
@@ -191,9 +194,10 @@ ksolve_rows_kernel(const RowLines g, const BandLU f, const double* in, double* o
             if (j >= 0 && j < n) {
 #pragma unroll
                 for (int i = 0; i < C; ++i)
-                    if (rv[i]) out[ra[i] + j] = s_out[wv][i * RPI + crow0][ccol];
+                    if (rv[i]) out[ra[i] + j] = s_in[wv][i * RPI + crow0][ccol];
             }
         }
+        wave_sync();   // every lane has read its outputs before the tile is refilled
         if (q + 1 < nch) {
 #pragma unroll
             for (int i = 0; i < C; ++i) s_in[wv][i * RPI + crow0][ccol] = pre[i];
@@ -210,38 +214,52 @@ static int mw_for(int w) {
     return 0;
 }
 
-int ksolve_strided_launch(const LineGeom& g, const BandLU& f, const double* in, double* out, hipStream_t st) {
-    const int64_t nt = g.no * g.n2;
-    if (nt == 0 || f.n == 0) return 0;
-    const dim3 grid((unsigned)((nt + 255) / 256));
+// (kl, K) pairs with compiled-in bandwidths: GLT collocation p = 2, 3 (1, 2) and
+// p = 4, 5 (2, 4), the symmetric p = 3 recipe (3, 6); anything else runs the
+// run-time-bandwidth kernels with a window of MW >= max(kl, K).
+template <template <int, int, int> class L, typename... A>
+static int dispatch(const BandLU& f, A&&... a) {
+    if (f.kl == 1 && f.K == 2) return L<2, 1, 2>::run(a...);
+    if (f.kl == 2 && f.K == 4) return L<4, 2, 4>::run(a...);
+    if (f.kl == 3 && f.K == 6) return L<8, 3, 6>::run(a...);
     switch (mw_for(std::max(f.kl, f.K))) {
-        case 2: hipLaunchKernelGGL(ksolve_strided_kernel<2>, grid, dim3(256), 0, st, g, f, in, out); break;
-        case 4: hipLaunchKernelGGL(ksolve_strided_kernel<4>, grid, dim3(256), 0, st, g, f, in, out); break;
-        case 8: hipLaunchKernelGGL(ksolve_strided_kernel<8>, grid, dim3(256), 0, st, g, f, in, out); break;
-        case 16: hipLaunchKernelGGL(ksolve_strided_kernel<16>, grid, dim3(256), 0, st, g, f, in, out); break;
+        case 2: return L<2, -1, -1>::run(a...);
+        case 4: return L<4, -1, -1>::run(a...);
+        case 8: return L<8, -1, -1>::run(a...);
+        case 16: return L<16, -1, -1>::run(a...);
         default: set_error("kron solve: kl + ku must be <= 16"); return 1;
     }
-    return 0;
 }
 
-template <int MW>
-static void rows_launch_mw(const RowLines& g, const BandLU& f, const double* in, double* out, hipStream_t st) {
-    const dim3 grid((unsigned)((g.nrows + 64 * kRowWaves - 1) / (64 * kRowWaves)));
-    hipLaunchKernelGGL((ksolve_rows_kernel<MW, 0>), grid, dim3(64 * kRowWaves), 0, st, g, f, in, out);
-    hipLaunchKernelGGL((ksolve_rows_kernel<MW, 1>), grid, dim3(64 * kRowWaves), 0, st, g, f,
-                       (const double*)out, out);
+template <int MW, int CKL, int CK>
+struct StridedL {
+    static int run(const LineGeom& g, const BandLU& f, const double* in, double* out, hipStream_t st) {
+        const int64_t nt = g.no * g.n2;
+        hipLaunchKernelGGL((ksolve_strided_kernel<MW, CKL, CK>), dim3((unsigned)((nt + 255) / 256)), dim3(256), 0,
+                           st, g, f, in, out);
+        return 0;
+    }
+};
+
+template <int MW, int CKL, int CK>
+struct RowsL {
+    static int run(const RowLines& g, const BandLU& f, const double* in, double* out, hipStream_t st) {
+        const dim3 grid((unsigned)((g.nrows + 64 * kRowWaves - 1) / (64 * kRowWaves)));
+        hipLaunchKernelGGL((ksolve_rows_kernel<MW, 0, CKL, CK>), grid, dim3(64 * kRowWaves), 0, st, g, f, in, out);
+        hipLaunchKernelGGL((ksolve_rows_kernel<MW, 1, CKL, CK>), grid, dim3(64 * kRowWaves), 0, st, g, f,
+                           (const double*)out, out);
+        return 0;
+    }
+};
+
+int ksolve_strided_launch(const LineGeom& g, const BandLU& f, const double* in, double* out, hipStream_t st) {
+    if (g.no * g.n2 == 0 || f.n == 0) return 0;
+    return dispatch<StridedL>(f, g, f, in, out, st);
 }
 
 int ksolve_rows_launch(const RowLines& g, const BandLU& f, const double* in, double* out, hipStream_t st) {
     if (g.nrows == 0 || f.n == 0) return 0;
-    switch (mw_for(std::max(f.kl, f.K))) {
-        case 2: rows_launch_mw<2>(g, f, in, out, st); break;
-        case 4: rows_launch_mw<4>(g, f, in, out, st); break;
-        case 8: rows_launch_mw<8>(g, f, in, out, st); break;
-        case 16: rows_launch_mw<16>(g, f, in, out, st); break;
-        default: set_error("kron solve: kl + ku must be <= 16"); return 1;
-    }
-    return 0;
+    return dispatch<RowsL>(f, g, f, in, out, st);
 }
 
 // ---- host: banded LU with partial pivoting (LAPACK dgbtf2, 0-based) --------

@@ -16,6 +16,11 @@ Cycle (`sources/mg_jac.py:84-119`):
     xf = xf + P xc ; ghost exchange                               # correction
     xf2, info_pos = pcg(Af, damped_jacobi, bf, x0=xf, tol, maxiter)  # post-smoothing
 
+``post_smoother="glt"`` runs `sources/mg_glt.py:113-123` instead: the post-smoother
+is ``pcg_glt(Af, M1, M2, bf, x0=xf, tol, maxiter=p+1)``, preconditioned by the
+Kronecker direct solve with the cardinal-spline collocation matrices
+(``collocation_cardinal_splines(p, n)`` per axis, `sources/mg_glt.py:115-118`).
+
 Grid convention: ``ncells_fine`` / ``ncells_coarse`` count CELLS; the knot
 vectors have ``n = N + p`` basis functions.  (The reference passes ``nc = 8``
 as a number of basis functions to ``make_open_knots``; with a uniform fine
@@ -68,8 +73,12 @@ class TwoLevelVCycle:
 
     def __init__(self, p: int, ncells_fine: int, ncells_coarse: int = 8, ndim: int = 3, *,
                  dist=None, mass_coef: float = 1.0, device=None, knots_fine=None, knots_coarse=None,
-                 tol: float = 1e-6, maxiter: int = 10, chunk: int = 0, align: bool = True):
+                 tol: float = 1e-6, maxiter: int = 10, chunk: int = 0, align: bool = True,
+                 post_smoother: str = "jacobi"):
         self.p, self.ndim = int(p), int(ndim)
+        if post_smoother not in ("jacobi", "glt"):
+            raise ValueError("post_smoother must be 'jacobi' (mg_jac.py) or 'glt' (mg_glt.py)")
+        self.post_smoother = post_smoother
         Tc = uniform_knots(p, ncells_coarse) if knots_coarse is None else np.asarray(knots_coarse, float)
         Tf = uniform_knots(p, ncells_fine) if knots_fine is None else np.asarray(knots_fine, float)
         T, Ts, P1 = two_level_setup_1d(p, Tf, Tc)
@@ -97,6 +106,11 @@ class TwoLevelVCycle:
         self.rc = torch.empty(Ac.shape[0], dtype=F64, device=dev)
         self.xc = torch.empty(Ac.shape[0], dtype=F64, device=dev)
         self.tol, self.maxiter = tol, maxiter
+        self.glt = None
+        if post_smoother == "glt":
+            from .splines import array_to_mat_stencil, collocation_cardinal_splines
+            Cm = array_to_mat_stencil(n, p, collocation_cardinal_splines(p, n))
+            self.glt = [Cm] * ndim
 
     @property
     def ndof(self) -> int:
@@ -125,7 +139,11 @@ class TwoLevelVCycle:
         xc = self.coarse_solve(rc, self.xc)
         self.transfer.prolong_add(xc, xf)
         xf.update_ghost_regions()
-        xf2, info_pos = pcg(A, damped_jacobi, bf, x0=xf, tol=self.tol, maxiter=self.maxiter)
+        if self.glt is not None:
+            from .solvers import pcg_kron
+            xf2, info_pos = pcg_kron(A, self.glt, bf, x0=xf, tol=self.tol, maxiter=self.p + 1)
+        else:
+            xf2, info_pos = pcg(A, damped_jacobi, bf, x0=xf, tol=self.tol, maxiter=self.maxiter)
         return xf2, info_pre, info_pos
 
 

@@ -121,6 +121,24 @@ def test_two_level_vcycle(gpu, ndim, p, Nf, Nc, align):
     assert rel(x.to_local_numpy(), xr) <= tol
 
 
+@pytest.mark.parametrize("ndim,p,Nf,Nc", [(2, 1, 16, 8), (2, 3, 32, 8), (3, 2, 16, 8), (3, 3, 24, 8)])
+def test_two_level_vcycle_glt_post(gpu, ndim, p, Nf, Nc):
+    """`sources/mg_glt.py`: pre pcg + damped Jacobi, coarse correction, GLT
+    post-smoother pcg_glt(maxiter = p + 1) with the collocation Kron solve."""
+    from poms_amd.mg import TwoLevelVCycle
+    from poms_amd.splines import collocation_cardinal_splines, dense_to_band, band_to_dense
+    mg = TwoLevelVCycle(p, Nf, Nc, ndim=ndim, post_smoother="glt")
+    b = mg.rhs_ones()
+    x, ipre, ipos = mg.cycle(b)
+    Cd = band_to_dense(dense_to_band(collocation_cardinal_splines(p, mg.n), p))
+    Ms, Ks = [mg.M1d] * ndim, [mg.K1d] * ndim
+    ones = np.ones((mg.n,) * ndim)
+    xr, rpre, rpos = orc.vcycle_two_level(Ms, Ks, mg.P1, ones, glt=[Cd] * ndim)
+    xr2, _, _ = orc.vcycle_two_level(Ms, Ks, mg.P1, ones, glt=[Cd] * ndim, reorder=True)
+    tol = max(1e-9, 20.0 * rel(xr2, xr))
+    assert ipre["niter"] == rpre["niter"] and ipos["niter"] == rpos["niter"] <= p + 1
+    assert rel(x.to_local_numpy(), xr) <= tol
+
 def test_transfer_restrict_prolong(gpu):
     from poms_amd.mg import TwoLevelVCycle
     import torch
