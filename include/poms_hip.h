@@ -84,6 +84,20 @@ int         poms_synchronize(poms_ctx* ctx, void* stream);
 int poms_op_create(poms_ctx* ctx, int ndim, const poms_layout* layout, int form,
                    int pmax, const double* const* factors, int64_t g0,
                    int64_t n0_global, poms_op** op);
+/* General stencil operator (spl StencilMatrix with its own coefficients per row,
+ * `slides/content.tex:285-290`): v[i] = sum_k M[i, k] u[i + k - p].  `data` is a
+ * HOST array in the spl `StencilMatrix._data` layout of the local slab: the padded
+ * local extents (n_d + 2 pads_d, C order), then 2 pads_d + 1 offsets per axis
+ * (2D: (n1+2p1, n2+2p2, 2p1+1, 2p2+1)); the stencil half-widths are the layout's
+ * pads.  Coefficients are copied to the device once as one plane per offset.
+ * Every poms_op_* entry point works on it (apply, residual, Jacobi sweep with norm
+ * and x_out.b, apply + x.y, diag_scale, run_reduce, run_dist) except the
+ * two-sweeps-from-zero epilogue.
+ * Replaces: `StencilMatrix.dot` of the operator `assembly_2d` builds
+ * (`sources/matrix_assembler.py:84-179`), called at `sources/solvers.py:85,103,
+ * 109,209` and `sources/mg_jac.py:93`.                                         */
+int poms_op_create_stencil(poms_ctx* ctx, int ndim, const poms_layout* layout, const double* data,
+                           int64_t g0, int64_t n0_global, poms_op** op);
 int poms_op_destroy(poms_op* op);
 /* Planes per workgroup along axis 0 (3D); 0 = automatic. */
 int poms_op_set_chunk(poms_op* op, int chunk);

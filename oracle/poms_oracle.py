@@ -26,7 +26,7 @@ from scipy.sparse.linalg import splu
 __all__ = [
     "band_dense", "band_csr", "kron_dot_pyccel_2d", "kron_product_apply", "kron_sum_apply",
     "kron_sum_csr", "kron_sum_diag", "residual", "damped_jacobi", "jacobi", "pcg",
-    "vcycle_two_level", "knots_to_insert", "to_bnd", "gbtrf", "gbtrs", "kron_solve", "pcg_glt",
+    "vcycle_two_level", "knots_to_insert", "to_bnd", "gbtrf", "gbtrs", "kron_solve", "pcg_glt", "crl",
     "cardinal_bspline", "collocation_cardinal_splines",
 ]
 
@@ -175,6 +175,32 @@ def damped_jacobi(apply, diag, b, x0=None, tol=1e-6, maxiter=10, return_info=Fal
     if return_info:
         return x, {"niter": k, "success": nrmr < tol_sqr, "res_norm": sqrt(nrmr)}
     return x
+
+
+def crl(apply, b, x0=None, tol=1e-5, maxiter=1000):
+    """`sources/solvers.py:3-65` (conjugate residual; stop test ``s.r < tol**2``, :38)."""
+    x = 0.0 * b.copy() if x0 is None else x0.copy()
+    r = b - apply(x)
+    p = r.copy()
+    q = apply(p)
+    s = q.copy()
+    sr = float(np.vdot(s, r))
+    tol_sqr = tol ** 2
+    k = 0
+    for k in range(1, maxiter + 1):
+        if sr < tol_sqr:
+            k -= 1
+            break
+        alpha = sr / float(np.vdot(q, q))
+        x = x + alpha * p
+        r = r - alpha * q
+        s = apply(r)
+        srold = sr
+        sr = float(np.vdot(s, r))
+        beta = sr / srold
+        p = r + beta * p
+        q = s + beta * q
+    return x, {"niter": k, "success": sr < tol_sqr, "res_norm": sqrt(sr)}
 
 
 def pcg(apply, psolve, b, x0=None, tol=1e-6, maxiter=100):

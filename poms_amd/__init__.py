@@ -14,24 +14,24 @@ from .splines import (assemble_1d, collocation_cardinal_splines, make_open_knots
                       matrix_multi_stages, uniform_knots)
 
 __all__ = [
-    "StencilVectorSpace", "StencilVector", "StencilMatrix1D", "KronOperator",
+    "StencilVectorSpace", "StencilVector", "StencilMatrix1D", "KronOperator", "StencilMatrix",
     "pcg", "damped_jacobi", "jacobi", "kron_dot_v2", "kron_dot_pyccel_2d",
     "knots_to_insert", "KronTransfer", "TwoLevelVCycle", "SlabDistribution",
     "assemble_1d", "make_open_knots", "uniform_knots", "matrix_multi_stages",
     "pcg_glt", "pcg_kron", "KronSolver", "kron_solve_serial", "kron_solve_par", "to_bnd",
-    "collocation_cardinal_splines", "MultilevelVCycle",
+    "collocation_cardinal_splines", "MultilevelVCycle", "crl",
 ]
 
 
 def __getattr__(name):
     # Lazy: torch-dependent modules load on first use.
-    if name in ("StencilVectorSpace", "StencilVector", "StencilMatrix1D", "KronOperator"):
+    if name in ("StencilVectorSpace", "StencilVector", "StencilMatrix1D", "KronOperator", "StencilMatrix"):
         from . import stencil
         return getattr(stencil, name)
     if name in ("KronSolver", "kron_solve_serial", "kron_solve_par", "to_bnd"):
         from . import kron_solve
         return getattr(kron_solve, name)
-    if name in ("pcg", "damped_jacobi", "jacobi", "pcg_glt", "pcg_kron"):
+    if name in ("pcg", "damped_jacobi", "jacobi", "pcg_glt", "pcg_kron", "crl"):
         from . import solvers
         return getattr(solvers, name)
     if name in ("kron_dot_v2", "kron_dot_pyccel_2d"):

@@ -8,10 +8,11 @@ namespace poms {
 
 constexpr int kBlock = 256;  // 4 wave64s per workgroup
 
-enum Form : int { FORM_SINGLE = 0, FORM_SUM = 1 };
+enum Form : int { FORM_SINGLE = 0, FORM_SUM = 1, FORM_STENCIL = 2 };
 enum Epi : int { EPI_APPLY = 0, EPI_RESID = 1, EPI_JACOBI = 2,
                  EPI_JACOBI0 = 3,   /* two damped-Jacobi sweeps from x0 = 0 (x planes = b) */
-                 EPI_APPLYDOT = 4   /* y = A x and per-block sums of x . y              */ };
+                 EPI_APPLYDOT = 4,  /* y = A x and per-block sums of x . y              */
+                 EPI_DIAG = 5       /* x = scale b / diag(A) (general stencil form)    */ };
 
 // Geometry of one fused Kronecker launch (all extents local to this rank's slab).
 struct KronGeom {
@@ -37,6 +38,18 @@ __device__ __forceinline__ void chunk_planes(const KronGeom& g, int ch, int& z0,
         z1 = min(z0 + g.chunk, g.z2_end);
     }
 }
+
+// One launch of the general-stencil kernel (stencil_general.hip): owned planes
+// [z_begin, z_end) u [z2_begin, z2_end) of the local slab.
+struct StencilGeom {
+    int64_t s0, s1;          // plane / row strides of the padded vectors
+    int n0, n1, n2;          // local interior extents
+    int pd0, pd1, pd2;       // storage pads
+    int p0, p1, p2;          // stencil half-widths
+    int w0, w1, w2;          // 2 p_d + 1 (1 on unused axes)
+    int64_t cstride;         // doubles per coefficient plane (n0 n1 n2)
+    int z_begin, z_end, z2_begin, z2_end;
+};
 
 // Padded row layout used by the row-wise vector kernels.
 struct RowGeom {

@@ -38,6 +38,9 @@ int diag_scale_launch(bool is3d, int form, const RowGeom& g, int P, int g0, doub
                       const double* a1, const double* b1, const double* a2, const double* b2,
                       double* partial, hipStream_t st, int* nblk_out);
 int dense_matvec_launch(int n, const double* M, const double* x, double* y, hipStream_t st);
+int stencil_launch(int epi, const StencilGeom& g, const double* coef, const double* x, double* y,
+                   const double* b, double omega, double* partial, double* partial2, int max_blocks,
+                   hipStream_t st, int* nblk_out);
 int transfer_pass_launch(bool restrict_dir, int ncm, const AxisPass& ps, const double* Pm,
                          const double* in, double* out, hipStream_t st);
 int transfer_band_launch(bool restrict_dir, const AxisPass& ps, const double* band, const int* lo, int w,
@@ -73,6 +76,8 @@ struct poms_op {
     int variant = 0;
     bool v2_ok = false;
     ToepConst tc{};
+    double* coef = nullptr;   // FORM_STENCIL: (2p+1)^d coefficient planes of the owned rows
+    int sp[3]{};              // FORM_STENCIL: stencil half-widths per axis
 };
 
 static int resolve_variant(const poms_op* o, int epi);
@@ -306,9 +311,50 @@ int poms_op_create(poms_ctx* ctx, int ndim, const poms_layout* layout, int form,
     return 0;
 }
 
+int poms_op_create_stencil(poms_ctx* ctx, int ndim, const poms_layout* layout, const double* data,
+                           int64_t g0, int64_t n0_global, poms_op** op) {
+    if (!ctx || !op || !data || !layout_ok(layout)) { set_error("poms_op_create_stencil: bad argument"); return 1; }
+    if (ndim < 1 || ndim > 3) { set_error("poms_op_create_stencil: ndim 1..3"); return 1; }
+    for (int d = 0; d < 3 - ndim; ++d)
+        if (layout->n[d] != 1 || layout->pads[d] != 0) {
+            set_error("poms_op_create_stencil: unused leading axes need n = 1, pads = 0");
+            return 1;
+        }
+    const RowGeom r = row_geom(layout);
+    const int p[3] = {r.pd0, r.pd1, r.pd2};
+    const int w[3] = {2 * p[0] + 1, 2 * p[1] + 1, 2 * p[2] + 1};
+    const int64_t W = (int64_t)w[0] * w[1] * w[2];
+    const int64_t cst = (int64_t)r.n0 * r.n1 * r.n2;
+    if (W * cst * 8 > ((int64_t)1 << 40)) { set_error("poms_op_create_stencil: coefficients too large"); return 1; }
+    POMS_HIP_CHECK(hipSetDevice(ctx->device));
+    // spl layout: rows over the padded local extents, then the W offsets of each row
+    const int64_t P1 = r.n1 + 2 * p[1], P2 = r.n2 + 2 * p[2];
+    std::vector<double> soa((size_t)(W * cst));
+    for (int64_t i0 = 0; i0 < r.n0; ++i0)
+        for (int64_t i1 = 0; i1 < r.n1; ++i1)
+            for (int64_t i2 = 0; i2 < r.n2; ++i2) {
+                const int64_t row = ((i0 + p[0]) * P1 + (i1 + p[1])) * P2 + (i2 + p[2]);
+                const int64_t lin = (i0 * r.n1 + i1) * r.n2 + i2;
+                const double* src = data + row * W;
+                for (int64_t k = 0; k < W; ++k) soa[(size_t)(k * cst + lin)] = src[k];
+            }
+    auto* o = new poms_op();
+    o->ctx = ctx;
+    o->ndim = ndim;
+    o->form = FORM_STENCIL;
+    o->pmax = std::max(p[0], std::max(p[1], p[2]));
+    o->L = *layout;
+    o->g0 = ndim == 3 ? g0 : 0;
+    o->n0g = ndim == 3 ? n0_global : 1;
+    for (int d = 0; d < 3; ++d) o->sp[d] = p[d];
+    if (upload(soa.data(), soa.size(), &o->coef)) { poms_op_destroy(o); return 1; }
+    *op = o;
+    return 0;
+}
+
 int poms_op_destroy(poms_op* o) {
     if (!o) return 0;
-    for (double* p : {o->a0t, o->b0t, o->a1, o->b1, o->a2, o->b2, o->dg2a, o->dg2b, o->rdiag0})
+    for (double* p : {o->a0t, o->b0t, o->a1, o->b1, o->a2, o->b2, o->dg2a, o->dg2b, o->rdiag0, o->coef})
         if (p) (void)hipFree(p);
     delete o;
     return 0;
@@ -427,7 +473,33 @@ static int op_geom(poms_op* o, int64_t zb, int64_t ze, KronGeom& g, int v = -1, 
 }
 
 // variants whose Jacobi epilogue also accumulates x_out . b (v3 and v4 kernels)
-static bool fused_dot_ok(const poms_op* o) { return o->variant >= 4 && o->variant <= 10; }
+static bool fused_dot_ok(const poms_op* o) {
+    return o->form == FORM_STENCIL || (o->variant >= 4 && o->variant <= 10);
+}
+
+// General-stencil launch (FORM_STENCIL): the epilogues of op_run plus EPI_DIAG.
+static int stencil_run(poms_op* o, int epi, double omega, const double* x, double* y, const double* b,
+                       int64_t zb, int64_t ze, int want_norm, void* stream, int want_dot, int64_t zb2,
+                       int64_t ze2) {
+    if (epi == EPI_JACOBI0) { set_error("general stencil: no two-sweeps-from-zero epilogue"); return 1; }
+    if (want_dot && epi != EPI_JACOBI && epi != EPI_APPLYDOT) { set_error("general stencil: dot needs Jacobi / apply+dot"); return 1; }
+    const RowGeom r = row_geom(&o->L);
+    if (zb < 0 || ze > r.n0 || zb > ze || zb2 < 0 || ze2 > r.n0 || zb2 > ze2) { set_error("general stencil: bad plane range"); return 1; }
+    StencilGeom g{r.s0, r.s1, r.n0, r.n1, r.n2, r.pd0, r.pd1, r.pd2, o->sp[0], o->sp[1], o->sp[2],
+                  2 * o->sp[0] + 1, 2 * o->sp[1] + 1, 2 * o->sp[2] + 1, (int64_t)r.n0 * r.n1 * r.n2,
+                  (int)zb, (int)ze, (int)zb2, (int)ze2};
+    const int maxb = (int)(kScratch / 2);
+    int nb = 0;
+    double* scr = o->ctx->scratch;
+    const bool red = want_norm || want_dot || epi == EPI_APPLYDOT;
+    if (stencil_launch(epi, g, o->coef, x, y, b, omega, want_norm ? scr : nullptr,
+                       (want_dot || epi == EPI_APPLYDOT) ? scr + std::min<int64_t>(maxb, std::max<int64_t>(1, ((int64_t)(ze - zb + ze2 - zb2) * r.n1 * r.n2 + 255) / 256)) : nullptr,
+                       maxb, as_stream(stream), &nb))
+        return 1;
+    POMS_HIP_CHECK(hipGetLastError());
+    o->last_partials = red ? nb : 0;
+    return 0;
+}
 
 // The kernel variant one launch of epilogue `epi` runs (see op_run).
 static int resolve_variant(const poms_op* o, int epi) {
@@ -450,6 +522,8 @@ static int op_run(poms_op* o, int epi, double omega, const double* x, double* y,
                   int64_t zb2 = 0, int64_t ze2 = 0) {
     if (!o || !x || !y) { set_error("null operator or vector"); return 1; }
     if (epi != EPI_APPLY && !b) { set_error("null right-hand side"); return 1; }
+    if (o->form == FORM_STENCIL)
+        return stencil_run(o, epi, omega, x, y, b, zb, ze, want_norm, stream, want_dot, zb2, ze2);
     if (epi == EPI_APPLYDOT && !(o->variant == 4 || o->variant == 5 || o->variant == 6 || o->variant == 8 ||
                                  o->variant == 9 || o->variant == 10)) {
         set_error("apply + x.y: kernel variants 4, 5, 6, 8, 9, 10 only");
@@ -527,7 +601,7 @@ int poms_op_apply_dot(poms_op* op, const double* x, double* y, int64_t zb, int64
 int poms_op_apply_dot_supported(poms_op* op, int* yes) {
     if (!op || !yes) { set_error("poms_op_apply_dot_supported: null argument"); return 1; }
     const int v = op->variant;
-    *yes = (v == 4 || v == 5 || v == 6 || v == 8 || v == 9 || v == 10) ? 1 : 0;
+    *yes = (op->form == FORM_STENCIL || v == 4 || v == 5 || v == 6 || v == 8 || v == 9 || v == 10) ? 1 : 0;
     return 0;
 }
 
@@ -542,7 +616,8 @@ int poms_op_jacobi_from_zero(poms_op* op, double omega, const double* b, double*
 int poms_op_from_zero_supported(poms_op* op, int* yes) {
     if (!op || !yes) { set_error("poms_op_from_zero_supported: null argument"); return 1; }
     const int64_t bytes = (int64_t)(op->L.n[0] + 2 * op->L.pads[0]) * row_geom(&op->L).s0 * 8;
-    *yes = (op->ndim == 3 && (op->variant == 8 || op->variant == 9 || op->variant == 10) && bytes < 0x7ffffff0LL) ? 1 : 0;
+    *yes = (op->ndim == 3 && op->form != FORM_STENCIL && (op->variant == 8 || op->variant == 9 || op->variant == 10) &&
+            bytes < 0x7ffffff0LL) ? 1 : 0;
     return 0;
 }
 
@@ -555,6 +630,8 @@ int poms_op_fused_dot_supported(poms_op* op, int* yes) {
 int poms_op_diag_scale(poms_op* o, double scale, const double* b, double* x, int want_norm,
                        void* stream) {
     if (!o || !b || !x) { set_error("poms_op_diag_scale: null argument"); return 1; }
+    if (o->form == FORM_STENCIL)
+        return stencil_run(o, EPI_DIAG, scale, b, x, b, 0, o->L.n[0], want_norm, stream, 0, 0, 0);
     const RowGeom g = row_geom(&o->L);
     int nb = 0;
     diag_scale_launch(o->ndim == 3, o->form, g, o->pmax, (int)o->g0, scale, b, x, o->a0t, o->b0t,

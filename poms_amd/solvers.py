@@ -10,6 +10,8 @@ Signatures, defaults, return conventions and stopping rules are those of
 * ``damped_jacobi(A, b, x0=None, tol=1e-6, maxiter=10, verbose=False) -> x``
   (:167-235), omega = 2/3, stop when ``dr.dr < tol**2`` *after* the update.
 * ``jacobi(A, b) -> x`` (:139-163).
+* ``crl(A, b, x0=None, tol=1e-5, maxiter=1000, verbose=False) -> (x, info)``
+  (:3-65): conjugate residual, stop when ``s.r < tol**2`` before the update.
 * ``pcg_glt(A, M1, M2, b, x0=None, tol=1e-6, maxiter=100, verbose=False) -> (x, info)``
   (:239-306): the same PCG with the Kronecker direct solve
   ``kron_solve_par(M2, M1, r)`` as preconditioner (:258, :290), factorised once
@@ -365,3 +367,45 @@ def pcg_glt(A, M1, M2, b, x0=None, tol=1e-6, maxiter=100, verbose=False):
     if b.space.ndim != 2:
         raise ValueError("pcg_glt is the 2D solver of the reference; use pcg_kron for other dimensions")
     return pcg_kron(A, (M2, M1), b, x0=x0, tol=tol, maxiter=maxiter, verbose=verbose)
+
+
+def crl(A, b, x0=None, tol=1e-5, maxiter=1000, verbose=False):
+    """Conjugate residual method (`sources/solvers.py:3-65`): device vectors, the
+    operator's fused residual / apply kernels, in-place vector updates."""
+    _check(A, b)
+    V = b.space
+    if x0 is None:
+        x = V.zeros()
+        r = V.empty().assign(b)          # b - A.0 = b exactly
+    else:
+        assert x0.shape == (A.shape[0],)
+        x = x0.copy()
+        r = A.residual(b, x)
+    p = r.copy()
+    q = A.dot(p)
+    s = q.copy()
+    sr = s.dot(r)
+    tol_sqr = tol ** 2
+    if verbose:
+        _print_header("CG solver:")
+        template = "| {:7d} | {:19.2e} |"
+    k = 0
+    for k in range(1, maxiter + 1):
+        if sr < tol_sqr:
+            k -= 1
+            break
+        alpha = sr / q.dot(q)
+        x.axpby_(alpha, p, 1.0)          # x = x + alpha p
+        r.axpby_(-alpha, q, 1.0)         # r = r - alpha q
+        A.dot(r, out=s)
+        srold = sr
+        sr = s.dot(r)
+        beta = sr / srold
+        p.axpby_(1.0, r, beta)           # p = r + beta p
+        q.axpby_(1.0, s, beta)           # q = s + beta q
+        if verbose:
+            print(template.format(k, sqrt(sr)))
+    if verbose:
+        print("+---------+---------------------+")
+    info = {"niter": k, "success": sr < tol_sqr, "res_norm": sqrt(sr)}
+    return x, info

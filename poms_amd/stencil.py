@@ -932,3 +932,150 @@ def _kron_all(ms):
     for m in ms[1:]:
         out = sp.kron(out, m, format="csr")
     return out.tocsr()
+
+
+class StencilMatrix(KronOperator):
+    """spl ``StencilMatrix(V, W=None)`` with its own coefficients per row
+    (`slides/content.tex:285-290`): ``v[i] = Σ_k M[i, k] u[i + k]``, ``k ∈ [-p, p]^d``.
+
+    ``_data`` is the host array in spl's layout (padded local rows, then the
+    ``2p+1`` offsets per axis); it is filled by ``M[i1, i2, k1, k2] = value`` (global
+    row indices, slices allowed) exactly as the reference's ``assembly_2d`` does
+    (`sources/matrix_assembler.py:84-179`), or from an assembled array with
+    :meth:`from_data`.  The coefficients go to the device (``poms_op_create_stencil``)
+    on the first device use after a change.  Every solver of :mod:`poms_amd.solvers`
+    accepts it as ``A`` (general-stencil kernel, ``csrc/stencil_general.hip``)."""
+
+    def __init__(self, V: StencilVectorSpace, W: StencilVectorSpace | None = None):
+        if W is not None and W is not V:
+            raise NotImplementedError("rectangular stencil matrices are not supported")
+        self.space, self.form = V, "stencil"
+        self.pmax = max(max(V.pads), 1)
+        self.bands = {}
+        self.timer = None
+        self._calls = 0
+        self._hh = C.c_void_p()
+        self._dirty = True
+        self._data = np.zeros(V.padded_shape + tuple(2 * p + 1 for p in V.pads))
+        self.pads = V.pads
+        self.starts, self.ends = V.starts, V.ends
+
+    @classmethod
+    def from_data(cls, V: StencilVectorSpace, data: np.ndarray) -> "StencilMatrix":
+        M = cls(V)
+        data = np.asarray(data, dtype=np.float64)
+        if data.shape != M._data.shape:
+            raise ValueError(f"stencil data must have the spl shape {M._data.shape}")
+        M._data[...] = data
+        return M
+
+    # the device handle, (re)created lazily after host-side changes
+    @property
+    def _h(self):
+        if self._dirty:
+            self._upload()
+        return self._hh
+
+    @_h.setter
+    def _h(self, v):
+        self._hh = v if v is not None else C.c_void_p()
+
+    def _upload(self):
+        V = self.space
+        if self._hh.value:
+            _lib.lib.poms_op_destroy(self._hh)
+            self._hh = C.c_void_p()
+        data = np.ascontiguousarray(self._data)
+        h = C.c_void_p()
+        g0 = V.starts[0] if V.ndim == 3 else 0
+        n0g = V.npts[0] if V.ndim == 3 else 1
+        _lib.call("poms_op_create_stencil", V.ctx, V.ndim, C.byref(V.layout), data.ctypes.data_as(C.c_void_p),
+                  g0, n0g, C.byref(h))
+        self._hh = h
+        self._dirty = False
+
+    def __del__(self):
+        h = getattr(self, "_hh", None)
+        if h is not None and h.value:
+            try:
+                _lib.lib.poms_op_destroy(h)
+            except Exception:
+                pass
+            self._hh = C.c_void_p()
+
+    # -- spl element access ----------------------------------------------------------
+    def _idx(self, key):
+        nd = self.space.ndim
+        if not isinstance(key, tuple) or len(key) != 2 * nd:
+            raise IndexError("expected (i..., k...) with one index and one offset per axis")
+        out = []
+        for d, (i, p, s) in enumerate(zip(key[:nd], self.pads, self.starts)):
+            if isinstance(i, slice):
+                if i != slice(None):
+                    a = (i.start if i.start is not None else s) - s + p
+                    b = (i.stop if i.stop is not None else self.ends[d] + 1) - s + p
+                    out.append(slice(a, b))
+                else:
+                    out.append(slice(p, p + self.space.local_npts[d]))
+            else:
+                out.append(int(i) - s + p)
+        for k, p in zip(key[nd:], self.pads):
+            if isinstance(k, slice):
+                out.append(slice((k.start if k.start is not None else -p) + p,
+                                 (k.stop if k.stop is not None else p + 1) + p))
+            else:
+                out.append(int(k) + p)
+        return tuple(out)
+
+    def __getitem__(self, key):
+        return self._data[self._idx(key)]
+
+    def __setitem__(self, key, value):
+        self._data[self._idx(key)] = value
+        self._dirty = True
+
+    def remove_spurious_entries(self):
+        """Zero the coefficients that couple to points outside the (non-periodic) grid."""
+        V = self.space
+        nd = V.ndim
+        for d in range(nd):
+            p = self.pads[d]
+            g = np.arange(V.local_npts[d]) + self.starts[d]
+            for k in range(-p, p + 1):
+                bad = (g + k < 0) | (g + k >= V.npts[d])
+                if bad.any():
+                    idx = [slice(None)] * (2 * nd)
+                    idx[d] = np.nonzero(bad)[0] + p
+                    idx[nd + d] = k + p
+                    self._data[tuple(idx)] = 0.0
+        self._dirty = True
+
+    def tosparse(self):
+        """Global sparse matrix of the local rows (small sizes)."""
+        import scipy.sparse as sp
+        V = self.space
+        nd = V.ndim
+        rows, cols, vals = [], [], []
+        W = [2 * p + 1 for p in self.pads]
+        inner = self._data[tuple(slice(p, p + n) for p, n in zip(self.pads, V.local_npts))]
+        grid = np.stack(np.meshgrid(*[np.arange(n) + s for n, s in zip(V.local_npts, self.starts)],
+                                    indexing="ij"), axis=-1).reshape(-1, nd)
+        flat = inner.reshape(-1, int(np.prod(W)))
+        for kk, ks in enumerate(np.ndindex(*W)):
+            off = np.array(ks) - np.array(self.pads)
+            tgt = grid + off
+            ok = np.all((tgt >= 0) & (tgt < np.array(V.npts)), axis=1) & (flat[:, kk] != 0.0)
+            rows.append(np.ravel_multi_index(grid[ok].T, V.npts))
+            cols.append(np.ravel_multi_index(tgt[ok].T, V.npts))
+            vals.append(flat[ok, kk])
+        n = V.dimension
+        return sp.csr_matrix((np.concatenate(vals), (np.concatenate(rows), np.concatenate(cols))), shape=(n, n))
+
+    def tocsr(self):
+        return self.tosparse()
+
+    def toarray(self):
+        return self.tosparse().toarray()
+
+    def diagonal_axes(self):
+        raise NotImplementedError("a general stencil has no per-axis factors")

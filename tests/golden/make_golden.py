@@ -5,7 +5,7 @@ Imports the reference's own Python (read-only, from /root/reference):
   * `pyccel/pyccel_functions.py`  -> kron_dot_pyccel_2d (the native Kron kernel)
   * `sources/utils.py`            -> populate_1d_matrix / kron_dot_ref
   * `sources/matrix_assembler.py` -> assembly_2d, assembly_1d
-  * `sources/solvers.py`          -> pcg, damped_jacobi, jacobi
+  * `sources/solvers.py`          -> pcg, damped_jacobi, jacobi, crl
   * `sources/multilevels.py`      -> knots_to_insert
   * `sources/kron_product.py`     -> kron_solve_serial / kron_solve_par / to_bnd
   * `pyccel/pyccel_functions.py`  -> kron_solve_serial_pyccel_2d, kron_solve_par_bnd_pyccel_2d/_3d
@@ -155,6 +155,10 @@ def golden_solvers():
             x, info = ref_solvers.pcg(A, ref_solvers.damped_jacobi, rhs, tol=1e-6, maxiter=10)
             res["pcg_mgjac"] = x.toarray()
             res["pcg_mgjac_info"] = [info["niter"], float(info["success"]), info["res_norm"]]
+            for m, tl in ((3, 0.0), (1000, 1e-5)):      # conjugate residual, `sources/solvers.py:3-65`
+                x, info = ref_solvers.crl(A, rhs, tol=tl, maxiter=m)
+                res[f"crl_m{m}"] = x.toarray()
+                res[f"crl_m{m}_info"] = [info["niter"], float(info["success"]), info["res_norm"]]
             res["p"], res["ne"] = p, ne
             out[key] = res
     with open(HERE / "solvers_2d.npz", "wb") as f:

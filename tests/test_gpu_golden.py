@@ -21,6 +21,20 @@ def rel(a, b):
     return float(np.linalg.norm((a - b).ravel()) / max(np.linalg.norm(b.ravel()), 1e-300))
 
 
+def _check_crl(info, ref, x, xref, m, rhs):
+    """Fixed-count CR iterates agree to 1e-10.  Run to convergence (tol = 1e-5 on
+    s.r, `sources/solvers.py:38`) the stop test reads a quantity near its
+    threshold, so 1-ulp operator differences can move the stop by one iteration;
+    the converged iterates then agree to the solver tolerance."""
+    assert info["success"] == bool(ref[1]), (rhs, m)
+    if m == 3:
+        assert info["niter"] == int(ref[0]), (rhs, m)
+        assert rel(x, xref) <= 1e-10, (rhs, m)
+    else:
+        assert abs(info["niter"] - int(ref[0])) <= 1, (rhs, m, info["niter"], ref[0])
+        assert rel(x, xref) <= 1e-6, (rhs, m)
+
+
 def test_kron_dot_pyccel_2d_golden(gpu, golden_dir):
     """poms_kron_dot_2d with the pyccel kernel's arguments == `pyccel/pyccel_functions.py:4-21` outputs."""
     from poms_amd.kron_product import kron_dot_pyccel_2d
@@ -59,7 +73,7 @@ def _pcg_bound(p, ne, c):
 @pytest.mark.parametrize("p,ne", [(1, 4), (1, 16), (3, 8)])
 def test_solvers_golden(gpu, golden_dir, p, ne):
     """damped_jacobi / pcg / jacobi on device == `sources/solvers.py` run by the reference."""
-    from poms_amd.solvers import damped_jacobi, jacobi, pcg
+    from poms_amd.solvers import crl, damped_jacobi, jacobi, pcg
     sol = load(golden_dir, "solvers_2d.npz")
     V, A = _space_op(p, ne)
     n = ne + p
@@ -82,6 +96,10 @@ def test_solvers_golden(gpu, golden_dir, p, ne):
         # 10 PCG iterations amplify 1-ulp operator differences; the bound is
         # the spread between the reference and the CPU oracle on our 1D factors
         assert rel(x.to_local_numpy().reshape(-1), c["pcg_mgjac"]) <= _pcg_bound(p, ne, c)
+        for m in (3, 1000):                      # conjugate residual (`sources/solvers.py:3-65`)
+            x, info = crl(A, b, tol=0.0 if m == 3 else 1e-5, maxiter=m)
+            ref = c[f"crl_m{m}_info"]
+            _check_crl(info, ref, x.to_local_numpy().reshape(-1), c[f"crl_m{m}"], m, rhs)
 
 
 def test_vcycle_golden(gpu, golden_dir):

@@ -151,6 +151,11 @@ def test_oracle_solvers_match_reference(golden_dir, p, ne):
         ref_info = c["pcg_mgjac_info"]
         assert info["niter"] == int(ref_info[0]) and info["success"] == bool(ref_info[1])
         assert rel(x, c["pcg_mgjac"]) <= 1e-9
+        for m in (3, 1000):                      # conjugate residual (`sources/solvers.py:3-65`)
+            x, info = orc.crl(apply, b, tol=0.0 if m == 3 else 1e-5, maxiter=m)
+            ref_info = c[f"crl_m{m}_info"]
+            assert info["niter"] == int(ref_info[0]) and info["success"] == bool(ref_info[1]), (rhs, m)
+            assert rel(x, c[f"crl_m{m}"]) <= (1e-10 if m == 3 else 1e-8), (rhs, m)
 
 
 def test_oracle_vcycle_matches_mg_jac(golden_dir):
