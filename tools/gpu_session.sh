@@ -13,7 +13,7 @@ what="${1:-all}"; shift || true
 stop() { echo "STOP: $1 (rc=$2)"; exit "$2"; }
 
 if [[ "$what" == "tests" || "$what" == "all" ]]; then
-  timeout -k 10 1200 python -m pytest tests -m gpu -q -p no:cacheprovider -rf > "$OUT/pytest_gpu.log" 2>&1
+  timeout -k 10 1500 python -u -m pytest tests -m gpu -v -p no:cacheprovider -rf --timeout 300 --timeout-method thread > "$OUT/pytest_gpu.log" 2>&1
   rc=$?; echo "pytest rc=$rc"; tail -5 "$OUT/pytest_gpu.log"
   [[ $rc -le 1 ]] || stop "pytest crashed or timed out" $rc
   timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > "$OUT/smoke.log" 2>&1
