@@ -98,6 +98,25 @@ int poms_op_create(poms_ctx* ctx, int ndim, const poms_layout* layout, int form,
  * 109,209` and `sources/mg_jac.py:93`.                                         */
 int poms_op_create_stencil(poms_ctx* ctx, int ndim, const poms_layout* layout, const double* data,
                            int64_t g0, int64_t n0_global, poms_op** op);
+/* On-device assembly of the variable-coefficient operator
+ * -div(a grad u) + c u on a tensor B-spline space into a general-stencil operator:
+ *   M[i, j] = sum_elements sum_quadrature w (c phi_i phi_j + a grad phi_i . grad phi_j),
+ * per element the quadrature sum first, as `assembly_2d` (`sources/matrix_assembler.py:
+ * 84-179`, a = c = 1, which this reproduces).  Per used axis d (HOST arrays): nel[d]
+ * elements (non-empty knot spans) with nq[d] Gauss points; first[d][e] = global index
+ * of element e's first basis function (span - p); es[d][i] / ee[d][i] = first / last
+ * element of basis function i's support (nglob[d] entries); basis[d] =
+ * (nel, nq, p+1, 2) values and first derivatives; weights[d] = (nel, nq) weights with
+ * the element Jacobian.  p[d] must equal layout->pads[d].  a_q, c_q: DEVICE arrays of
+ * the coefficients at every quadrature point, C order over (e0 q0, e1 q1, e2 q2) of
+ * the GLOBAL grid, or NULL for a = 1, c = mass_coef.  Axis 0 may be a slab (g0).    */
+int poms_op_assemble_stencil(poms_ctx* ctx, int ndim, const poms_layout* layout, const int* nel, const int* nq,
+                             const int* p, const int* const* first, const int* const* es, const int* const* ee,
+                             const double* const* basis, const double* const* weights, const int64_t* nglob,
+                             const double* a_q, const double* c_q, double mass_coef, int64_t g0, poms_op** op);
+/* The coefficients of a general-stencil operator in the spl StencilMatrix._data
+ * layout (the layout poms_op_create_stencil takes), HOST output.               */
+int poms_op_stencil_data(poms_op* op, double* data_host);
 int poms_op_destroy(poms_op* op);
 /* Planes per workgroup along axis 0 (3D); 0 = automatic. */
 int poms_op_set_chunk(poms_op* op, int chunk);

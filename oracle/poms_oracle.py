@@ -27,7 +27,7 @@ __all__ = [
     "band_dense", "band_csr", "kron_dot_pyccel_2d", "kron_product_apply", "kron_sum_apply",
     "kron_sum_csr", "kron_sum_diag", "residual", "damped_jacobi", "jacobi", "pcg",
     "vcycle_two_level", "knots_to_insert", "to_bnd", "gbtrf", "gbtrs", "kron_solve", "pcg_glt", "crl",
-    "cardinal_bspline", "collocation_cardinal_splines",
+    "cardinal_bspline", "collocation_cardinal_splines", "assembly_varcoef",
 ]
 
 
@@ -334,6 +334,53 @@ def collocation_cardinal_splines(p: int, n: int) -> np.ndarray:
     cardinal B-spline sampled at the integers."""
     i = np.arange(n)
     return cardinal_bspline(p, (p + 1) / 2.0 + i[:, None] - i[None, :])
+
+
+# ---------------------------------------------------------------------------
+# Quadrature assembly: sources/matrix_assembler.py:84-179 (assembly_2d), in d
+# dimensions and with coefficient fields a, c at the quadrature points
+# ---------------------------------------------------------------------------
+def assembly_varcoef(knots, p, a=None, c=None, mass_coef=1.0):
+    """spl-layout stencil ``_data`` of ``-div(a grad u) + c u``: element loop, local
+    basis pairs, quadrature sum per element added into ``M[i, j - i]`` as
+    `sources/matrix_assembler.py:136-177` (a = c = 1 there).  Basis tables from the
+    spl stand-in's ``SplineSpace`` (its own Cox-de Boor evaluation).  ``a``/``c``:
+    arrays over the global quadrature grid ``(nel_0 nq_0, nel_1 nq_1, ...)`` or None."""
+    from itertools import product
+    from oracle.spl_standin import SplineSpace
+    S = [SplineSpace(pd, knots=np.asarray(T, float)) for T, pd in zip(knots, p)]
+    nd = len(S)
+    n = [s.nbasis for s in S]
+    nq = [s.quad_order for s in S]
+    out = np.zeros(tuple(ni + 2 * pi for ni, pi in zip(n, p)) + tuple(2 * pi + 1 for pi in p))
+    for es in np.ndindex(*[s.ne for s in S]):
+        first = [int(S[d].spans[es[d]]) - p[d] - 1 for d in range(nd)]
+        B = [S[d].basis[:, :, :, es[d]] for d in range(nd)]          # (p+1, 2, nq)
+        w = S[0].weights[:, es[0]]
+        for d in range(1, nd):
+            w = np.multiply.outer(w, S[d].weights[:, es[d]])
+        blk = tuple(slice(es[d] * nq[d], (es[d] + 1) * nq[d]) for d in range(nd))
+        ca = 1.0 if a is None else a[blk]
+        cc = mass_coef if c is None else c[blk]
+
+        def tens(il, der_axis):
+            t = B[0][il[0], 1 if der_axis == 0 else 0]
+            for d in range(1, nd):
+                t = np.multiply.outer(t, B[d][il[d], 1 if der_axis == d else 0])
+            return t
+
+        for il in product(*[range(pd + 1) for pd in p]):
+            bi = [tens(il, -1)] + [tens(il, d) for d in range(nd)]
+            for jl in product(*[range(pd + 1) for pd in p]):
+                bj = [tens(jl, -1)] + [tens(jl, d) for d in range(nd)]
+                grad = bi[1] * bj[1]
+                for d in range(2, nd + 1):
+                    grad = grad + bi[d] * bj[d]
+                v = float(np.sum((cc * bi[0] * bj[0] + ca * grad) * w))
+                i = [first[d] + il[d] for d in range(nd)]
+                j = [first[d] + jl[d] for d in range(nd)]
+                out[tuple(i[d] + p[d] for d in range(nd)) + tuple(j[d] - i[d] + p[d] for d in range(nd))] += v
+    return out
 
 
 # ---------------------------------------------------------------------------

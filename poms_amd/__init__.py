@@ -19,7 +19,7 @@ __all__ = [
     "knots_to_insert", "KronTransfer", "TwoLevelVCycle", "SlabDistribution",
     "assemble_1d", "make_open_knots", "uniform_knots", "matrix_multi_stages",
     "pcg_glt", "pcg_kron", "KronSolver", "kron_solve_serial", "kron_solve_par", "to_bnd",
-    "collocation_cardinal_splines", "MultilevelVCycle", "crl",
+    "collocation_cardinal_splines", "MultilevelVCycle", "crl", "assemble_stencil",
 ]
 
 
@@ -28,6 +28,9 @@ def __getattr__(name):
     if name in ("StencilVectorSpace", "StencilVector", "StencilMatrix1D", "KronOperator", "StencilMatrix"):
         from . import stencil
         return getattr(stencil, name)
+    if name == "assemble_stencil":
+        from .assembly import assemble_stencil
+        return assemble_stencil
     if name in ("KronSolver", "kron_solve_serial", "kron_solve_par", "to_bnd"):
         from . import kron_solve
         return getattr(kron_solve, name)

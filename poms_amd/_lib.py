@@ -56,6 +56,9 @@ _SIGS = {
     "poms_op_create": [_vp, _i, _LP, _i, _i, C.POINTER(C.c_void_p), _i64, _i64, _pp],
     "poms_op_destroy": [_vp],
     "poms_op_create_stencil": [_vp, _i, _LP, _vp, _i64, _i64, _pp],
+    "poms_op_assemble_stencil": [_vp, _i, _LP, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _d, _i64,
+                                 _pp],
+    "poms_op_stencil_data": [_vp, _vp],
     "poms_op_set_chunk": [_vp, _i],
     "poms_op_set_tile_cols": [_vp, _i],
     "poms_op_set_variant": [_vp, _i],

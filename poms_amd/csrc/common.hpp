@@ -51,6 +51,17 @@ struct StencilGeom {
     int z_begin, z_end, z2_begin, z2_end;
 };
 
+// One axis of an on-device quadrature assembly (stencil_general.hip): elements
+// (non-empty knot spans), nq Gauss points each, the p+1 local B-splines.
+struct AssembleAxis {
+    const int* first;      // nel: global index of the element's first basis function
+    const int* es;         // n  : first element of basis function i's support
+    const int* ee;         // n  : last element of basis function i's support
+    const double* basis;   // nel*nq*(p+1)*2: value, derivative
+    const double* w;       // nel*nq: quadrature weights (with the element Jacobian)
+    int nel, nq, p, n;
+};
+
 // Padded row layout used by the row-wise vector kernels.
 struct RowGeom {
     int64_t s0, s1;

@@ -38,6 +38,9 @@ int diag_scale_launch(bool is3d, int form, const RowGeom& g, int P, int g0, doub
                       const double* a1, const double* b1, const double* a2, const double* b2,
                       double* partial, hipStream_t st, int* nblk_out);
 int dense_matvec_launch(int n, const double* M, const double* x, double* y, hipStream_t st);
+int assemble_launch(const AssembleAxis* ax, int g0, int nl0, const double* a_q, const double* c_q, double mass_coef,
+                    double* coef, hipStream_t st);
+int stencil_to_spl_launch(const StencilGeom& g, const double* coef, double* out, hipStream_t st);
 int stencil_launch(int epi, const StencilGeom& g, const double* coef, const double* x, double* y,
                    const double* b, double omega, double* partial, double* partial2, int max_blocks,
                    hipStream_t st, int* nblk_out);
@@ -349,6 +352,111 @@ int poms_op_create_stencil(poms_ctx* ctx, int ndim, const poms_layout* layout, c
     for (int d = 0; d < 3; ++d) o->sp[d] = p[d];
     if (upload(soa.data(), soa.size(), &o->coef)) { poms_op_destroy(o); return 1; }
     *op = o;
+    return 0;
+}
+
+// On-device assembly of -div(a grad u) + c u into a FORM_STENCIL operator.
+int poms_op_assemble_stencil(poms_ctx* ctx, int ndim, const poms_layout* layout, const int* nel, const int* nq,
+                             const int* p, const int* const* first, const int* const* es, const int* const* ee,
+                             const double* const* basis, const double* const* weights, const int64_t* nglob,
+                             const double* a_q, const double* c_q, double mass_coef, int64_t g0, poms_op** op) {
+    if (!ctx || !op || !layout_ok(layout) || !nel || !nq || !p || !first || !es || !ee || !basis || !weights || !nglob) {
+        set_error("poms_op_assemble_stencil: bad argument");
+        return 1;
+    }
+    if (ndim < 1 || ndim > 3) { set_error("poms_op_assemble_stencil: ndim 1..3"); return 1; }
+    const int d0 = 3 - ndim;
+    for (int d = 0; d < d0; ++d)
+        if (layout->n[d] != 1 || layout->pads[d] != 0) {
+            set_error("poms_op_assemble_stencil: unused leading axes need n = 1, pads = 0");
+            return 1;
+        }
+    for (int d = d0; d < 3; ++d) {
+        if (p[d] != layout->pads[d] || nel[d] < 1 || nq[d] < 1 || !first[d] || !es[d] || !ee[d] || !basis[d] ||
+            !weights[d]) {
+            set_error("poms_op_assemble_stencil: axis " + std::to_string(d) + " (degree must equal the pad)");
+            return 1;
+        }
+        if (d > 0 && nglob[d] != layout->n[d]) { set_error("poms_op_assemble_stencil: only axis 0 may be sliced"); return 1; }
+    }
+    if (ndim == 3 && (g0 < 0 || g0 + layout->n[0] > nglob[0])) { set_error("poms_op_assemble_stencil: bad slab"); return 1; }
+    POMS_HIP_CHECK(hipSetDevice(ctx->device));
+    const RowGeom r = row_geom(layout);
+    const int64_t W = (int64_t)(2 * r.pd0 + 1) * (2 * r.pd1 + 1) * (2 * r.pd2 + 1);
+    const int64_t cst = (int64_t)r.n0 * r.n1 * r.n2;
+    auto* o = new poms_op();
+    o->ctx = ctx;
+    o->ndim = ndim;
+    o->form = FORM_STENCIL;
+    o->pmax = std::max(r.pd0, std::max(r.pd1, r.pd2));
+    o->L = *layout;
+    o->g0 = ndim == 3 ? g0 : 0;
+    o->n0g = ndim == 3 ? nglob[0] : 1;
+    o->sp[0] = r.pd0; o->sp[1] = r.pd1; o->sp[2] = r.pd2;
+    std::vector<void*> tmp;
+    auto up_i = [&](const int* h, int64_t n) -> const int* {
+        void* d = nullptr;
+        if (hipMalloc(&d, std::max<int64_t>(n, 1) * sizeof(int)) != hipSuccess) return nullptr;
+        tmp.push_back(d);
+        if (hipMemcpy(d, h, n * sizeof(int), hipMemcpyHostToDevice) != hipSuccess) return nullptr;
+        return static_cast<const int*>(d);
+    };
+    auto up_d = [&](const double* h, int64_t n) -> const double* {
+        void* d = nullptr;
+        if (hipMalloc(&d, std::max<int64_t>(n, 1) * sizeof(double)) != hipSuccess) return nullptr;
+        tmp.push_back(d);
+        if (hipMemcpy(d, h, n * sizeof(double), hipMemcpyHostToDevice) != hipSuccess) return nullptr;
+        return static_cast<const double*>(d);
+    };
+    static const int zero_i = 0;
+    static const double unit_b[2] = {1.0, 0.0}, unit_w = 1.0;
+    AssembleAxis ax[3];
+    int rc = 0;
+    for (int d = 0; d < 3 && !rc; ++d) {
+        const bool used = d >= d0;
+        const int ne = used ? nel[d] : 1, q = used ? nq[d] : 1, pp = used ? p[d] : 0;
+        const int64_t n = used ? nglob[d] : 1;
+        ax[d].first = up_i(used ? first[d] : &zero_i, ne);
+        ax[d].es = up_i(used ? es[d] : &zero_i, n);
+        ax[d].ee = up_i(used ? ee[d] : &zero_i, n);
+        ax[d].basis = up_d(used ? basis[d] : unit_b, (int64_t)ne * q * (pp + 1) * 2);
+        ax[d].w = up_d(used ? weights[d] : &unit_w, (int64_t)ne * q);
+        ax[d].nel = ne; ax[d].nq = q; ax[d].p = pp; ax[d].n = (int)n;
+        if (!ax[d].first || !ax[d].es || !ax[d].ee || !ax[d].basis || !ax[d].w) rc = 1;
+    }
+    if (!rc && hipMalloc(reinterpret_cast<void**>(&o->coef), std::max<int64_t>(W * cst, 1) * sizeof(double)) != hipSuccess)
+        rc = 1;
+    if (!rc) {
+        assemble_launch(ax, (int)o->g0, r.n0, a_q, c_q, mass_coef, o->coef, nullptr);
+        if (hipGetLastError() != hipSuccess || hipDeviceSynchronize() != hipSuccess) rc = 1;
+    }
+    for (void* d : tmp) (void)hipFree(d);
+    if (rc) {
+        set_error("poms_op_assemble_stencil: allocation, upload or launch failed");
+        poms_op_destroy(o);
+        return 1;
+    }
+    *op = o;
+    return 0;
+}
+
+int poms_op_stencil_data(poms_op* o, double* data_host) {
+    if (!o || !data_host || o->form != FORM_STENCIL) { set_error("poms_op_stencil_data: needs a general-stencil operator"); return 1; }
+    const RowGeom r = row_geom(&o->L);
+    StencilGeom g{r.s0, r.s1, r.n0, r.n1, r.n2, r.pd0, r.pd1, r.pd2, o->sp[0], o->sp[1], o->sp[2],
+                  2 * o->sp[0] + 1, 2 * o->sp[1] + 1, 2 * o->sp[2] + 1, (int64_t)r.n0 * r.n1 * r.n2, 0, 0, 0, 0};
+    const int64_t W = (int64_t)g.w0 * g.w1 * g.w2;
+    const int64_t rows = (int64_t)(r.n0 + 2 * o->sp[0]) * (r.n1 + 2 * o->sp[1]) * (r.n2 + 2 * o->sp[2]);
+    double* d = nullptr;
+    POMS_HIP_CHECK(hipMalloc(reinterpret_cast<void**>(&d), rows * W * sizeof(double)));
+    int rc = 0;
+    if (hipMemset(d, 0, rows * W * sizeof(double)) != hipSuccess) rc = 1;
+    if (!rc) stencil_to_spl_launch(g, o->coef, d, nullptr);
+    if (!rc && (hipGetLastError() != hipSuccess ||
+                hipMemcpy(data_host, d, rows * W * sizeof(double), hipMemcpyDeviceToHost) != hipSuccess))
+        rc = 1;
+    (void)hipFree(d);
+    if (rc) { set_error("poms_op_stencil_data: copy failed"); return 1; }
     return 0;
 }
 

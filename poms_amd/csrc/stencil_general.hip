@@ -83,6 +83,107 @@ stencil_kernel(const StencilGeom g, const double* __restrict__ coef, const doubl
     }
 }
 
+// On-device assembly of -div(a grad u) + c u (`sources/matrix_assembler.py:84-179`,
+// where a = c = 1): one thread per (owned row, stencil offset), writing coefficient
+// plane k of row `lin`.  The row pair (i, j) meets on the elements both supports
+// share; per element the quadrature sum is formed first and then added, as the
+// reference's element loop does.  a_q / c_q: coefficients at every quadrature
+// point (index ((e0 nq0 + g0) NQ1 + e1 nq1 + g1) NQ2 + e2 nq2 + g2), or null for
+// a = 1, c = mass_coef.
+__global__ void __launch_bounds__(256)
+assemble_kernel(const AssembleAxis A0, const AssembleAxis A1, const AssembleAxis A2, int g0, int nl0,
+                const double* __restrict__ a_q, const double* __restrict__ c_q, double mass_coef,
+                double* __restrict__ coef) {
+    const int64_t cst = (int64_t)nl0 * A1.n * A2.n;
+    const int W1 = 2 * A1.p + 1, W2 = 2 * A2.p + 1;
+    const int64_t total = cst * (int64_t)(2 * A0.p + 1) * W1 * W2;
+    const int64_t tid = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    if (tid >= total) return;
+    const int64_t lin = tid % cst;
+    const int k = (int)(tid / cst);
+    const int k2 = k % W2, k1 = (k / W2) % W1, k0 = k / (W2 * W1);
+    const int i2 = (int)(lin % A2.n), i1 = (int)((lin / A2.n) % A1.n), i0 = g0 + (int)(lin / ((int64_t)A2.n * A1.n));
+    const int j0 = i0 + k0 - A0.p, j1 = i1 + k1 - A1.p, j2 = i2 + k2 - A2.p;
+    double tot = 0.0;
+    if (j0 >= 0 && j0 < A0.n && j1 >= 0 && j1 < A1.n && j2 >= 0 && j2 < A2.n) {
+        const int ea0 = max(A0.es[i0], A0.es[j0]), eb0 = min(A0.ee[i0], A0.ee[j0]);
+        const int ea1 = max(A1.es[i1], A1.es[j1]), eb1 = min(A1.ee[i1], A1.ee[j1]);
+        const int ea2 = max(A2.es[i2], A2.es[j2]), eb2 = min(A2.ee[i2], A2.ee[j2]);
+        const int NQ1 = A1.nel * A1.nq, NQ2 = A2.nel * A2.nq;
+        for (int e0 = ea0; e0 <= eb0; ++e0) {
+            const int li0 = i0 - A0.first[e0], lj0 = j0 - A0.first[e0];
+            for (int e1 = ea1; e1 <= eb1; ++e1) {
+                const int li1 = i1 - A1.first[e1], lj1 = j1 - A1.first[e1];
+                for (int e2 = ea2; e2 <= eb2; ++e2) {
+                    const int li2 = i2 - A2.first[e2], lj2 = j2 - A2.first[e2];
+                    double v = 0.0;
+                    for (int q0 = 0; q0 < A0.nq; ++q0) {
+                        const double* B0 = A0.basis + (int64_t)(e0 * A0.nq + q0) * (A0.p + 1) * 2;
+                        const double w0 = A0.w[e0 * A0.nq + q0];
+                        const double bi0 = B0[2 * li0], di0 = B0[2 * li0 + 1];
+                        const double bj0 = B0[2 * lj0], dj0 = B0[2 * lj0 + 1];
+                        for (int q1 = 0; q1 < A1.nq; ++q1) {
+                            const double* B1 = A1.basis + (int64_t)(e1 * A1.nq + q1) * (A1.p + 1) * 2;
+                            const double w1 = A1.w[e1 * A1.nq + q1];
+                            const double bi1 = B1[2 * li1], di1 = B1[2 * li1 + 1];
+                            const double bj1 = B1[2 * lj1], dj1 = B1[2 * lj1 + 1];
+                            for (int q2 = 0; q2 < A2.nq; ++q2) {
+                                const double* B2 = A2.basis + (int64_t)(e2 * A2.nq + q2) * (A2.p + 1) * 2;
+                                const double w2 = A2.w[e2 * A2.nq + q2];
+                                const double bi2 = B2[2 * li2], di2 = B2[2 * li2 + 1];
+                                const double bj2 = B2[2 * lj2], dj2 = B2[2 * lj2 + 1];
+                                // bi_0 bj_0 + bi_x bj_x + bi_y bj_y (+ bi_z bj_z), times wvol
+                                const double i_0 = bi0 * (bi1 * bi2), j_0 = bj0 * (bj1 * bj2);
+                                const double gx = (di0 * (bi1 * bi2)) * (dj0 * (bj1 * bj2));
+                                const double gy = (bi0 * (di1 * bi2)) * (bj0 * (dj1 * bj2));
+                                const double gz = (bi0 * (bi1 * di2)) * (bj0 * (bj1 * dj2));
+                                const int64_t qi = ((int64_t)(e0 * A0.nq + q0) * NQ1 + (e1 * A1.nq + q1)) * NQ2 +
+                                                   (e2 * A2.nq + q2);
+                                const double ca = a_q ? a_q[qi] : 1.0;
+                                const double cc = c_q ? c_q[qi] : mass_coef;
+                                v = fma(cc * i_0 * j_0 + ca * (gx + gy + gz), w0 * (w1 * w2), v);
+                            }
+                        }
+                    }
+                    tot += v;
+                }
+            }
+        }
+    }
+    coef[k * cst + lin] = tot;
+}
+
+int assemble_launch(const AssembleAxis* ax, int g0, int nl0, const double* a_q, const double* c_q, double mass_coef,
+                    double* coef, hipStream_t st) {
+    const int64_t total = (int64_t)nl0 * ax[1].n * ax[2].n * (2 * ax[0].p + 1) * (2 * ax[1].p + 1) * (2 * ax[2].p + 1);
+    if (total == 0) return 0;
+    hipLaunchKernelGGL(assemble_kernel, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, st, ax[0], ax[1], ax[2],
+                       g0, nl0, a_q, c_q, mass_coef, coef);
+    return 0;
+}
+
+// Coefficient planes -> the spl StencilMatrix._data layout (padded rows, offsets last).
+__global__ void __launch_bounds__(256)
+stencil_to_spl_kernel(const StencilGeom g, const double* __restrict__ coef, double* __restrict__ out) {
+    const int W = g.w0 * g.w1 * g.w2;
+    const int64_t total = g.cstride * W;
+    const int64_t tid = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    if (tid >= total) return;
+    const int64_t lin = tid / W;
+    const int k = (int)(tid % W);
+    const int64_t i2 = lin % g.n2, i1 = (lin / g.n2) % g.n1, i0 = lin / ((int64_t)g.n2 * g.n1);
+    const int64_t P1 = g.n1 + 2 * g.p1, P2 = g.n2 + 2 * g.p2;
+    const int64_t row = ((i0 + g.p0) * P1 + (i1 + g.p1)) * P2 + (i2 + g.p2);
+    out[row * W + k] = coef[k * g.cstride + lin];
+}
+
+int stencil_to_spl_launch(const StencilGeom& g, const double* coef, double* out, hipStream_t st) {
+    const int64_t total = g.cstride * g.w0 * g.w1 * g.w2;
+    if (total == 0) return 0;
+    hipLaunchKernelGGL(stencil_to_spl_kernel, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, st, g, coef, out);
+    return 0;
+}
+
 // Blocks of the grid-stride launch (<= max_blocks so the partials fit the scratch).
 int stencil_launch(int epi, const StencilGeom& g, const double* coef, const double* x, double* y,
                    const double* b, double omega, double* partial, double* partial2, int max_blocks,

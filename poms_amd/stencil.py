@@ -956,9 +956,31 @@ class StencilMatrix(KronOperator):
         self._calls = 0
         self._hh = C.c_void_p()
         self._dirty = True
-        self._data = np.zeros(V.padded_shape + tuple(2 * p + 1 for p in V.pads))
+        self._host = np.zeros(V.padded_shape + tuple(2 * p + 1 for p in V.pads))
         self.pads = V.pads
         self.starts, self.ends = V.starts, V.ends
+
+    @classmethod
+    def _from_handle(cls, V: StencilVectorSpace, h: C.c_void_p) -> "StencilMatrix":
+        """Wrap a device-built general-stencil operator (``poms_op_assemble_stencil``);
+        the host copy is fetched on first host-side access."""
+        M = cls.__new__(cls)
+        M.space, M.form = V, "stencil"
+        M.pmax = max(max(V.pads), 1)
+        M.bands, M.timer, M._calls = {}, None, 0
+        M._hh, M._dirty, M._host = h, False, None
+        M.pads, M.starts, M.ends = V.pads, V.starts, V.ends
+        return M
+
+    @property
+    def _data(self) -> np.ndarray:
+        """Host coefficients in the spl layout (downloaded once if device-built)."""
+        if self._host is None:
+            V = self.space
+            out = np.zeros(V.padded_shape + tuple(2 * p + 1 for p in V.pads))
+            _lib.call("poms_op_stencil_data", self._hh, out.ctypes.data_as(C.c_void_p))
+            self._host = out
+        return self._host
 
     @classmethod
     def from_data(cls, V: StencilVectorSpace, data: np.ndarray) -> "StencilMatrix":

@@ -118,3 +118,15 @@ def test_collocation_cardinal_splines_restatement():
         assert np.allclose(C.sum(axis=1)[p:-p], 1.0, atol=1e-14)
         assert np.array_equal(C, C.T)
         assert np.array_equal(C, orc.collocation_cardinal_splines(p, 3 * p + 3))
+
+
+def test_assembly_varcoef_oracle_matches_reference(golden_dir):
+    """The d-dimensional quadrature-assembly restatement (a = c = 1) == the reference's
+    own `assembly_2d` stencils (`sources/matrix_assembler.py:84-179`)."""
+    from oracle import spl_standin as S
+    for name, c in load(golden_dir, "assembly_2d.npz").items():
+        p = int(c["p"])
+        ne = [int(v) for v in c["ne"]]
+        T = [S.make_open_knots(p, e + p) for e in ne]
+        o = orc.assembly_varcoef(T, [p, p])
+        assert np.max(np.abs(o - c["stencil"])) <= 1e-14 * np.max(np.abs(c["stencil"])), name
