@@ -115,7 +115,11 @@ kron_v5_kernel(const double* __restrict__ x, double* __restrict__ y, const doubl
     constexpr int XI_OFF = BS_OFF + (HASB ? 2 * T1 * TC : 0);
     constexpr int C2_OFF = XI_OFF + (XIN ? 2 * T1 * TC : 0);
     constexpr int RED_OFF = C2_OFF + 2 * W * TC;
-    constexpr int LDS_N = RED_OFF + NW;
+    // Jacobi (register-history builds; the x_in ring leaves no room): 1/diag on the
+    // axis-0 Toeplitz interior planes, one row per wave
+    constexpr bool RCIL = JAC && XH;
+    constexpr int RCI_OFF = RED_OFF + NW;
+    constexpr int LDS_N = RCI_OFF + (RCIL ? T1 * TC : 0);
     __shared__ __attribute__((aligned(16))) double lds[LDS_N];
 
     const int tid = threadIdx.x;
@@ -162,6 +166,13 @@ kron_v5_kernel(const double* __restrict__ x, double* __restrict__ y, const doubl
     const double* __restrict__ ra = a1 + orc * W;
     const double* __restrict__ rb = b1 + orc * W;
     // plane-invariant parts of diag(A) = d0a X + d0b Y at this lane's columns
+    auto rcp_nr = [](double dg) {   // 1/dg: v_rcp_f64 + two Newton steps
+        double r = __builtin_amdgcn_rcp(dg);
+        double ee = fma(-dg, r, 1.0);
+        r = fma(r, ee, r);
+        ee = fma(-dg, r, 1.0);
+        return fma(r, ee, r);
+    };
     double dX[2] = {0.0, 0.0}, dY[2] = {0.0, 0.0};
     if constexpr (JAC) {
         const double d1a = ra[P], d1b = rb[P];
@@ -171,6 +182,10 @@ kron_v5_kernel(const double* __restrict__ x, double* __restrict__ y, const doubl
             const double d2a = a2[col * W + P], d2b = b2[col * W + P];
             dX[e] = d1a * d2a;
             dY[e] = fma(d1b, d2a, d1a * d2b);
+            // on the axis-0 Toeplitz interior planes d0a, d0b are the Toeplitz centre
+            // (bitwise), so 1/diag there is plane-invariant: computed once, kept in LDS
+            // (two more VGPRs would spill); each wave reads back only its own row
+            if constexpr (RCIL) lds[RCI_OFF + wv * TC + 2 * lane + e] = rcp_nr(fma(tc.t0a[0], dX[e], tc.t0b[0] * dY[e]));
         }
     }
 
@@ -401,18 +416,15 @@ kron_v5_kernel(const double* __restrict__ x, double* __restrict__ y, const doubl
                         double rc[2];
                         if (fast1 && fast2 && rdiag0 != nullptr) {
                             rc[0] = rc[1] = rdiag0[g.g0 + zo];
+                        } else if (RCIL && g.g0 + zo >= tc.lo0 && g.g0 + zo < tc.hi0) {
+                            const d2 ri = *(const d2*)(lds + RCI_OFF + wv * TC + 2 * lane);
+                            rc[0] = ri[0];
+                            rc[1] = ri[1];
                         } else {
                             const int i0 = (g.g0 + zo + P) * W + P;
                             const double d0a = a0t[i0], d0b = b0t[i0];
 #pragma unroll
-                            for (int e = 0; e < 2; ++e) {
-                                const double dg = fma(d0a, dX[e], d0b * dY[e]);
-                                double r = __builtin_amdgcn_rcp(dg);
-                                double ee = fma(-dg, r, 1.0);
-                                r = fma(r, ee, r);
-                                ee = fma(-dg, r, 1.0);
-                                rc[e] = fma(r, ee, r);
-                            }
+                            for (int e = 0; e < 2; ++e) rc[e] = rcp_nr(fma(d0a, dX[e], d0b * dY[e]));
                         }
 #pragma unroll
                         for (int e = 0; e < 2; ++e) {
