@@ -243,6 +243,10 @@ int poms_vec_axpby(poms_ctx* ctx, const poms_layout* L, double a, const double* 
 int poms_vec_scale(poms_ctx* ctx, const poms_layout* L, double a, const double* x,
                    double* z, void* stream);
 int poms_vec_fill(poms_ctx* ctx, const poms_layout* L, double v, double* z, void* stream);
+/* Zero everything OUTSIDE the interior (ghost planes / rows / columns and dead
+ * pitch columns; the interior is untouched): the zero ghost regions a new spl
+ * `StencilVector(V)` has (`sources/solvers.py:71,169`), one launch.            */
+int poms_vec_zero_ghosts(poms_ctx* ctx, const poms_layout* L, double* z, void* stream);
 /* Local (un-reduced across ranks) inner product over the interior; result to
  * out_dev[0].  Replaces `StencilVector.dot` (`sources/solvers.py:87,91,104,111`). */
 int poms_vec_dot(poms_ctx* ctx, const poms_layout* L, const double* x,

@@ -99,6 +99,7 @@ _SIGS = {
     "poms_vec_axpby": [_vp, _LP, _d, _vp, _d, _vp, _vp, _vp],
     "poms_vec_scale": [_vp, _LP, _d, _vp, _vp, _vp],
     "poms_vec_fill": [_vp, _LP, _d, _vp, _vp],
+    "poms_vec_zero_ghosts": [_vp, _LP, _vp, _vp],
     "poms_vec_dot": [_vp, _LP, _vp, _vp, _vp, _vp],
     "poms_pcg_update": [_vp, _LP, _d, _vp, _vp, _vp, _vp, _vp, _vp],
     "poms_pcg_r_update": [_vp, _LP, _d, _vp, _vp, _vp, _vp],

@@ -33,6 +33,7 @@ int reduce_launch(const double* partial, int count, double* out, hipStream_t st,
 int vec_flat_launch(int op, int64_t count, double a, double b, const double* x, const double* y,
                     double* z, double* w, const double* q, double* partial, hipStream_t st,
                     int* nblk_out, const double* ab = nullptr);
+int zero_ghosts_launch(const RowGeom& g, double* z, hipStream_t st);
 int diag_scale_launch(bool is3d, int form, const RowGeom& g, int P, int g0, double scale,
                       const double* b, double* x, const double* a0t, const double* b0t,
                       const double* a1, const double* b1, const double* a2, const double* b2,
@@ -921,6 +922,13 @@ int poms_vec_scale(poms_ctx* ctx, const poms_layout* L, double a, const double* 
 int poms_vec_fill(poms_ctx* ctx, const poms_layout* L, double v, double* z, void* stream) {
     if (!z) { set_error("fill: null vector"); return 1; }
     return vec_common(ctx, L, V_FILL, v, 0.0, nullptr, nullptr, z, nullptr, nullptr, nullptr, stream);
+}
+
+int poms_vec_zero_ghosts(poms_ctx* ctx, const poms_layout* L, double* z, void* stream) {
+    if (!ctx || !layout_ok(L) || !z) { set_error("zero_ghosts: bad argument"); return 1; }
+    zero_ghosts_launch(row_geom(L), z, as_stream(stream));
+    POMS_HIP_CHECK(hipGetLastError());
+    return 0;
 }
 
 int poms_vec_dot(poms_ctx* ctx, const poms_layout* L, const double* x, const double* y,

@@ -282,6 +282,34 @@ int vec_launch(int op, const RowGeom& g, double a, double b, const double* x, co
     return 1;
 }
 
+// Zero every padded entry outside the interior -- ghost planes, ghost rows, ghost
+// columns and dead pitch columns -- in one launch (a fresh vector's ghosts; the
+// interior is left as it is).  One wave per padded row, four rows per block.
+__global__ void __launch_bounds__(256)
+zero_ghosts_kernel(const RowGeom g, int64_t nrows, int nr1, double* __restrict__ z) {
+    const int64_t row = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+    if (row >= nrows) return;
+    const int lane = threadIdx.x & 63;
+    const int64_t i0 = row / nr1;
+    const int i1 = (int)(row - i0 * nr1);
+    double* __restrict__ zr = z + i0 * g.s0 + (int64_t)i1 * g.s1;
+    const bool ghost = i0 < g.pd0 || i0 >= g.pd0 + g.n0 || i1 < g.pd1 || i1 >= g.pd1 + g.n1;
+    if (ghost) {
+        for (int64_t c = lane; c < g.s1; c += 64) zr[c] = 0.0;
+    } else {
+        if (lane < g.pd2) zr[lane] = 0.0;
+        for (int64_t c = g.pd2 + g.n2 + lane; c < g.s1; c += 64) zr[c] = 0.0;
+    }
+}
+
+int zero_ghosts_launch(const RowGeom& g, double* z, hipStream_t st) {
+    const int nr1 = g.n1 + 2 * g.pd1;
+    const int64_t nrows = (int64_t)(g.n0 + 2 * g.pd0) * nr1;
+    if (nrows < 1) return 0;
+    hipLaunchKernelGGL(zero_ghosts_kernel, dim3((unsigned)((nrows + 3) / 4)), dim3(256), 0, st, g, nrows, nr1, z);
+    return 0;
+}
+
 // Flat form over `count` doubles starting at each pointer (whole interior planes).
 // The pointers must share their alignment modulo 16 B (same layout): returns 1
 // (nothing launched) otherwise, and for ops without a flat form (V_FILL).

@@ -114,18 +114,9 @@ class StencilVectorSpace:
     def empty(self) -> "StencilVector":
         """Vector with unspecified interior and zero ghost cells (no full memset)."""
         store = torch.empty(self.store_elems, dtype=F64, device=f"cuda:{self.device}")
-        t = self.view(store)
-        for ax, p in enumerate(self.pads):
-            if p:
-                idx = [slice(None)] * self.ndim
-                idx[ax] = slice(0, p)
-                t[tuple(idx)] = 0.0
-                idx[ax] = slice(t.shape[ax] - p, t.shape[ax])
-                t[tuple(idx)] = 0.0
-        if self.pitch > self.padded_shape[-1]:   # dead columns: finite, never NaN
-            dead = torch.as_strided(store, self.padded_shape[:-1] + (self.pitch - self.padded_shape[-1],),
-                                    self.strides[:-1] + (1,), self.shift + self.padded_shape[-1])
-            dead.zero_()
+        # ghost planes / rows / columns and dead pitch columns (finite, never NaN) in one launch
+        _lib.call("poms_vec_zero_ghosts", self.ctx, C.byref(self.layout), rt.ptr(self.view(store)),
+                  rt.stream_handle())
         return StencilVector(self, _store=store)
 
     def scalar_buffer(self) -> torch.Tensor:

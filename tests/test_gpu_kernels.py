@@ -148,6 +148,28 @@ def test_vector_ops(gpu):
     np.testing.assert_array_equal(flat, a.reshape(-1))
 
 
+@pytest.mark.parametrize("ndim,npts,p,align", [(3, (9, 7, 21), 3, True), (3, (9, 7, 21), 2, False),
+                                               (2, (13, 40), 3, True), (1, (33,), 2, False)])
+def test_zero_ghosts(gpu, ndim, npts, p, align):
+    """poms_vec_zero_ghosts (behind V.empty()): every entry outside the interior is
+    0 -- ghost planes / rows / columns and dead pitch columns -- and the interior is
+    left untouched (NaN here)."""
+    import ctypes as C
+    import torch
+    from poms_amd import _lib, runtime as rt
+    from poms_amd.stencil import StencilVectorSpace
+    V = StencilVectorSpace(list(npts), [p] * ndim, align=align)
+    store = torch.full((V.store_elems,), float("nan"), dtype=torch.float64, device=gpu)
+    _lib.call("poms_vec_zero_ghosts", V.ctx, C.byref(V.layout), rt.ptr(V.view(store)), rt.stream_handle())
+    full = torch.as_strided(store, V.padded_shape[:-1] + (V.pitch,), V.strides, V.shift).cpu().numpy()
+    inner = np.zeros(full.shape, dtype=bool)
+    inner[tuple(slice(p, p + n) for n in npts)] = True
+    assert np.all(np.isnan(full[inner]))
+    assert np.all(full[~inner] == 0.0)
+    v = V.empty()
+    assert np.all(torch.as_strided(v._store, full.shape, V.strides, V.shift).cpu().numpy()[~inner] == 0.0)
+
+
 def test_kron_dot_pyccel_2d_dropin(gpu):
     """Host-pointer drop-in vs the restated pyccel loop nest on a sub-block with ghost data."""
     from poms_amd.kron_product import kron_dot_pyccel_2d
