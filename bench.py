@@ -47,7 +47,7 @@ def parse():
     ap.add_argument("--cpu-cells", type=int, default=160)
     ap.add_argument("--cpu-cycles", type=int, default=3)
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--pmc-json", type=str, default=str(ROOT / "profiles" / "r01" / "pmc_traffic_jacobi_v5.json"),
+    ap.add_argument("--pmc-json", type=str, default=str(ROOT / "profiles" / "r01" / "pmc_traffic_jacobi_v5b.json"),
                     help="tools/pmc_traffic.py summary of a separate rocprofv3 --pmc pass "
                          "(FETCH_SIZE x2 + WRITE_SIZE per launch) used for roofline.traffic")
     return ap.parse_args()

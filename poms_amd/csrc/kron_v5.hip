@@ -165,7 +165,6 @@ kron_v5_kernel(const double* __restrict__ x, double* __restrict__ y, const doubl
     const int orc = min(orow, g.n1 - 1);
     const double* __restrict__ ra = a1 + orc * W;
     const double* __restrict__ rb = b1 + orc * W;
-    // plane-invariant parts of diag(A) = d0a X + d0b Y at this lane's columns
     auto rcp_nr = [](double dg) {   // 1/dg: v_rcp_f64 + two Newton steps
         double r = __builtin_amdgcn_rcp(dg);
         double ee = fma(-dg, r, 1.0);
@@ -173,21 +172,17 @@ kron_v5_kernel(const double* __restrict__ x, double* __restrict__ y, const doubl
         ee = fma(-dg, r, 1.0);
         return fma(r, ee, r);
     };
-    double dX[2] = {0.0, 0.0}, dY[2] = {0.0, 0.0};
-    if constexpr (JAC) {
+    // plane-invariant parts of diag(A) = d0a X + d0b Y at this lane's column e: the
+    // wave's row by scalar loads, the column from the Toeplitz centre (fast2: every
+    // output column is Toeplitz; other lanes are never stored) or the C2 table.
+    // Recomputed where needed rather than held in 8 VGPRs across the march.
+    auto diag_xy = [&](int e, double& X, double& Y) {
         const double d1a = ra[P], d1b = rb[P];
-#pragma unroll
-        for (int e = 0; e < 2; ++e) {
-            const int col = min(max(cg0 + e, 0), g.n2 - 1);
-            const double d2a = a2[col * W + P], d2b = b2[col * W + P];
-            dX[e] = d1a * d2a;
-            dY[e] = fma(d1b, d2a, d1a * d2b);
-            // on the axis-0 Toeplitz interior planes d0a, d0b are the Toeplitz centre
-            // (bitwise), so 1/diag there is plane-invariant: computed once, kept in LDS
-            // (two more VGPRs would spill); each wave reads back only its own row
-            if constexpr (RCIL) lds[RCI_OFF + wv * TC + 2 * lane + e] = rcp_nr(fma(tc.t0a[0], dX[e], tc.t0b[0] * dY[e]));
-        }
-    }
+        const double d2a = fast2 ? tc.t2a[0] : lds[C2_OFF + P * TC + 2 * lane + e];
+        const double d2b = fast2 ? tc.t2b[0] : lds[C2_OFF + (W + P) * TC + 2 * lane + e];
+        X = d1a * d2a;
+        Y = fma(d1b, d2a, d1a * d2b);
+    };
 
     int z0, z1;
     chunk_planes(g, ch, z0, z1);
@@ -234,6 +229,17 @@ kron_v5_kernel(const double* __restrict__ x, double* __restrict__ y, const doubl
     double nrm = 0.0, dotp = 0.0;
 
     __syncthreads();  // C2 table visible; no DMA in flight yet
+    if constexpr (RCIL) {
+        // on the axis-0 Toeplitz interior planes d0a, d0b are the Toeplitz centre
+        // (bitwise), so omega/diag there is plane-invariant: computed once into LDS (two
+        // more VGPRs would spill); each wave reads back only its own row
+#pragma unroll
+        for (int e = 0; e < 2; ++e) {
+            double X, Y;
+            diag_xy(e, X, Y);
+            lds[RCI_OFF + wv * TC + 2 * lane + e] = omega * rcp_nr(fma(tc.t0a[0], X, tc.t0b[0] * Y));
+        }
+    }
 
 #pragma unroll
     for (int i = 0; i < PFX; ++i) dma_x(i < nplanes ? z0 - P + i : -(1 << 20), i);
@@ -415,7 +421,7 @@ kron_v5_kernel(const double* __restrict__ x, double* __restrict__ y, const doubl
                         }
                         double rc[2];
                         if (fast1 && fast2 && rdiag0 != nullptr) {
-                            rc[0] = rc[1] = rdiag0[g.g0 + zo];
+                            rc[0] = rc[1] = omega * rdiag0[g.g0 + zo];   // one multiply per plane
                         } else if (RCIL && g.g0 + zo >= tc.lo0 && g.g0 + zo < tc.hi0) {
                             const d2 ri = *(const d2*)(lds + RCI_OFF + wv * TC + 2 * lane);
                             rc[0] = ri[0];
@@ -424,11 +430,15 @@ kron_v5_kernel(const double* __restrict__ x, double* __restrict__ y, const doubl
                             const int i0 = (g.g0 + zo + P) * W + P;
                             const double d0a = a0t[i0], d0b = b0t[i0];
 #pragma unroll
-                            for (int e = 0; e < 2; ++e) rc[e] = rcp_nr(fma(d0a, dX[e], d0b * dY[e]));
+                            for (int e = 0; e < 2; ++e) {
+                                double X, Y;
+                                diag_xy(e, X, Y);
+                                rc[e] = omega * rcp_nr(fma(d0a, X, d0b * Y));
+                            }
                         }
 #pragma unroll
                         for (int e = 0; e < 2; ++e) {
-                            const double dr = omega * (bv[e] - vo[e]) * rc[e];
+                            const double dr = (bv[e] - vo[e]) * rc[e];   // rc = omega / diag
                             outv[e] = xin[e] + dr;
                             nrm = ok[e] ? fma(dr, dr, nrm) : nrm;
                             if constexpr (JDOT) dotp = ok[e] ? fma(outv[e], bv[e], dotp) : dotp;
