@@ -103,7 +103,9 @@ kron_v5_kernel(const double* __restrict__ x, double* __restrict__ y, const doubl
     constexpr bool HASB = (EPI == EPI_RESID) || (EPI == EPI_JACOBI);
     constexpr bool JAC = (EPI == EPI_JACOBI);
     constexpr bool APD = (EPI == EPI_APPLYDOT);
-    constexpr bool HIST = APD || (JAC && XH);   // x at the output point from a register history
+    // two sweeps from x = 0: the x ring holds b, scaled on the fly to x1 = omega b / diag
+    constexpr bool J0 = (EPI == EPI_JACOBI0);
+    constexpr bool HIST = APD || (JAC && XH) || J0;   // x (J0: x1) at the output point from a register history
     constexpr bool XIN = JAC && !XH;            // ... or DMA'd next to b (fewer VGPRs, 8 B/DOF more reads)
     constexpr int XAUX = (CP & 1) ? 2 : 0, BAUX = (CP & 2) ? 2 : 0, YAUX = (CP & 4) ? 2 : 0;
     constexpr int NWIN = 2 * P + 2;     // columns 2j-P .. 2j+1+P of a lane's pair
@@ -119,7 +121,12 @@ kron_v5_kernel(const double* __restrict__ x, double* __restrict__ y, const doubl
     // axis-0 Toeplitz interior planes, one row per wave
     constexpr bool RCIL = JAC && XH;
     constexpr int RCI_OFF = RED_OFF + NW;
-    constexpr int LDS_N = RCI_OFF + (RCIL ? T1 * TC : 0);
+    // J0: omega/diag of every x-tile point on the axis-0 Toeplitz planes (XR rows) and
+    // the axis-2 diagonal entries of the tile's columns
+    constexpr int RS_OFF = RCI_OFF + (RCIL ? T1 * TC : 0);
+    constexpr int D2_OFF = RS_OFF + (J0 ? XR * TC : 0);
+    constexpr int D1_OFF = D2_OFF + (J0 ? 2 * TC : 0);   // J0: axis-1 diagonal entries of the x-tile rows
+    constexpr int LDS_N = D1_OFF + (J0 ? 2 * XR : 0);
     __shared__ __attribute__((aligned(16))) double lds[LDS_N];
 
     const int tid = threadIdx.x;
@@ -158,6 +165,18 @@ kron_v5_kernel(const double* __restrict__ x, double* __restrict__ y, const doubl
             const int col = min(max(c0 - H + ci, 0), g.n2 - 1);
             lds[C2_OFF + e] = a2[col * W + k];
             lds[C2_OFF + W * TC + e] = b2[col * W + k];
+        }
+    }
+    if constexpr (J0) {
+        if (tid < TC) {
+            const int col = min(max(c0 - H + tid, 0), g.n2 - 1);
+            lds[D2_OFF + tid] = a2[col * W + P];
+            lds[D2_OFF + TC + tid] = b2[col * W + P];
+        }
+        if (tid < XR) {   // x-tile row q = interior row r0 - P + q (clamped: ghost rows hold b = 0)
+            const int row = min(max(r0 - P + tid, 0), g.n1 - 1);
+            lds[D1_OFF + 2 * tid] = a1[row * W + P];
+            lds[D1_OFF + 2 * tid + 1] = b1[row * W + P];
         }
     }
     // this wave's axis-1 band row (read by scalar loads where used: kept out of
@@ -229,6 +248,19 @@ kron_v5_kernel(const double* __restrict__ x, double* __restrict__ y, const doubl
     double nrm = 0.0, dotp = 0.0;
 
     __syncthreads();  // C2 table visible; no DMA in flight yet
+    // J0: omega/diag at x-tile row q, lane-column ci, of a plane with axis-0 diagonal
+    // entries d0a, d0b (LDS tables only: no VMEM inside the march)
+    auto j0_scale = [&](int q, int ci, double d0a, double d0b) {
+        const double d1a = lds[D1_OFF + 2 * q], d1b = lds[D1_OFF + 2 * q + 1];
+        const double d2a = lds[D2_OFF + ci], d2b = lds[D2_OFF + TC + ci];
+        const double dg = fma(d0a, d1a * d2a, d0b * fma(d1b, d2a, d1a * d2b));
+        return dg != 0.0 ? omega * rcp_nr(dg) : 0.0;   // zero diagonal: a ghost plane (b = 0)
+    };
+    if constexpr (J0) {
+        for (int e = tid; e < XR * TC; e += NW * 64)
+            lds[RS_OFF + e] = j0_scale(e / TC, e % TC, tc.t0a[0], tc.t0b[0]);
+        __syncthreads();
+    }
     if constexpr (RCIL) {
         // on the axis-0 Toeplitz interior planes d0a, d0b are the Toeplitz centre
         // (bitwise), so omega/diag there is plane-invariant: computed once into LDS (two
@@ -276,6 +308,25 @@ kron_v5_kernel(const double* __restrict__ x, double* __restrict__ y, const doubl
                 d2 xv[W];
 #pragma unroll
                 for (int k = 0; k < W; ++k) xv[k] = *(const d2*)(xs + (wv + k) * TC);
+                if constexpr (J0) {
+                    const int m = g.g0 + z0 - P + t;   // global plane of x(t)
+                    if (m >= tc.lo0 && m < tc.hi0) {
+#pragma unroll
+                        for (int k = 0; k < W; ++k) {
+                            const d2 sc = *(const d2*)(lds + RS_OFF + (wv + k) * TC + 2 * lane);
+                            xv[k][0] *= sc[0];
+                            xv[k][1] *= sc[1];
+                        }
+                    } else {   // the p planes next to each global end (and ghost planes)
+                        const int i0 = (m + P) * W + P;
+                        const double d0a = a0t[i0], d0b = b0t[i0];
+#pragma unroll
+                        for (int k = 0; k < W; ++k) {
+                            xv[k][0] *= j0_scale(wv + k, 2 * lane, d0a, d0b);
+                            xv[k][1] *= j0_scale(wv + k, 2 * lane + 1, d0a, d0b);
+                        }
+                    }
+                }
                 if constexpr (MODE == 1) {
                     const bool ok0 = t >= 2 * P && row_ok && col_ok[0];
                     bstore2_s(ry, ok0 ? (orow + P) * s1 * 8 + colb + (zo_of(t) + g.pd0) * (int)plane8 : 0x7ffffff0,
@@ -408,6 +459,29 @@ kron_v5_kernel(const double* __restrict__ x, double* __restrict__ y, const doubl
                     outv[1] = vo[1];
 #pragma unroll
                     for (int e = 0; e < 2; ++e) dotp = ok[e] ? fma(xin[e], outv[e], dotp) : dotp;
+                } else if constexpr (J0) {
+                    // x1 = s b, x2 = x1 + s (b - A x1) = x1 + (x1 - s A x1), s = omega/diag;
+                    // xin = x1 at the output point (the scaled centre tap)
+                    const int m = g.g0 + zo;
+                    double sc[2];
+                    if (m >= tc.lo0 && m < tc.hi0) {
+                        const d2 r = *(const d2*)(lds + RS_OFF + (wv + P) * TC + 2 * lane);
+                        sc[0] = r[0];
+                        sc[1] = r[1];
+                    } else {
+                        const int i0 = (m + P) * W + P;
+                        const double d0a = a0t[i0], d0b = b0t[i0];
+                        sc[0] = j0_scale(wv + P, 2 * lane, d0a, d0b);
+                        sc[1] = j0_scale(wv + P, 2 * lane + 1, d0a, d0b);
+                    }
+#pragma unroll
+                    for (int e = 0; e < 2; ++e) {
+                        const double x1 = xin[e];
+                        const double dr = fma(-vo[e], sc[e], x1);
+                        outv[e] = x1 + dr;
+                        nrm = ok[e] ? fma(dr, dr, nrm) : nrm;      // ||dr_2||^2
+                        dotp = ok[e] ? fma(x1, x1, dotp) : dotp;   // ||x1||^2 = ||dr_1||^2
+                    }
                 } else {
                     const d2 bv = *(const d2*)(lds + BS_OFF + ((t & 1) * T1 + wv) * TC + 2 * lane);
                     if constexpr (EPI == EPI_RESID) {
@@ -469,7 +543,7 @@ kron_v5_kernel(const double* __restrict__ x, double* __restrict__ y, const doubl
     }
     v5_wait_vm<0>();  // no LDS-DMA may outlive the workgroup
 
-    if constexpr (JAC || APD) {
+    if constexpr (JAC || APD || J0) {
         if (partial != nullptr) {
 #pragma unroll
             for (int off = 32; off > 0; off >>= 1) nrm += __shfl_xor(nrm, off, 64);
@@ -550,8 +624,13 @@ static int v5_launch_p(int epi, const KronPtrs& p, const KronGeom& g, const Toep
         case EPI_RESID: return v5_launch_t<P, EPI_RESID, 3, 0, 6>(p, g, tc, H, omega, st);
         case EPI_JACOBI: return v5_launch_t<P, EPI_JACOBI, 3, 0, 6, true>(p, g, tc, H, omega, st);
         case EPI_APPLYDOT: return v5_launch_t<P, EPI_APPLYDOT, 4, 0, 6>(p, g, tc, H, omega, st);
+        // x ring = b (read once, apply's policy), y = x2 streamed; p = 3 needs 130
+        // VGPRs (2 spilled at every D / CP tried): built for p <= 2 only
+        case EPI_JACOBI0:
+            if constexpr (P <= 2) return v5_launch_t<P, EPI_JACOBI0, 4, 0, 14>(p, g, tc, H, omega, st);
+            break;
     }
-    set_error("v5: epilogue not built (two sweeps from zero: variant 9)");
+    set_error("v5: epilogue not built");
     return 1;
 }
 

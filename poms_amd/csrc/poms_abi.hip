@@ -622,7 +622,7 @@ static int resolve_variant(const poms_op* o, int epi) {
         else
             v = ((epi == EPI_APPLY || epi == EPI_RESID) && o->pmax <= 3) ? 7 : 9;
     }
-    if (v == 10 && (!v5_ok(o) || epi == EPI_JACOBI0)) v = 9;
+    if (v == 10 && (!v5_ok(o) || (epi == EPI_JACOBI0 && o->pmax > 2))) v = 9;   // v5 two-sweeps: p <= 2
     return v;
 }
 

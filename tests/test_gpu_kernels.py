@@ -228,8 +228,10 @@ def test_jacobi_sweep_fused_dot(gpu, variant, ndim, cells, p):
     assert not A.fused_dot_supported
 
 
-@pytest.mark.parametrize("ndim,cells,p", [(3, (25, 18, 70), 3), (3, (20, 24, 65), 2), (3, (14, 12, 66), 5)])
-def test_jacobi_from_zero(gpu, ndim, cells, p):
+@pytest.mark.parametrize("variant", [8, 9, 10])
+@pytest.mark.parametrize("ndim,cells,p", [(3, (25, 18, 70), 3), (3, (20, 24, 65), 2), (3, (14, 12, 66), 5),
+                                          (3, (21, 33, 40), 1)])
+def test_jacobi_from_zero(gpu, ndim, cells, p, variant):
     """poms_op_jacobi_from_zero == diag_scale (sweep 1) followed by one sweep, with both norms."""
     from poms_amd.stencil import KronOperator
     rng = np.random.default_rng(5)
@@ -237,6 +239,7 @@ def test_jacobi_from_zero(gpu, ndim, cells, p):
     n = [N + p for N in cells]
     V = _space(n, [p] * ndim)
     A = KronOperator.laplace(V, [f[0] for f in F], [f[1] for f in F])
+    A.set_variant(variant)   # 10: v5 for p <= 3, falls back to 9 above
     assert A.from_zero_supported
     b = V.zeros().from_numpy(rng.standard_normal(n))
     x1, x2 = V.zeros(), V.zeros()

@@ -66,7 +66,8 @@ def main():
                     fn = {"dot": lambda: x.dot(b),
                           "apply": lambda: A.dot(x, out=y),
                           "residual": lambda: A.residual(b, x, out=y),
-                          "jacobi": lambda: A.jacobi_sweep(b, x, y, 2.0 / 3.0, want_norm=False)}[kind]
+                          "jacobi": lambda: A.jacobi_sweep(b, x, y, 2.0 / 3.0, want_norm=False),
+                          "from_zero": lambda: A.jacobi_from_zero(b, y, 2.0 / 3.0, want_norm=False)}[kind]
                     for _ in range(2):
                         fn()
                     torch.cuda.synchronize()
@@ -90,7 +91,7 @@ def main():
     out = []
     for (ch, tcols, var, kind), ts in res.items():
         med = statistics.median(ts)
-        bpd = 16 if kind in ("apply", "dot") else 24
+        bpd = 16 if kind in ("apply", "dot", "from_zero") else 24
         row = {"chunk": ch, "tile_cols": tcols, "aligned": not a.no_align, "variant": var, "kind": kind, "median_us": med, "min_us": min(ts),
                "GBps": bpd * dof / med / 1e3, "GDOFps": dof / med / 1e3}
         out.append(row)
