@@ -26,6 +26,7 @@ struct KronGeom {
     int nch1;            // chunks of [z_begin, z_end); chunks nch1.. cover [z2_begin, z2_end)
     int z2_begin, z2_end;  // optional second plane range of the same launch (the other slab boundary)
     int tout;            // output columns per 64-column tile (v3 / v4 kernels; <= 64 - 2P)
+    int order = 0;       // v5 / v6 tile order within an XCD: 0 = axis-2 tiles fastest, 1 = axis-1 tiles fastest
 };
 
 // Output planes [z0, z1) of axis-0 chunk `ch` (3D launches may cover two ranges).
@@ -99,6 +100,7 @@ struct KronPtrs {
     double* partial;    // Jacobi: per-block sums of dr.dr (or null)
     double* partial2;   // Jacobi: per-block sums of x_out.b (or null)
     const double* rdiag0 = nullptr;  // 1/diag(A) per global plane inside the axis-1/2 Toeplitz interior
+    const double* ab0 = nullptr;     // axis-0 (A0, M0) band pairs, global plane j at pair row j + 2P (v6)
 };
 
 // Banded LU factors of one axis of a Kronecker solve (kron_solve.hip).

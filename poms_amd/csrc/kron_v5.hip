@@ -140,10 +140,22 @@ kron_v5_kernel(const double* __restrict__ x, double* __restrict__ y, const doubl
         bid = (xcd < rr ? xcd * (q + 1) : rr * (q + 1) + (xcd - rr) * q) + k;
     }
     const int TO = g.tout;
-    const int t2 = bid % g.tiles2;
-    bid /= g.tiles2;
-    const int t1 = bid % g.tiles1;
-    const int ch = bid / g.tiles1;
+    // tile order within an XCD's contiguous range: t1 fastest (g.order = 1: the
+    // tiles above and below, which read each other's halo rows, run together on one
+    // L2) or t2 fastest (0)
+    int t1, t2;
+    if (g.order) {
+        t1 = bid % g.tiles1;
+        bid /= g.tiles1;
+        t2 = bid % g.tiles2;
+        bid /= g.tiles2;
+    } else {
+        t2 = bid % g.tiles2;
+        bid /= g.tiles2;
+        t1 = bid % g.tiles1;
+        bid /= g.tiles1;
+    }
+    const int ch = bid;
     const int c0 = t2 * TO;             // lane-column ci <-> interior column c0 - H + ci
     const int r0 = t1 * T1;
     const int orow = r0 + wv;           // this wave's output row

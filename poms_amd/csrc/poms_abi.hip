@@ -3,6 +3,7 @@
 #include "../../include/poms_hip.h"
 
 #include <algorithm>
+#include <cstdlib>
 #include <cstring>
 #include <vector>
 
@@ -22,6 +23,9 @@ int kron_v4_launch(int pmax, bool is3d, int form, int epi, const KronPtrs& p, co
 int kron_v5_launch(int pmax, int epi, const KronPtrs& p, const KronGeom& g, const ToepConst& tc, int H,
                    double omega, hipStream_t st, int diag_mode);
 void kron_v5_tile(int pmax, bool aligned, int* H, int* TO);
+int kron_v6_launch(int pmax, int epi, const KronPtrs& p, const KronGeom& g, const ToepConst& tc, int H,
+                   double omega, hipStream_t st, int diag_mode);
+int kron_v6_rows(int pmax, int epi);
 int kron_v2_stamps(int variant, int epi, const KronPtrs& p, const KronGeom& g, const ToepConst& tc,
                    double omega, unsigned long long* dbg, hipStream_t st);
 int kron_tile_rows();
@@ -77,6 +81,7 @@ struct poms_op {
     int64_t last_partials = 0;
     double *dg2a = nullptr, *dg2b = nullptr;  // contiguous axis-2 band diagonals
     double* rdiag0 = nullptr;                  // 1/diag(A) per global plane (Toeplitz interior of axes 1, 2)
+    double* ab0 = nullptr;                     // (A0, M0) pairs of at/bt interleaved: ab0[(j*W + s)*2 + {0,1}]
     int variant = 0;
     bool v2_ok = false;
     ToepConst tc{};
@@ -265,6 +270,15 @@ int poms_op_create(poms_ctx* ctx, int ndim, const poms_layout* layout, int form,
             }
         rc |= upload(ta.data(), ta.size(), &o->a0t);
         if (sum) rc |= upload(tb.data(), tb.size(), &o->b0t);
+        // v6: pair row j + 2P of global plane j (P more zero rows in front, so the
+        // kernel's coefficient window, which starts P planes back, never starts
+        // before the table)
+        std::vector<double> tab(2 * (nrow + pmax) * W, 0.0);
+        for (int64_t e = 0; e < nrow * W; ++e) {
+            tab[2 * (e + pmax * W)] = ta[e];
+            tab[2 * (e + pmax * W) + 1] = tb[e];
+        }
+        rc |= upload(tab.data(), tab.size(), &o->ab0);
     }
     rc |= upload(f[2], (size_t)layout->n[1] * W, &o->a1);
     rc |= upload(f[4], (size_t)layout->n[2] * W, &o->a2);
@@ -463,14 +477,14 @@ int poms_op_stencil_data(poms_op* o, double* data_host) {
 
 int poms_op_destroy(poms_op* o) {
     if (!o) return 0;
-    for (double* p : {o->a0t, o->b0t, o->a1, o->b1, o->a2, o->b2, o->dg2a, o->dg2b, o->rdiag0, o->coef})
+    for (double* p : {o->a0t, o->b0t, o->a1, o->b1, o->a2, o->b2, o->dg2a, o->dg2b, o->rdiag0, o->ab0, o->coef})
         if (p) (void)hipFree(p);
     delete o;
     return 0;
 }
 
 int poms_op_set_variant(poms_op* op, int variant) {
-    if (!op || variant < 0 || (variant > 10 && (variant < 90 || variant > 109))) { set_error("poms_op_set_variant: bad argument"); return 1; }
+    if (!op || variant < 0 || (variant > 11 && (variant < 90 || variant > 112))) { set_error("poms_op_set_variant: bad argument"); return 1; }
     if (variant > 0 && !op->v2_ok) { set_error("poms_op_set_variant: variant needs pads == pmax"); return 1; }
     if (variant == 5 && op->pmax > 3) variant = 4;  // 32-row tile does not fit LDS at p >= 4
     op->variant = variant;
@@ -543,8 +557,25 @@ static bool v5_aligned(const poms_op* o, const double* x) {
     return pitch % 16 == 0 && (reinterpret_cast<uintptr_t>(x + o->L.pads[2]) & 127) == 0;
 }
 
+// v6 (variant 11): one 512-thread workgroup per CU; the critical path of nc
+// chunks per tile is ceil(nc tiles / 256) rounds of (chunk + 2p) planes
+static int auto_chunk_v6(int nz, int tiles, int p) {
+    if (nz <= 0) return 1;
+    tiles = std::max(tiles, 1);
+    double best = 1e300;
+    int best_chunk = nz;
+    for (int nc = 1; nc <= std::max(1, nz / 4); ++nc) {
+        const int ch = (nz + nc - 1) / nc;
+        const int ncu = (nz + ch - 1) / ch;
+        const double rounds = std::ceil((double)ncu * tiles / 256.0);
+        const double cost = rounds * (ch + 2 * p);
+        if (cost < best - 1e-9) { best = cost; best_chunk = ch; }
+    }
+    return best_chunk;
+}
+
 static int op_geom(poms_op* o, int64_t zb, int64_t ze, KronGeom& g, int v = -1, int v5_to = 0,
-                   int64_t zb2 = 0, int64_t ze2 = 0) {
+                   int64_t zb2 = 0, int64_t ze2 = 0, int epi = EPI_APPLY) {
     if (v < 0) v = o->variant;
     const bool is3d = o->ndim == 3;
     const RowGeom r = row_geom(&o->L);
@@ -554,9 +585,10 @@ static int op_geom(poms_op* o, int64_t zb, int64_t ze, KronGeom& g, int v = -1, 
     g.pd0 = r.pd0; g.pd1 = r.pd1; g.pd2 = r.pd2;
     g.g0 = (int)o->g0;
     g.tiles2 = (int)((o->L.n[2] + kron_tile_cols() - 1) / kron_tile_cols());
-    const int trows = (v == 3 || v == 5 || v == 10) ? (v == 10 ? 16 : 32) : kron_tile_rows();
+    const int trows = v == 11 ? kron_v6_rows(o->pmax, epi)
+                    : (v == 3 || v == 5 || v == 10) ? (v == 10 ? 16 : 32) : kron_tile_rows();
     g.tiles1 = (int)((o->L.n[1] + trows - 1) / trows);
-    g.tout = v == 10 ? v5_to : (o->tout > 0 ? o->tout : 64 - 2 * o->pmax);
+    g.tout = (v == 10 || v == 11) ? v5_to : (o->tout > 0 ? o->tout : 64 - 2 * o->pmax);
     if (v >= 4) g.tiles2 = (int)((o->L.n[2] + g.tout - 1) / g.tout);
     if (!is3d) {
         g.z_begin = 0; g.z_end = 1; g.chunk = 1; g.nchunks = 1; g.nch1 = 1; g.z2_begin = g.z2_end = 0;
@@ -567,13 +599,23 @@ static int op_geom(poms_op* o, int64_t zb, int64_t ze, KronGeom& g, int v = -1, 
         set_error("second plane range outside the slab or overlapping the first");
         return 1;
     }
+    {   // tile order (tuning: POMS_TILE_ORDER=0/1)
+        static int ord = -1;
+        if (ord < 0) {
+            const char* e = getenv("POMS_TILE_ORDER");
+            ord = e ? (atoi(e) ? 1 : 0) : 1;
+        }
+        g.order = ord;
+    }
     g.z_begin = (int)zb;
     g.z_end = (int)ze;
     g.z2_begin = (int)zb2;
     g.z2_end = (int)ze2;
     const int nz = (int)(ze - zb) + (int)(ze2 - zb2);
     int chunk = o->chunk;
-    if (chunk <= 0) chunk = auto_chunk(nz, g.tiles2 * g.tiles1, o->pmax, v == 10 ? 256.0 : 512.0);
+    if (chunk <= 0)
+        chunk = v == 11 ? auto_chunk_v6(nz, g.tiles2 * g.tiles1, o->pmax)
+                        : auto_chunk(nz, g.tiles2 * g.tiles1, o->pmax, v == 10 ? 256.0 : 512.0);
     chunk = std::max(1, std::min(chunk, std::max(nz, 1)));
     g.chunk = chunk;
     g.nch1 = (int)((ze - zb + chunk - 1) / chunk);
@@ -583,7 +625,7 @@ static int op_geom(poms_op* o, int64_t zb, int64_t ze, KronGeom& g, int v = -1, 
 
 // variants whose Jacobi epilogue also accumulates x_out . b (v3 and v4 kernels)
 static bool fused_dot_ok(const poms_op* o) {
-    return o->form == FORM_STENCIL || (o->variant >= 4 && o->variant <= 10);
+    return o->form == FORM_STENCIL || (o->variant >= 4 && o->variant <= 11);
 }
 
 // General-stencil launch (FORM_STENCIL): the epilogues of op_run plus EPI_DIAG.
@@ -622,6 +664,8 @@ static int resolve_variant(const poms_op* o, int epi) {
         else
             v = ((epi == EPI_APPLY || epi == EPI_RESID) && o->pmax <= 3) ? 7 : 9;
     }
+    if (v == 11 && (!v5_ok(o) || epi == EPI_JACOBI0))   // v6: no two-sweeps-from-zero epilogue
+        v = (v5_ok(o) && (epi != EPI_JACOBI0 || o->pmax <= 2)) ? 10 : 9;
     if (v == 10 && (!v5_ok(o) || (epi == EPI_JACOBI0 && o->pmax > 2))) v = 9;   // v5 two-sweeps: p <= 2
     return v;
 }
@@ -634,15 +678,15 @@ static int op_run(poms_op* o, int epi, double omega, const double* x, double* y,
     if (o->form == FORM_STENCIL)
         return stencil_run(o, epi, omega, x, y, b, zb, ze, want_norm, stream, want_dot, zb2, ze2);
     if (epi == EPI_APPLYDOT && !(o->variant == 4 || o->variant == 5 || o->variant == 6 || o->variant == 8 ||
-                                 o->variant == 9 || o->variant == 10)) {
-        set_error("apply + x.y: kernel variants 4, 5, 6, 8, 9, 10 only");
+                                 o->variant == 9 || o->variant == 10 || o->variant == 11)) {
+        set_error("apply + x.y: kernel variants 4, 5, 6, 8, 9, 10, 11 only");
         return 1;
     }
     if (want_dot && ((epi != EPI_JACOBI && epi != EPI_JACOBI0 && epi != EPI_APPLYDOT) || !fused_dot_ok(o))) {
         set_error("fused x_out.b needs a Jacobi sweep on kernel variants 4-9");
         return 1;
     }
-    if (epi == EPI_JACOBI0 && !(o->variant == 8 || o->variant == 9 || o->variant == 10)) {
+    if (epi == EPI_JACOBI0 && !(o->variant == 8 || o->variant == 9 || o->variant == 10 || o->variant == 11)) {
         set_error("two sweeps from zero: kernel variant 8, 9 or 10 only");
         return 1;
     }
@@ -656,16 +700,21 @@ static int op_run(poms_op* o, int epi, double omega, const double* x, double* y,
     int v = resolve_variant(o, epi);
     const int v5_diag = (v >= 101 && v <= 109) ? v - 100 : 0;   // v5 diagnostic / tuning builds
     if (v5_diag) v = 10;
+    const int v6_diag = (v == 111 || v == 112) ? v - 110 : 0;   // v6 diagnostic builds
+    if (v6_diag) v = 11;
     int v5_h = 0, v5_to = 0;
-    if (v == 10) kron_v5_tile(o->pmax, v5_aligned(o, x), &v5_h, &v5_to);
+    if (v == 10 || v == 11) kron_v5_tile(o->pmax, v5_aligned(o, x), &v5_h, &v5_to);
     KronGeom g;
-    if (op_geom(o, zb, ze, g, v, v5_to, zb2, ze2)) return 1;
+    if (op_geom(o, zb, ze, g, v, v5_to, zb2, ze2, epi)) return 1;
     const int64_t nblk = (int64_t)g.tiles2 * g.tiles1 * g.nchunks;
     if (nblk == 0) { o->last_partials = 0; return 0; }
     if ((want_norm || want_dot) && 2 * nblk > kScratch) { set_error("too many blocks for the partial-sum scratch"); return 1; }
     KronPtrs p{x, y, b, o->a0t, o->b0t, o->a1, o->b1, o->a2, o->b2,
-               want_norm ? o->ctx->scratch : nullptr, want_dot ? o->ctx->scratch + nblk : nullptr, o->rdiag0};
-    const int rc = v == 10
+               want_norm ? o->ctx->scratch : nullptr, want_dot ? o->ctx->scratch + nblk : nullptr, o->rdiag0,
+               o->ab0};
+    const int rc = v == 11
+        ? kron_v6_launch(o->pmax, epi, p, g, o->tc, v5_h, omega, as_stream(stream), v6_diag)
+        : v == 10
         ? kron_v5_launch(o->pmax, epi, p, g, o->tc, v5_h, omega, as_stream(stream), v5_diag)
         : v == 0
         ? kron_launch(o->pmax, o->ndim == 3, o->form, epi, p, g, omega, as_stream(stream))
@@ -710,7 +759,7 @@ int poms_op_apply_dot(poms_op* op, const double* x, double* y, int64_t zb, int64
 int poms_op_apply_dot_supported(poms_op* op, int* yes) {
     if (!op || !yes) { set_error("poms_op_apply_dot_supported: null argument"); return 1; }
     const int v = op->variant;
-    *yes = (op->form == FORM_STENCIL || v == 4 || v == 5 || v == 6 || v == 8 || v == 9 || v == 10) ? 1 : 0;
+    *yes = (op->form == FORM_STENCIL || v == 4 || v == 5 || v == 6 || v == 8 || v == 9 || v == 10 || v == 11) ? 1 : 0;
     return 0;
 }
 
@@ -725,7 +774,7 @@ int poms_op_jacobi_from_zero(poms_op* op, double omega, const double* b, double*
 int poms_op_from_zero_supported(poms_op* op, int* yes) {
     if (!op || !yes) { set_error("poms_op_from_zero_supported: null argument"); return 1; }
     const int64_t bytes = (int64_t)(op->L.n[0] + 2 * op->L.pads[0]) * row_geom(&op->L).s0 * 8;
-    *yes = (op->ndim == 3 && op->form != FORM_STENCIL && (op->variant == 8 || op->variant == 9 || op->variant == 10) &&
+    *yes = (op->ndim == 3 && op->form != FORM_STENCIL && (op->variant == 8 || op->variant == 9 || op->variant == 10 || op->variant == 11) &&
             bytes < 0x7ffffff0LL) ? 1 : 0;
     return 0;
 }

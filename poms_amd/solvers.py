@@ -346,6 +346,11 @@ def _damped_jacobi(A, b, x0=None, tol=1e-6, maxiter=10, verbose=False, want_dot=
                 break
             if verbose:
                 print(template.format(k, sqrt(nrmr)))
+    if pending is not None and len(pending) == 3:
+        # maxiter == 2 from zero: the loop never ran, so sweep 1's stop test is still
+        # open -- if it fired, the reference returns x1 (`sources/solvers.py:219-222`)
+        done, xprev = settle(pending)
+        return xprev, None
     if pending is not None and not device_dot:   # the last sweep's test cannot change the result
         pending[0].value()
     if verbose:

@@ -114,3 +114,40 @@ def test_vcycle_golden(gpu, golden_dir):
         xf2, ipre, ipos = mg.cycle(bf)
         assert ipre["niter"] == int(c["info_pre"][0]) and ipos["niter"] == int(c["info_pos"][0]), name
         assert rel(xf2.to_local_numpy().reshape(-1), c["xf2"]) <= 1e-8, name
+
+
+def _populate_1d_matrix(M, diag):
+    """`sources/utils.py:7-17` on a :class:`StencilMatrix1D` (same setter calls)."""
+    s, e, p = M.starts[0], M.ends[0], M.pads[0]
+    for i in range(s, e + 1):
+        for k in range(-p, p + 1):
+            M[i, k] = k
+        M[i, 0] = diag
+    M.remove_spurious_entries()
+
+
+def test_kron_dot_v2_reference_recipe(gpu, golden_dir):
+    """The spl-level ``kron_dot_v2(A, B, X)`` (`sources/kron_product.py:56-89`) on the
+    recipe of `sources/tests/test_kron_dot.py:14-35,125-126`: device StencilVector X = 1
+    on 8 x 4, p = (2, 1), 1D StencilMatrix factors from ``populate_1d_matrix`` (5 / 6).
+    Against the reference pyccel kernel's Y and ``utils.kron_dot_ref`` (scipy kron)."""
+    from poms_amd.kron_product import kron_dot_v2
+    from poms_amd.stencil import StencilMatrix1D, StencilVectorSpace
+    c = load(golden_dir, "kron_dot_2d.npz")["recipe"]
+    n1, n2, p1, p2 = 8, 4, 2, 1
+    V = StencilVectorSpace([n1, n2], [p1, p2])
+    A, B = StencilMatrix1D(n1, p1), StencilMatrix1D(n2, p2)
+    _populate_1d_matrix(A, 5.0)
+    _populate_1d_matrix(B, 6.0)
+    np.testing.assert_array_equal(A.band, c["A"])
+    np.testing.assert_array_equal(B.band, c["B"])
+    X = V.zeros()
+    for i1 in range(n1):                   # populate_2d_vector (`sources/utils.py:31-40`)
+        for i2 in range(n2):
+            X[i1, i2] = 1.0
+    Y = kron_dot_v2(A, B, X)
+    got = Y.to_local_numpy()
+    assert got.shape == (n1, n2)
+    assert rel(got, c["Y"][p1:p1 + n1, p2:p2 + n2]) <= 1e-15
+    assert rel(Y.toarray(), c["Y_kron_ref"]) <= 1e-15
+    assert rel(kron_dot_v2(A.band, B.band, X).to_local_numpy(), got) == 0.0

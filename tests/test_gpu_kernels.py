@@ -49,7 +49,7 @@ CASES = [
 ]
 
 
-VARIANTS = [0, 1, 2, 3, 4, 5, 6, 7, 8, 9, 10]
+VARIANTS = [0, 1, 2, 3, 4, 5, 6, 7, 8, 9, 10, 11]
 
 
 @pytest.mark.parametrize("ndim,cells,p", CASES)
@@ -202,7 +202,7 @@ def test_diag_scale_and_first_sweep(gpu):
     assert abs(nrm - float(np.vdot(ref, ref))) <= 1e-12 * float(np.vdot(ref, ref))
 
 
-@pytest.mark.parametrize("variant", [4, 7, 8, 9, 10])
+@pytest.mark.parametrize("variant", [4, 7, 8, 9, 10, 11])
 @pytest.mark.parametrize("ndim,cells,p", [(3, (25, 18, 70), 3), (2, (64, 64), 3), (3, (14, 12, 66), 5)])
 def test_jacobi_sweep_fused_dot(gpu, variant, ndim, cells, p):
     """poms_op_jacobi_sweep_dot: same x_out as the plain sweep, x_out.b == StencilVector.dot."""
@@ -257,7 +257,7 @@ def test_jacobi_from_zero(gpu, ndim, cells, p, variant):
     assert not bool(g.any())
 
 
-@pytest.mark.parametrize("variant", [4, 8, 9, 10])
+@pytest.mark.parametrize("variant", [4, 8, 9, 10, 11])
 @pytest.mark.parametrize("ndim,cells,p", [(3, (25, 18, 70), 3), (2, (64, 64), 3), (3, (14, 12, 66), 5)])
 def test_apply_fused_inner(gpu, variant, ndim, cells, p):
     """poms_op_apply_dot: q = A p bit-identical to the apply of the same kernel family, p.q == dot."""
@@ -281,7 +281,7 @@ def test_apply_fused_inner(gpu, variant, ndim, cells, p):
 
 
 @pytest.mark.parametrize("p,cells", [(2, (20, 24, 131)), (3, (25, 18, 140)), (5, (14, 12, 100))])
-@pytest.mark.parametrize("variant", [7, 8, 9, 10])
+@pytest.mark.parametrize("variant", [7, 8, 9, 10, 11])
 @pytest.mark.parametrize("tile_cols", [0, 48, 32])
 def test_aligned_layout_and_tile_cols(gpu, p, cells, variant, tile_cols):
     """Line-aligned row pitch (poms_layout.pitch) and narrower v3/v4 tiles give the
@@ -344,7 +344,7 @@ def test_native_comm_single_rank(gpu):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("variant", [9, 10])
+@pytest.mark.parametrize("variant", [9, 10, 11])
 def test_two_range_launch(gpu, variant):
     """poms_op_run_reduce2: interior planes, then both p-plane boundaries in ONE launch
     (the overlapped slab schedule) == one launch over all planes, norms included."""

@@ -68,11 +68,13 @@ def test_pcg_fixed_count(gpu, ndim, N, p):
     bv = V.zeros().from_numpy(b)
     apply = lambda v: Acsr @ v
     Ms, Ks = [A.M[0]] * ndim, [A.K[0]] * ndim
-    for m in (1, 3, 6):
+    for m in (1, 2, 3, 6):
         x, info = pcg(A, lambda AA, r: damped_jacobi(AA, r, tol=0.0), bv, tol=0.0, maxiter=m)
         run = lambda ap: orc.pcg(ap, lambda r: orc.damped_jacobi(ap, D, r, tol=0.0), b.reshape(-1),
                                  tol=0.0, maxiter=m)[0]
         tol, xr = parity_bound(run, ndim, n, Ms, Ks)
+        if m <= 3:   # <= 1e-9 after m iterations -- no roundoff-spread allowance
+            tol = 1e-9
         ir = orc.pcg(apply, lambda r: orc.damped_jacobi(apply, D, r, tol=0.0), b.reshape(-1), tol=0.0, maxiter=m)[1]
         assert info["niter"] == ir["niter"] == m
         assert rel(x.to_local_numpy().reshape(-1), xr) <= tol
@@ -225,3 +227,94 @@ def test_transfer_banded(gpu, ndim, p, Nf):
     sub2 = "ia,jb,kc,abc->ijk" if ndim == 3 else "ia,jb,ab->ij"
     ref2 = f + np.einsum(sub2, *([P1] * ndim), xc.reshape((P1.shape[1],) * ndim), optimize=True)
     assert rel(out.to_local_numpy(), ref2) <= 1e-13
+
+
+@pytest.mark.parametrize("align", [True, False])
+@pytest.mark.parametrize("maxiter", [1, 2, 3])
+def test_two_level_vcycle_fixed_count_3d_p3(gpu, maxiter, align):
+    """The headline order (3D p = 3) pinned at the SURVEY §8c floor: the reference's
+    V-cycle schedule (`sources/mg_jac.py:84-119`, tol = 1e-6) with pre/post
+    pcg(maxiter <= 3), where the roundoff amplification of omega = 2/3 Jacobi is
+    still negligible (two oracle orderings agree to ~5e-16): <= 1e-9 and identical
+    niter, no spread allowance."""
+    from poms_amd.mg import TwoLevelVCycle
+    mg = TwoLevelVCycle(3, 16, 4, ndim=3, maxiter=maxiter, align=align)
+    x, ipre, ipos = mg.cycle(mg.rhs_ones())
+    xr, rpre, rpos = orc.vcycle_two_level([mg.M1d] * 3, [mg.K1d] * 3, mg.P1, np.ones((mg.n,) * 3), maxiter=maxiter)
+    assert ipre["niter"] == rpre["niter"] == maxiter and ipos["niter"] == rpos["niter"] == maxiter
+    assert ipre["success"] == rpre["success"] and ipos["success"] == rpos["success"]
+    assert rel(x.to_local_numpy(), xr) <= 1e-9
+
+
+@pytest.mark.parametrize("maxiter", [3, 10])
+def test_two_level_vcycle_reference_coarse_convention_3d(gpu, maxiter):
+    """3D p = 3 on the reference driver's knots: ``nc = 8`` BASIS FUNCTIONS on the coarse
+    grid (`sources/mg_jac.py:25,28`: ``make_open_knots(p, nc)``, 5 cells at p = 3) and a
+    fine grid of ``nf = 19`` basis functions, whose union with the inserted knots is
+    non-uniform (23 fine DOF per axis).  maxiter = 3 at 1e-9; the reference's
+    maxiter = 10 with identical niter and the roundoff-spread bound."""
+    from poms_amd.mg import TwoLevelVCycle
+    from poms_amd.splines import make_open_knots
+    Tf, Tc = make_open_knots(3, 19), make_open_knots(3, 8)
+    mg = TwoLevelVCycle(3, 0, 0, ndim=3, knots_fine=Tf, knots_coarse=Tc, maxiter=maxiter)
+    assert mg.P1.shape == (23, 8)
+    x, ipre, ipos = mg.cycle(mg.rhs_ones())
+    ones = np.ones((mg.n,) * 3)
+    xr, rpre, rpos = orc.vcycle_two_level([mg.M1d] * 3, [mg.K1d] * 3, mg.P1, ones, maxiter=maxiter)
+    tol = 1e-9
+    if maxiter > 3:
+        xr2, _, _ = orc.vcycle_two_level([mg.M1d] * 3, [mg.K1d] * 3, mg.P1, ones, maxiter=maxiter, reorder=True)
+        tol = max(1e-9, 20.0 * rel(xr2, xr))
+    assert ipre["niter"] == rpre["niter"] and ipos["niter"] == rpos["niter"]
+    assert rel(x.to_local_numpy(), xr) <= tol
+
+
+@pytest.mark.parametrize("convention", ["cells", "mg_jac"])
+def test_two_level_vcycle_1d_p2_n128(gpu, convention):
+    """BASELINE config 1: 1D Poisson p = 2, 128 cells, Jacobi-smoothed two-level
+    V-cycle with the reference schedule (pcg(tol=1e-6, maxiter=10) pre/post).
+    ``cells``: 8 coarse cells nested in 128 (130 fine DOF); ``mg_jac``: the
+    reference's ``make_open_knots(p, 8)`` coarse / ``make_open_knots(p, 130)`` fine
+    knots (`sources/mg_jac.py:25-35`).  Runs the 1D operator, smoother and the
+    ``KronTransfer`` 1D embedding on the device."""
+    from poms_amd.mg import TwoLevelVCycle
+    from poms_amd.splines import make_open_knots
+    if convention == "cells":
+        mg = TwoLevelVCycle(2, 128, 8, ndim=1)
+        assert mg.n == 130
+    else:
+        mg = TwoLevelVCycle(2, 0, 0, ndim=1, knots_fine=make_open_knots(2, 130), knots_coarse=make_open_knots(2, 8))
+    x, ipre, ipos = mg.cycle(mg.rhs_ones())
+    ones = np.ones(mg.n)
+    xr, rpre, rpos = orc.vcycle_two_level([mg.M1d], [mg.K1d], mg.P1, ones)
+    xr2, _, _ = orc.vcycle_two_level([mg.M1d], [mg.K1d], mg.P1, ones, reorder=True)
+    assert ipre["niter"] == rpre["niter"] and ipos["niter"] == rpos["niter"]
+    assert ipre["success"] == rpre["success"] and ipos["success"] == rpos["success"]
+    assert rel(x.to_local_numpy(), xr) <= max(1e-9, 20.0 * rel(xr2, xr))
+    # repeated cycles converge to the direct solution of A u = 1
+    from oracle.poms_oracle import kron_sum_csr
+    from scipy.sparse.linalg import spsolve
+    u = spsolve(kron_sum_csr([mg.M1d], [mg.K1d]).tocsc(), ones)
+    xk = x
+    for _ in range(3):
+        xk, _, _ = mg.cycle(mg.rhs_ones(), x0=xk)
+    assert rel(xk.to_local_numpy(), u) <= 1e-8
+
+
+@pytest.mark.parametrize("ndim,N,p", [(2, 12, 3), (3, 8, 2)])
+def test_damped_jacobi_maxiter2_stops_after_sweep1(gpu, ndim, N, p):
+    """maxiter = 2 from x0 = None with ||dr_1||^2 < tol^2: the reference stops after
+    sweep 1 and returns x1 (`sources/solvers.py:219-222`).  Covers the lazily read
+    two-sweeps-from-zero path, whose loop never runs at maxiter = 2."""
+    from poms_amd.solvers import damped_jacobi
+    V, A, Acsr, D, n = _problem(ndim, N, p)
+    b = np.random.default_rng(3).uniform(0.5, 1.0, (n,) * ndim)
+    tol = 1e-6
+    dr1 = (2.0 / 3.0) * b.reshape(-1) / D
+    for frac in (0.5, 2.0):   # ||dr_1||^2 = frac * tol^2: stop after sweep 1, or run both
+        bs = b * np.sqrt(frac) * tol / np.linalg.norm(dr1)
+        x = damped_jacobi(A, V.zeros().from_numpy(bs), tol=tol, maxiter=2).to_local_numpy()
+        xr = orc.damped_jacobi(lambda v: Acsr @ v, D, bs.reshape(-1), tol=tol, maxiter=2)
+        assert rel(x.reshape(-1), xr) <= 1e-12, frac
+        if frac < 1:
+            assert rel(x.reshape(-1), (2.0 / 3.0) * bs.reshape(-1) / D) <= 1e-14
