@@ -44,12 +44,16 @@ def parse():
     ap.add_argument("--coarse", type=int, default=8)
     ap.add_argument("--chunk", type=int, default=0)
     ap.add_argument("--kron-reps", type=int, default=30)
-    ap.add_argument("--cpu-cells", type=int, default=160)
-    ap.add_argument("--cpu-cycles", type=int, default=3)
+    ap.add_argument("--cpu-cells", type=int, default=160,
+                    help="cells per axis of the CPU baseline's V-cycle sample (all nproc cores)")
+    ap.add_argument("--cpu-cycles", type=int, default=2)
+    ap.add_argument("--cpu-cells-1core", type=int, default=64,
+                    help="cells per axis of the single-core V-cycle sample")
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--pmc-json", type=str, default=str(ROOT / "profiles" / "r01" / "pmc_traffic_jacobi_v5b.json"),
+    ap.add_argument("--pmc-json", type=str, default=str(ROOT / "profiles" / "r02" / "pmc_traffic_jacobi.json"),
                     help="tools/pmc_traffic.py summary of a separate rocprofv3 --pmc pass "
-                         "(FETCH_SIZE x2 + WRITE_SIZE per launch) used for roofline.traffic")
+                         "(FETCH_SIZE x2 + WRITE_SIZE per launch) used for roofline.traffic; used only "
+                         "when its recorded p and kernel variant are this run's")
     return ap.parse_args()
 
 
@@ -71,7 +75,9 @@ def main():
     from poms_amd.mg import TwoLevelVCycle
 
     n = args.cells + args.p
+    # N > 1: the library's RCCL communicator, or an exception (no silent fall-back)
     slab = SlabDistribution.from_process_group(n) if world > 1 else None
+    transport = slab.transport if slab is not None else "none"
     mg = TwoLevelVCycle(args.p, args.cells, args.coarse, ndim=3, dist=slab, chunk=args.chunk)
     bf = mg.rhs_ones()
     A = mg.A
@@ -148,19 +154,33 @@ def main():
     traffic = None
     if args.pmc_json and Path(args.pmc_json).exists():
         pm = json.loads(Path(args.pmc_json).read_text())
-        if pm.get("bytes_per_dof"):   # per-DOF HBM bytes of the same kernel, scaled to this rank's slab
+        # per-DOF HBM bytes of the SAME kernel (order p, variant) scaled to this rank's slab
+        if pm.get("bytes_per_dof") and pm.get("p") == args.p and pm.get("variant") == jac_v:
             traffic = pm["bytes_per_dof"] * local_dof
 
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         try:
             from oracle import cpu_baseline as cb
-            threads = min(16, os.cpu_count() or 1)
+            host = cb.host_info()
+            threads = host["nproc"]   # every CPU this process may use (GNU nproc)
             r = cb.time_vcycle(N=args.cpu_cells, p=args.p, Nc=args.coarse, cycles=args.cpu_cycles, threads=threads)
+            r1 = cb.time_vcycle(N=args.cpu_cells_1core, p=args.p, Nc=args.coarse, cycles=1, threads=1)
+            full = cb.time_apply(N=args.cells, p=args.p, threads=threads, reps=2)
             cpu = {"value": r["dof_per_s"], "unit": "DOF/s", "cores": r["threads"], "kind": "port",
-                   "sample": (f"{args.cpu_cycles} full two-level V-cycles (same schedule) at {args.cpu_cells}^3 "
-                              f"cells p={args.p} ({r['dof']} DOF), C/OpenMP restatement of the reference loop "
-                              f"nests (oracle/kron_cpu.c), {r['seconds_per_cycle']:.2f} s per cycle")}
+                   "nproc": host["nproc"], "os_cpu_count": host["os_cpu_count"], "cpu_model": host["cpu_model"],
+                   "sample": (f"{args.cpu_cycles} full two-level V-cycles (same schedule, incl. the reference's "
+                              f"discarded mat-vec) at {args.cpu_cells}^3 cells p={args.p} ({r['dof']} DOF) on "
+                              f"{r['threads']} threads, C/OpenMP restatement of the reference loop nests "
+                              f"(oracle/kron_cpu.c), {r['seconds_per_cycle']:.2f} s per cycle; a bench-size "
+                              f"({args.cells}^3) CPU V-cycle is ~{r['seconds_per_cycle'] * (args.cells + args.p) ** 3 / r['dof']:.0f} s "
+                              f"at this rate, outside the bounded sample"),
+                   "single_core": {"value": r1["dof_per_s"], "unit": "DOF/s", "cores": 1,
+                                   "sample": f"1 V-cycle at {args.cpu_cells_1core}^3 cells ({r1['dof']} DOF), "
+                                             f"{r1['seconds_per_cycle']:.2f} s"},
+                   "kron_apply_full_size": {"value": full["gbps"], "unit": "GB/s (16 B/DOF)",
+                                            "cores": full["threads"], "seconds_per_apply": full["seconds_per_apply"],
+                                            "sample": f"{args.cells}^3 cells ({full['dof']} DOF), the bench size"}}
         except Exception as e:  # baseline is informative only
             cpu = {"value": None, "unit": "DOF/s", "cores": 0, "kind": "port", "sample": f"failed: {e!r}"}
 
@@ -185,6 +205,7 @@ def main():
                 "global_dof": gdof, "p": args.p, "cells": args.cells, "coarse_cells": args.coarse,
                 "parallelism": f"slab{world}",
             },
+            "comm": transport,
             "roofline": {
                 "kernel": f"{KERNEL_NAMES.get(jac_v, f'variant {jac_v}')}<P={args.p},3D,SUM,JACOBI> (Kron apply + damped-Jacobi update)",
                 "bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBPS, "unit": "GB/s",

@@ -357,6 +357,19 @@ int poms_comm_unique_id(char* out, int len);          /* rank 0; broadcast it */
 int poms_comm_create(int device, const char* id, int rank, int nranks, poms_comm** out);
 int poms_comm_destroy(poms_comm* comm);
 int poms_comm_stream(poms_comm* comm, void** stream);
+/* Host transport: the same communicator API and schedule (poms_op_run_dist,
+ * lazy ring slots) with the data moved by host callbacks instead of RCCL, for
+ * process groups without RCCL peers (e.g. gloo ranks sharing one GPU in the
+ * tests).  Each call synchronises the caller's stream and stages through host
+ * memory.  exchange: send_lo (cnt doubles) to prev and recv_lo from it, send_hi
+ * to next and recv_hi from it (prev / next = -1: none); allreduce: in-place sum
+ * of cnt doubles over the ranks.  Callbacks return 0 on success.              */
+typedef int (*poms_host_exchange_fn)(void* user, const double* send_lo, double* recv_lo, const double* send_hi,
+                                     double* recv_hi, int64_t cnt, int prev, int next);
+typedef int (*poms_host_allreduce_fn)(void* user, double* buf, int64_t cnt);
+int poms_comm_create_host(int device, int rank, int nranks, poms_host_exchange_fn exchange,
+                          poms_host_allreduce_fn allreduce, void* user, poms_comm** out);
+int poms_comm_is_host(poms_comm* comm, int* yes);
 /* data -> plane 0 of the padded local array (first ghost plane); the first /
  * last `width` owned planes go to prev / next (-1: none), the neighbours'
  * planes land in the ghost planes.  Starts after the work queued on `stream`;

@@ -187,3 +187,45 @@ def time_vcycle(N: int = 96, p: int = 3, Nc: int = 8, cycles: int = 1, threads: 
     dt = (time.perf_counter() - t0) / cycles
     return {"seconds_per_cycle": dt, "dof": n ** 3, "dof_per_s": n ** 3 / dt,
             "threads": lib().oracle_num_threads(), "info_pre": ipre, "info_pos": ipos, "N": N, "p": p}
+
+
+def host_info() -> dict:
+    """The host the baseline ran on: `nproc` (the CPUs this process may use; GNU
+    nproc honours OMP_NUM_THREADS / affinity), os.cpu_count(), the CPU model."""
+    import subprocess
+    try:
+        nproc = int(subprocess.run(["nproc"], capture_output=True, text=True, check=True).stdout.strip())
+    except Exception:
+        nproc = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else (os.cpu_count() or 1)
+    model = "unknown"
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                model = line.split(":", 1)[1].strip()
+                break
+    except OSError:
+        pass
+    return {"nproc": nproc, "os_cpu_count": os.cpu_count(), "cpu_model": model}
+
+
+def time_apply(N: int, p: int = 3, threads: int | None = None, reps: int = 2) -> dict:
+    """The sum-factorised -Δu+u apply (the reference kernel's loop nest) at N^3
+    cells on the host: seconds per apply and algorithmic GB/s (16 B/DOF)."""
+    import sys
+    sys.path.insert(0, str(HERE.parent))
+    from poms_amd.splines import assemble_1d, uniform_knots
+
+    if threads:
+        lib().oracle_set_num_threads(int(threads))
+    M, K = assemble_1d(uniform_knots(p, N), p)
+    A = CpuLaplace3D(M, K, p)
+    x = A.zeros()
+    x[p:-p, p:-p, p:-p] = np.random.default_rng(0).uniform(-1, 1, (A.n,) * 3)
+    y = A.zeros()
+    A._run(x, None, y, 0)   # first touch of the temporaries
+    t0 = time.perf_counter()
+    for _ in range(reps):
+        A._run(x, None, y, 0)
+    dt = (time.perf_counter() - t0) / reps
+    return {"seconds_per_apply": dt, "dof": A.ndof, "gbps": 16.0 * A.ndof / dt / 1e9,
+            "threads": lib().oracle_num_threads(), "N": N, "p": p}

@@ -17,6 +17,7 @@
 #include <rccl/rccl.h>
 
 #include <cstring>
+#include <vector>
 
 using namespace poms;
 
@@ -34,6 +35,15 @@ struct poms_comm {
     double* ring = nullptr;         // kRing x 2 doubles
     hipEvent_t ring_ev[kRing] = {};
     int ring_next = 0;
+    // host transport (poms_comm_create_host): the same schedule with the data moved
+    // by caller-supplied host callbacks (e.g. torch.distributed / gloo) instead of
+    // RCCL -- every call synchronises the caller's stream, stages the planes or
+    // scalars through host memory and runs the callback in line
+    bool host = false;
+    poms_host_exchange_fn xchg = nullptr;
+    poms_host_allreduce_fn ar = nullptr;
+    void* user = nullptr;
+    std::vector<double> stage;      // 4 x width x plane_elems (send lo / recv lo / send hi / recv hi)
 };
 
 #define POMS_NCCL_CHECK(expr)                                                    \
@@ -50,6 +60,7 @@ static hipStream_t cstream(void* s) { return reinterpret_cast<hipStream_t>(s); }
 extern "C" {
 
 int poms_comm_destroy(poms_comm* c);
+static int comm_common_init(poms_comm* c);
 
 int poms_comm_unique_id(char* out, int len) {
     if (!out || len < (int)sizeof(ncclUniqueId)) { set_error("poms_comm_unique_id: buffer too small"); return 1; }
@@ -76,13 +87,20 @@ int poms_comm_create(int device, const char* id, int rank, int nranks, poms_comm
         delete c;
         return 1;
     }
+    if (comm_common_init(c)) {
+        poms_comm_destroy(c);
+        return 1;
+    }
+    *out = c;
+    return 0;
+}
+
+static int comm_common_init(poms_comm* c) {
     if (hipStreamCreateWithFlags(&c->cs, hipStreamNonBlocking) != hipSuccess ||
         hipEventCreateWithFlags(&c->ev_in, hipEventDisableTiming) != hipSuccess ||
         hipEventCreateWithFlags(&c->ev_halo, hipEventDisableTiming) != hipSuccess ||
         hipEventCreateWithFlags(&c->ev_red, hipEventDisableTiming) != hipSuccess) {
         set_error("poms_comm_create: stream / event creation failed");
-        ncclCommDestroy(c->comm);
-        delete c;
         return 1;
     }
     bool ok = hipMalloc(reinterpret_cast<void**>(&c->ring), poms_comm::kRing * 2 * sizeof(double)) == hipSuccess;
@@ -90,10 +108,47 @@ int poms_comm_create(int device, const char* id, int rank, int nranks, poms_comm
         ok = hipEventCreateWithFlags(&c->ring_ev[i], hipEventDisableTiming) == hipSuccess;
     if (!ok) {
         set_error("poms_comm_create: ring allocation failed");
+        return 1;
+    }
+    return 0;
+}
+
+int poms_comm_create_host(int device, int rank, int nranks, poms_host_exchange_fn xchg,
+                          poms_host_allreduce_fn ar, void* user, poms_comm** out) {
+    if (!xchg || !ar || !out || nranks < 1 || rank < 0 || rank >= nranks) {
+        set_error("poms_comm_create_host: bad argument");
+        return 1;
+    }
+    POMS_HIP_CHECK(hipSetDevice(device));
+    auto* c = new poms_comm();
+    c->rank = rank;
+    c->nranks = nranks;
+    c->device = device;
+    c->host = true;
+    c->xchg = xchg;
+    c->ar = ar;
+    c->user = user;
+    if (comm_common_init(c)) {
         poms_comm_destroy(c);
         return 1;
     }
     *out = c;
+    return 0;
+}
+
+int poms_comm_is_host(poms_comm* c, int* yes) {
+    if (!c || !yes) { set_error("poms_comm_is_host: null argument"); return 1; }
+    *yes = c->host ? 1 : 0;
+    return 0;
+}
+
+// host transport: in-place sum of `count` device doubles through the callback
+static int host_allreduce(poms_comm* c, double* buf, int64_t count, hipStream_t st) {
+    POMS_HIP_CHECK(hipStreamSynchronize(st));
+    if (c->stage.size() < (size_t)count) c->stage.resize((size_t)count);
+    POMS_HIP_CHECK(hipMemcpy(c->stage.data(), buf, count * sizeof(double), hipMemcpyDeviceToHost));
+    if (c->ar(c->user, c->stage.data(), count)) { set_error("host transport: all-reduce callback failed"); return 1; }
+    POMS_HIP_CHECK(hipMemcpy(buf, c->stage.data(), count * sizeof(double), hipMemcpyHostToDevice));
     return 0;
 }
 
@@ -129,6 +184,29 @@ int poms_halo_start(poms_comm* c, double* data, int64_t plane_elems, int64_t n_l
         return 1;
     }
     if (width == 0 || (prev < 0 && next < 0)) return 0;
+    if (c->host) {   // stage the boundary planes, exchange through the callback, copy back
+        hipStream_t st = cstream(stream);
+        POMS_HIP_CHECK(hipStreamSynchronize(st));
+        const size_t cnt = (size_t)width * (size_t)plane_elems;
+        if (c->stage.size() < 4 * cnt) c->stage.resize(4 * cnt);
+        double *slo = c->stage.data(), *rlo = slo + cnt, *shi = rlo + cnt, *rhi = shi + cnt;
+        if (prev >= 0)
+            POMS_HIP_CHECK(hipMemcpy(slo, data + (int64_t)pad * plane_elems, cnt * 8, hipMemcpyDeviceToHost));
+        if (next >= 0)
+            POMS_HIP_CHECK(hipMemcpy(shi, data + (int64_t)(pad + n_local - width) * plane_elems, cnt * 8,
+                                     hipMemcpyDeviceToHost));
+        if (c->xchg(c->user, slo, rlo, shi, rhi, (int64_t)cnt, prev, next)) {
+            set_error("host transport: exchange callback failed");
+            return 1;
+        }
+        if (prev >= 0)
+            POMS_HIP_CHECK(hipMemcpy(data + (int64_t)(pad - width) * plane_elems, rlo, cnt * 8, hipMemcpyHostToDevice));
+        if (next >= 0)
+            POMS_HIP_CHECK(hipMemcpy(data + (int64_t)(pad + n_local) * plane_elems, rhi, cnt * 8,
+                                     hipMemcpyHostToDevice));
+        POMS_HIP_CHECK(hipEventRecord(c->ev_halo, st));
+        return 0;
+    }
     POMS_HIP_CHECK(hipEventRecord(c->ev_in, cstream(stream)));
     POMS_HIP_CHECK(hipStreamWaitEvent(c->cs, c->ev_in, 0));
     const size_t cnt = (size_t)width * (size_t)plane_elems;
@@ -160,6 +238,7 @@ int poms_halo_finish(poms_comm* c, void* stream) {
 // caller queues its device -> host copy (lazy norms: the next sweep never waits).
 int poms_allreduce_sum(poms_comm* c, double* buf, int64_t count, void* stream, int wait_back) {
     if (!c || !buf || count < 0) { set_error("poms_allreduce_sum: bad argument"); return 1; }
+    if (c->host) return host_allreduce(c, buf, count, cstream(stream));
     POMS_HIP_CHECK(hipEventRecord(c->ev_in, cstream(stream)));
     POMS_HIP_CHECK(hipStreamWaitEvent(c->cs, c->ev_in, 0));
     POMS_NCCL_CHECK(ncclAllReduce(buf, buf, (size_t)count, ncclDouble, ncclSum, c->comm, c->cs));
@@ -191,6 +270,12 @@ int poms_allreduce_to_host(poms_comm* c, int ticket, int count, double* host_dst
         return 1;
     }
     double* slot = c->ring + 2 * ticket;
+    if (c->host) {
+        if (host_allreduce(c, slot, count, cstream(stream))) return 1;
+        POMS_HIP_CHECK(hipMemcpy(host_dst, slot, count * sizeof(double), hipMemcpyDeviceToHost));
+        POMS_HIP_CHECK(hipEventRecord(c->ring_ev[ticket], cstream(stream)));
+        return 0;
+    }
     POMS_HIP_CHECK(hipEventRecord(c->ev_in, cstream(stream)));
     POMS_HIP_CHECK(hipStreamWaitEvent(c->cs, c->ev_in, 0));
     POMS_NCCL_CHECK(ncclAllReduce(slot, slot, (size_t)count, ncclDouble, ncclSum, c->comm, c->cs));

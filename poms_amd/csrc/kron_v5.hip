@@ -161,11 +161,13 @@ kron_v5_kernel(const double* __restrict__ x, double* __restrict__ y, const doubl
     const int orow = r0 + wv;           // this wave's output row
     const bool row_ok = orow < g.n1;
     const int cg0 = c0 - H + 2 * lane;  // interior column of this lane's element 0
-    bool col_ok[2];
+    // output columns of this lane as a VGPR bit mask (lane-dependent bools would pin
+    // two SGPRs each for the whole march; SGPR spills cost VGPR lanes)
+    int cok = 0;
 #pragma unroll
     for (int e = 0; e < 2; ++e) {
         const int ci = 2 * lane + e;
-        col_ok[e] = ci >= H && ci < H + TO && cg0 + e < g.n2;
+        cok |= (ci >= H && ci < H + TO && cg0 + e < g.n2) ? (1 << e) : 0;
     }
     const bool fast1 = orow >= tc.lo1 && orow < tc.hi1;                          // per wave
     const bool fast2 = (c0 >= tc.lo2) && (min(c0 + TO, g.n2) <= tc.hi2);         // per workgroup
@@ -311,6 +313,37 @@ kron_v5_kernel(const double* __restrict__ x, double* __restrict__ y, const doubl
                     else if (xtra) v5_wait_vm<(PFX - 1) * 2>();
                     else v5_wait_vm<(PFX - 1) * 1>();
                 }
+                if constexpr (J0) {
+                    // x1 = omega b / diag: each wave scales the rows it DMA'd itself, once, in
+                    // place, before the barrier publishes them (instead of every reading wave
+                    // scaling all 2P+1 rows it reads: 2P+1 LDS reads and 4P+2 multiplies less
+                    // per lane and plane, and the VGPRs p = 3 lacked)
+                    const int m = g.g0 + z0 - P + t;   // global plane of x(t)
+                    const bool tp = m >= tc.lo0 && m < tc.hi0;
+                    double d0a = 0.0, d0b = 0.0;
+                    if (!tp) {
+                        const int i0 = (m + P) * W + P;
+                        d0a = a0t[i0];
+                        d0b = b0t[i0];
+                    }
+                    double* xs0 = lds + XS_OFF + (t % D) * XR * TC + 2 * lane;
+#pragma unroll
+                    for (int r = 0; r < 2; ++r) {
+                        if (r == 1 && !xtra) break;
+                        const int qr = wv + r * NW;
+                        d2 v = *(const d2*)(xs0 + qr * TC);
+                        if (tp) {
+                            const d2 sc = *(const d2*)(lds + RS_OFF + qr * TC + 2 * lane);
+                            v[0] *= sc[0];
+                            v[1] *= sc[1];
+                        } else {   // the p planes next to each global end (and ghost planes)
+                            v[0] *= j0_scale(qr, 2 * lane, d0a, d0b);
+                            v[1] *= j0_scale(qr, 2 * lane + 1, d0a, d0b);
+                        }
+                        *(d2*)(xs0 + qr * TC) = v;
+                    }
+                    __builtin_amdgcn_s_waitcnt(0xc07f);   // lgkmcnt(0): the scaled rows written
+                }
                 v5_barrier();
                 if constexpr (HASB) dma_b(zo_of(t + 1), (t + 1) & 1);
                 dma_x(t + PFX < nplanes ? z0 - P + t + PFX : -(1 << 20), (t + PFX) % D);
@@ -320,27 +353,8 @@ kron_v5_kernel(const double* __restrict__ x, double* __restrict__ y, const doubl
                 d2 xv[W];
 #pragma unroll
                 for (int k = 0; k < W; ++k) xv[k] = *(const d2*)(xs + (wv + k) * TC);
-                if constexpr (J0) {
-                    const int m = g.g0 + z0 - P + t;   // global plane of x(t)
-                    if (m >= tc.lo0 && m < tc.hi0) {
-#pragma unroll
-                        for (int k = 0; k < W; ++k) {
-                            const d2 sc = *(const d2*)(lds + RS_OFF + (wv + k) * TC + 2 * lane);
-                            xv[k][0] *= sc[0];
-                            xv[k][1] *= sc[1];
-                        }
-                    } else {   // the p planes next to each global end (and ghost planes)
-                        const int i0 = (m + P) * W + P;
-                        const double d0a = a0t[i0], d0b = b0t[i0];
-#pragma unroll
-                        for (int k = 0; k < W; ++k) {
-                            xv[k][0] *= j0_scale(wv + k, 2 * lane, d0a, d0b);
-                            xv[k][1] *= j0_scale(wv + k, 2 * lane + 1, d0a, d0b);
-                        }
-                    }
-                }
                 if constexpr (MODE == 1) {
-                    const bool ok0 = t >= 2 * P && row_ok && col_ok[0];
+                    const bool ok0 = t >= 2 * P && row_ok && (cok & 1);
                     bstore2_s(ry, ok0 ? (orow + P) * s1 * 8 + colb + (zo_of(t) + g.pd0) * (int)plane8 : 0x7ffffff0,
                               0u, xv[P][0] + xv[0][0], xv[P][1] + xv[W - 1][1]);
                     continue;
@@ -461,7 +475,7 @@ kron_v5_kernel(const double* __restrict__ x, double* __restrict__ y, const doubl
                 }
                 bool ok[2];
 #pragma unroll
-                for (int e = 0; e < 2; ++e) ok[e] = en && row_ok && col_ok[e];
+                for (int e = 0; e < 2; ++e) ok[e] = en && row_ok && ((cok >> e) & 1);
                 double outv[2];
                 if constexpr (EPI == EPI_APPLY) {
                     outv[0] = vo[0];
@@ -636,11 +650,9 @@ static int v5_launch_p(int epi, const KronPtrs& p, const KronGeom& g, const Toep
         case EPI_RESID: return v5_launch_t<P, EPI_RESID, 3, 0, 6>(p, g, tc, H, omega, st);
         case EPI_JACOBI: return v5_launch_t<P, EPI_JACOBI, 3, 0, 6, true>(p, g, tc, H, omega, st);
         case EPI_APPLYDOT: return v5_launch_t<P, EPI_APPLYDOT, 4, 0, 6>(p, g, tc, H, omega, st);
-        // x ring = b (read once, apply's policy), y = x2 streamed; p = 3 needs 130
-        // VGPRs (2 spilled at every D / CP tried): built for p <= 2 only
-        case EPI_JACOBI0:
-            if constexpr (P <= 2) return v5_launch_t<P, EPI_JACOBI0, 4, 0, 14>(p, g, tc, H, omega, st);
-            break;
+        // x ring = b (read once, apply's policy), scaled in place to x1 after it lands;
+        // y = x2 streamed
+        case EPI_JACOBI0: return v5_launch_t<P, EPI_JACOBI0, 4, 0, 14>(p, g, tc, H, omega, st);
     }
     set_error("v5: epilogue not built");
     return 1;

@@ -603,7 +603,7 @@ static int op_geom(poms_op* o, int64_t zb, int64_t ze, KronGeom& g, int v = -1, 
         static int ord = -1;
         if (ord < 0) {
             const char* e = getenv("POMS_TILE_ORDER");
-            ord = e ? (atoi(e) ? 1 : 0) : 1;
+            ord = e ? (atoi(e) ? 1 : 0) : 0;
         }
         g.order = ord;
     }
@@ -666,7 +666,8 @@ static int resolve_variant(const poms_op* o, int epi) {
     }
     if (v == 11 && (!v5_ok(o) || epi == EPI_JACOBI0))   // v6: no two-sweeps-from-zero epilogue
         v = (v5_ok(o) && (epi != EPI_JACOBI0 || o->pmax <= 2)) ? 10 : 9;
-    if (v == 10 && (!v5_ok(o) || (epi == EPI_JACOBI0 && o->pmax > 2))) v = 9;   // v5 two-sweeps: p <= 2
+    // v5 two-sweeps-from-zero: p <= 2 (at p = 3 the build still spills)
+    if (v == 10 && (!v5_ok(o) || (epi == EPI_JACOBI0 && o->pmax > 2))) v = 9;
     return v;
 }
 

@@ -16,7 +16,6 @@ the first ``n % w`` ranks get one extra plane (515 = 3x65 + 5x64).
 from __future__ import annotations
 
 import os
-import warnings
 from dataclasses import dataclass
 
 import torch
@@ -61,15 +60,35 @@ class SlabDistribution:
         return self.end - self.start
 
     @classmethod
-    def from_process_group(cls, n0_global: int, group=None, device_reductions: bool | None = None
-                           ) -> "SlabDistribution":
+    def from_process_group(cls, n0_global: int, group=None, device_reductions: bool | None = None,
+                           host_transport: bool = False) -> "SlabDistribution":
+        """Slab of this rank.  With the ``nccl`` (RCCL) backend the library's own
+        communicator is used (``POMS_NATIVE_COMM=0`` selects torch.distributed
+        instead); if it cannot be created or fails its self-test this RAISES --
+        a silent fall-back would hide a broken production path.  ``host_transport``
+        (any backend, e.g. gloo): the same native schedule with the data moved by
+        torch.distributed host callbacks (``poms_comm_create_host``)."""
         import torch.distributed as dist
         backend = dist.get_backend(group)
         d = cls(n0_global, dist.get_rank(group), dist.get_world_size(group), group,
                 cuda_transport=(backend == "nccl"), device_reductions=device_reductions)
-        if backend == "nccl" and d.world > 1 and os.environ.get("POMS_NATIVE_COMM", "1") != "0":
+        if host_transport:
+            if d.device_reductions is None or not d.device_reductions:
+                d.device_reductions = True
+            d.native = NativeComm.create_host(group)
+        elif backend == "nccl" and d.world > 1 and os.environ.get("POMS_NATIVE_COMM", "1") != "0":
             d.native = NativeComm.create(group)
         return d
+
+    @property
+    def transport(self) -> str:
+        """Which path moves ghosts and sums: "native" (RCCL from C), "native-host"
+        (the C schedule over host callbacks), "torch" (torch.distributed) or "none"."""
+        if self.world == 1:
+            return "none"
+        if self.native is None:
+            return "torch"
+        return "native-host" if self.native.is_host else "native"
 
     # ------------------------------------------------------------------
     def start_exchange(self, data: torch.Tensor, width: int, pad: int):
@@ -148,44 +167,110 @@ class NativeComm:
     against their known results) and returns None -- the torch.distributed path
     is used -- if anything fails."""
 
-    def __init__(self, handle, device: int):
+    def __init__(self, handle, device: int, callbacks=None):
         import ctypes as C
         from . import _lib
         self.h = handle
         self.device = device
+        self._callbacks = callbacks   # host transport: keep the ctypes thunks alive
         s = C.c_void_p()
         _lib.call("poms_comm_stream", self.h, C.byref(s))
         self.stream = torch.cuda.ExternalStream(s.value, device=torch.device("cuda", device))
+        yes = C.c_int()
+        _lib.call("poms_comm_is_host", self.h, C.byref(yes))
+        self.is_host = bool(yes.value)
 
     @classmethod
     def create(cls, group=None):
+        """RCCL communicator over the group's ranks, self-tested; raises on failure."""
         import ctypes as C
         import torch.distributed as dist
         from . import _lib
+        dev = torch.cuda.current_device()
+        nb = _lib.lib.poms_comm_id_bytes()
+        obj = [None]
+        if dist.get_rank(group) == 0:
+            buf = C.create_string_buffer(nb)
+            _lib.call("poms_comm_unique_id", buf, nb)
+            obj[0] = bytes(buf.raw[:nb])
+        dist.broadcast_object_list(obj, src=dist.get_global_rank(group, 0) if group is not None else 0,
+                                   group=group)
+        h = C.c_void_p()
+        _lib.call("poms_comm_create", dev, C.c_char_p(obj[0]), dist.get_rank(group),
+                  dist.get_world_size(group), C.byref(h))
+        comm = cls(h, dev)
+        comm._check_self_test(group)
+        return comm
+
+    @classmethod
+    def create_host(cls, group=None):
+        """The native schedule over torch.distributed host callbacks (any backend).
+
+        The C side stages the boundary planes / scalars through host memory and
+        calls back: the exchange is one ``batch_isend_irecv`` with rank +-1 on CPU
+        tensors, the sum one ``all_reduce``.  Used by the multi-rank tests to drive
+        ``poms_op_run_dist``'s schedule with real neighbours where RCCL cannot run
+        (several ranks on one GPU)."""
+        import ctypes as C
+        import numpy as np
+        import torch.distributed as dist
+        from . import _lib
+
+        def peer(r):
+            return r if group is None else dist.get_global_rank(group, r)
+
+        def view(ptr, cnt):
+            return torch.from_numpy(np.ctypeslib.as_array(C.cast(ptr, C.POINTER(C.c_double)), shape=(int(cnt),)))
+
+        def exchange(user, slo, rlo, shi, rhi, cnt, prev, nxt):
+            try:
+                ops = []
+                if prev >= 0:
+                    ops.append(dist.P2POp(dist.isend, view(slo, cnt), peer(prev), group))
+                    ops.append(dist.P2POp(dist.irecv, view(rlo, cnt), peer(prev), group))
+                if nxt >= 0:
+                    ops.append(dist.P2POp(dist.isend, view(shi, cnt), peer(nxt), group))
+                    ops.append(dist.P2POp(dist.irecv, view(rhi, cnt), peer(nxt), group))
+                if ops:
+                    for w in dist.batch_isend_irecv(ops):
+                        w.wait()
+                return 0
+            except Exception:   # reported through poms_last_error by the caller
+                return 1
+
+        def allreduce(user, buf, cnt):
+            try:
+                dist.all_reduce(view(buf, cnt), group=group)
+                return 0
+            except Exception:
+                return 1
+
+        XF = C.CFUNCTYPE(C.c_int, C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p, C.c_int64,
+                         C.c_int, C.c_int)
+        AF = C.CFUNCTYPE(C.c_int, C.c_void_p, C.c_void_p, C.c_int64)
+        cbs = (XF(exchange), AF(allreduce))
+        dev = torch.cuda.current_device()
+        h = C.c_void_p()
+        _lib.call("poms_comm_create_host", dev, dist.get_rank(group), dist.get_world_size(group),
+                  C.cast(cbs[0], C.c_void_p), C.cast(cbs[1], C.c_void_p), None, C.byref(h))
+        comm = cls(h, dev, callbacks=cbs)
+        comm._check_self_test(group)
+        return comm
+
+    def _check_self_test(self, group):
+        """All ranks agree that the all-reduce and the ghost exchange work, or raise."""
+        import torch.distributed as dist
         try:
-            dev = torch.cuda.current_device()
-            nb = _lib.lib.poms_comm_id_bytes()
-            obj = [None]
-            if dist.get_rank(group) == 0:
-                buf = C.create_string_buffer(nb)
-                _lib.call("poms_comm_unique_id", buf, nb)
-                obj[0] = bytes(buf.raw[:nb])
-            dist.broadcast_object_list(obj, src=dist.get_global_rank(group, 0) if group is not None else 0,
-                                       group=group)
-            h = C.c_void_p()
-            _lib.call("poms_comm_create", dev, C.c_char_p(obj[0]), dist.get_rank(group),
-                      dist.get_world_size(group), C.byref(h))
-            comm = cls(h, dev)
-            ok = comm._self_test(dist.get_rank(group), dist.get_world_size(group))
-        except Exception as e:   # fall back to torch.distributed
-            warnings.warn(f"native RCCL communicator unavailable ({e!r}); using torch.distributed")
-            return None
-        oks = torch.tensor([1.0 if ok else 0.0], dtype=torch.float64, device=f"cuda:{dev}")
+            ok = self._self_test(dist.get_rank(group), dist.get_world_size(group))
+            err = ""
+        except Exception as e:
+            ok, err = False, repr(e)
+        oks = torch.tensor([1.0 if ok else 0.0], dtype=torch.float64)
+        if dist.get_backend(group) == "nccl":
+            oks = oks.to(f"cuda:{self.device}")
         dist.all_reduce(oks, op=dist.ReduceOp.MIN, group=group)
         if float(oks.item()) < 1.0:
-            warnings.warn("native RCCL communicator failed its self-test; using torch.distributed")
-            return None
-        return comm
+            raise RuntimeError(f"native communicator failed its self-test on some rank {err}".strip())
 
     def _self_test(self, rank: int, world: int) -> bool:
         from . import runtime as rt

@@ -81,7 +81,11 @@ class KronTransfer:
         out = self.coarse_empty() if out is None else out
         _lib.call("poms_restrict", self._h, rt.ptr(fine._data), rt.ptr(out), rt.stream_handle())
         if allreduce and self.space.is_distributed:
-            rt.Comm.from_env(self.space.dist.group).allreduce_sum_(out)
+            d = self.space.dist
+            if d.native is not None:   # the library's communicator, on the device stream
+                d.native.allreduce(out, rt.stream_handle(), wait_back=True)
+            else:
+                rt.Comm.from_env(d.group).allreduce_sum_(out)
         return out
 
     def prolong_add(self, coarse: torch.Tensor, fine: StencilVector) -> StencilVector:

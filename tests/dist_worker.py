@@ -125,7 +125,9 @@ def run_gpu():
     M, K = assemble_1d(uniform_knots(p, N), p)
     rng = np.random.default_rng(3)
     xg, bg = rng.standard_normal((n, n, n)), rng.standard_normal((n, n, n))
-    d = SlabDistribution.from_process_group(n)
+    host_tr = os.environ.get("POMS_TEST_HOST_TRANSPORT") == "1"
+    d = SlabDistribution.from_process_group(n, host_transport=host_tr)
+    check(d.transport == ("native-host" if host_tr else "torch"), f"transport {d.transport}")
     V = StencilVectorSpace([n] * 3, [p] * 3, dist=d)
     A = KronOperator.laplace(V, [M] * 3, [K] * 3)
     x, b = V.zeros().from_numpy(xg), V.zeros().from_numpy(bg)
@@ -141,6 +143,9 @@ def run_gpu():
     dr = 2.0 / 3.0 * (bg - Ag) / D
     check(rel(xo.to_local_numpy(), (xg + dr)[sl]) <= 1e-14, "distributed jacobi sweep")
     check(abs(nrm - float(np.vdot(dr, dr))) <= 1e-12 * float(np.vdot(dr, dr)), "global sweep norm")
+    if host_tr:   # the lazily read, all-reduced sweep norm through the C ring slots
+        lz = A.jacobi_sweep(b, x, xo, 2.0 / 3.0, want_norm=True, lazy=True)
+        check(abs(lz.value() - float(np.vdot(dr, dr))) <= 1e-12 * float(np.vdot(dr, dr)), "lazy global norm")
     g = x.dot(b)
     check(abs(g - float(np.vdot(xg, bg))) <= 1e-12 * abs(float(np.vdot(xg, bg))) + 1e-12, "global dot")
     # transfer: slab restriction + allreduce, prolongation on the owned planes
@@ -158,7 +163,8 @@ def run_gpu():
     check(rel(z.to_local_numpy(), pz[sl]) <= 1e-14, "distributed prolongation")
     # two-level V-cycle over the slabs vs the global oracle (p=2: stable smoother)
     devred = os.environ.get("POMS_TEST_DEVRED") == "1"
-    mg = TwoLevelVCycle(2, 16, 4, ndim=3, dist=SlabDistribution.from_process_group(18, device_reductions=devred))
+    mg = TwoLevelVCycle(2, 16, 4, ndim=3, dist=SlabDistribution.from_process_group(18, device_reductions=devred,
+                                                                                   host_transport=host_tr))
     assert mg.space.lazy_reductions == devred or not devred
     bf = mg.rhs_ones()
     xf2, ipre, ipos = mg.cycle(bf)

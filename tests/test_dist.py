@@ -77,6 +77,19 @@ def test_two_rank_distributed_operator_and_vcycle_gpu(device_reductions):
 
 @pytest.mark.gpu
 @pytest.mark.parametrize("world", [2, 3])
+def test_two_rank_native_schedule_with_peers_gpu(world):
+    """The production slab schedule (poms_op_run_dist: exchange, interior planes,
+    both boundaries in one launch; lazy ring-slot norms; device-scalar pcg;
+    restriction all-reduce through the library communicator) with REAL
+    neighbours: the communicator's host transport moves the planes and sums over
+    gloo, since RCCL cannot pair ranks that share one GPU."""
+    import torch
+    assert torch.cuda.device_count() >= 1, "GPU test selected but no GPU visible"
+    _launch("gpu", world=world, extra_env={"POMS_TEST_DEVRED": "1", "POMS_TEST_HOST_TRANSPORT": "1"})
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("world", [2, 3])
 def test_distributed_kron_solve_gpu(world):
     import torch
     assert torch.cuda.device_count() >= 1, "GPU test selected but no GPU visible"

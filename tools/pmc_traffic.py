@@ -1,7 +1,7 @@
 #!/usr/bin/env python3
 """HBM traffic per launch from rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes.
 
-    python tools/pmc_traffic.py gpurun_out/pmc <kernel-substring> <dof> [out.json]
+    python tools/pmc_traffic.py gpurun_out/pmc <kernel-substring> <dof> [out.json [p variant]]
 
 Corrections (MI355X_MICROARCH.md, HBM section, gfx950): FETCH_SIZE counts half
 of the bytes of wide streaming reads (x2); WRITE_SIZE is exact for streaming
@@ -37,6 +37,8 @@ def main():
            "hbm_read_bytes_per_launch": rd, "hbm_write_bytes_per_launch": wr,
            "hbm_bytes_per_launch": rd + wr, "bytes_per_dof": (rd + wr) / dof,
            "correction": "read = 2 x FETCH_SIZE (gfx950), write = WRITE_SIZE; KiB -> bytes"}
+    if len(sys.argv) > 6:   # optional provenance: p, kernel variant (bench.py matches them)
+        out["p"], out["variant"] = int(sys.argv[5]), int(sys.argv[6])
     print(json.dumps(out, indent=1))
     if len(sys.argv) > 4:
         Path(sys.argv[4]).write_text(json.dumps(out, indent=1))
