@@ -33,6 +33,8 @@
 // Preconditions (host): 3D, FORM_SUM, P <= 3, storage pads == P, array < 2 GiB.
 #include "common.hpp"
 
+#include <cstdlib>
+
 namespace poms {
 
 typedef __attribute__((address_space(3))) void lds5_void_t;
@@ -84,7 +86,8 @@ __device__ __forceinline__ void v5_barrier() {
 // aligned layout): one 16-B store per lane, else two 8-B stores.
 // JDOT: the Jacobi sweep also accumulates x_out . b (only the last sweep of a
 // preconditioner call asks for it).
-template <int P, int EPI, int D, int MODE = 0, int CP = 0, bool XH = false, bool ST16 = true, bool JDOT = true>
+template <int P, int EPI, int D, int MODE = 0, int CP = 0, bool XH = false, bool ST16 = true, bool JDOT = true,
+          bool SAME12 = false>
 __global__ void __launch_bounds__(1024, 1)
 kron_v5_kernel(const double* __restrict__ x, double* __restrict__ y, const double* __restrict__ bvec,
                const double* __restrict__ a0t, const double* __restrict__ b0t,
@@ -107,7 +110,11 @@ kron_v5_kernel(const double* __restrict__ x, double* __restrict__ y, const doubl
     constexpr bool J0 = (EPI == EPI_JACOBI0);
     constexpr bool HIST = APD || (JAC && XH) || J0;   // x (J0: x1) at the output point from a register history
     constexpr bool XIN = JAC && !XH;            // ... or DMA'd next to b (fewer VGPRs, 8 B/DOF more reads)
-    constexpr int XAUX = (CP & 1) ? 2 : 0, BAUX = (CP & 2) ? 2 : 0, YAUX = (CP & 4) ? 2 : 0;
+    // y stores: nt (bit 4), or sc1 (bit 16: written through, the line is dropped from
+    // the XCD's L2 instead of kept -- leaves the L2 to the x halo rows the neighbouring
+    // tiles re-read), or sc0 sc1 (bit 32)
+    constexpr int XAUX = (CP & 1) ? 2 : 0, BAUX = (CP & 2) ? 2 : 0;
+    constexpr int YAUX = (CP & 16) ? 16 : (CP & 32) ? 17 : (CP & 4) ? 2 : 0;
     constexpr int NWIN = 2 * P + 2;     // columns 2j-P .. 2j+1+P of a lane's pair
     static_assert(D >= 3 || !HASB, "the b ring's wait count assumes x(t) was issued before b(t)");
     typedef double d2 __attribute__((ext_vector_type(2)));
@@ -129,6 +136,11 @@ kron_v5_kernel(const double* __restrict__ x, double* __restrict__ y, const doubl
     constexpr int LDS_N = D1_OFF + (J0 ? 2 * XR : 0);
     __shared__ __attribute__((aligned(16))) double lds[LDS_N];
 
+    // SAME12: axis 2's Toeplitz rows equal axis 1's bitwise (one knot vector on both
+    // axes): one set of constants held in SGPRs instead of two (the set the
+    // compiler otherwise spilled into VGPR lanes, read back by v_readlane per plane)
+#define T2A(k) (SAME12 ? tc.t1a[k] : tc.t2a[k])
+#define T2B(k) (SAME12 ? tc.t1b[k] : tc.t2b[k])
     const int tid = threadIdx.x;
     const int lane = tid & 63;
     const int wv = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -211,8 +223,8 @@ kron_v5_kernel(const double* __restrict__ x, double* __restrict__ y, const doubl
     // Recomputed where needed rather than held in 8 VGPRs across the march.
     auto diag_xy = [&](int e, double& X, double& Y) {
         const double d1a = ra[P], d1b = rb[P];
-        const double d2a = fast2 ? tc.t2a[0] : lds[C2_OFF + P * TC + 2 * lane + e];
-        const double d2b = fast2 ? tc.t2b[0] : lds[C2_OFF + (W + P) * TC + 2 * lane + e];
+        const double d2a = fast2 ? T2A(0) : lds[C2_OFF + P * TC + 2 * lane + e];
+        const double d2b = fast2 ? T2B(0) : lds[C2_OFF + (W + P) * TC + 2 * lane + e];
         X = d1a * d2a;
         Y = fma(d1b, d2a, d1a * d2b);
     };
@@ -418,12 +430,12 @@ kron_v5_kernel(const double* __restrict__ x, double* __restrict__ y, const doubl
                             pu[k] = wu[e + P - k] + wu[e + P + k];
                             pv[k] = wvv[e + P - k] + wvv[e + P + k];
                         }
-                        double c = tc.t2a[0] * pu[0];
-                        double d = fma(tc.t2a[0], pv[0], tc.t2b[0] * pu[0]);
+                        double c = T2A(0) * pu[0];
+                        double d = fma(T2A(0), pv[0], T2B(0) * pu[0]);
 #pragma unroll
                         for (int k = 1; k <= P; ++k) {
-                            c = fma(tc.t2a[k], pu[k], c);
-                            d = fma(tc.t2a[k], pv[k], fma(tc.t2b[k], pu[k], d));
+                            c = fma(T2A(k), pu[k], c);
+                            d = fma(T2A(k), pv[k], fma(T2B(k), pu[k], d));
                         }
                         cc[e] = c;
                         dd[e] = d;
@@ -597,15 +609,18 @@ kron_v5_kernel(const double* __restrict__ x, double* __restrict__ y, const doubl
     }
 }
 
-template <int P, int EPI, int D, int MODE = 0, int CP = 0, bool XH = false, bool ST16 = true, bool JDOT = true>
-static int v5_launch_t1(const KronPtrs& p, const KronGeom& g, const ToepConst& tc, int H, double omega,
+#undef T2A
+#undef T2B
+
+template <int P, int EPI, int D, int MODE, int CP, bool XH, bool ST16, bool JDOT, bool SAME12>
+static int v5_launch_t2(const KronPtrs& p, const KronGeom& g, const ToepConst& tc, int H, double omega,
                         hipStream_t st) {
     // the hand-counted vmcnt waits assume the only VMEM ops in the loop are the
     // DMAs and the store: a build that spills to scratch would break them
     static int scratch = -1;
     if (scratch < 0) {
         hipFuncAttributes at{};
-        if (hipFuncGetAttributes(&at, reinterpret_cast<const void*>(&kron_v5_kernel<P, EPI, D, MODE, CP, XH, ST16, JDOT>)) != hipSuccess) {
+        if (hipFuncGetAttributes(&at, reinterpret_cast<const void*>(&kron_v5_kernel<P, EPI, D, MODE, CP, XH, ST16, JDOT, SAME12>)) != hipSuccess) {
             set_error("v5: hipFuncGetAttributes failed");
             return 1;
         }
@@ -616,9 +631,23 @@ static int v5_launch_t1(const KronPtrs& p, const KronGeom& g, const ToepConst& t
         return 1;
     }
     const int nblk = g.tiles2 * g.tiles1 * g.nchunks;
-    hipLaunchKernelGGL((kron_v5_kernel<P, EPI, D, MODE, CP, XH, ST16, JDOT>), dim3(nblk), dim3(1024), 0, st, p.x, p.y, p.b, p.a0t, p.b0t,
-                       p.a1, p.b1, p.a2, p.b2, p.partial, p.partial2, p.rdiag0, g, tc, H, omega);
+    hipLaunchKernelGGL((kron_v5_kernel<P, EPI, D, MODE, CP, XH, ST16, JDOT, SAME12>), dim3(nblk), dim3(1024), 0, st, p.x,
+                       p.y, p.b, p.a0t, p.b0t, p.a1, p.b1, p.a2, p.b2, p.partial, p.partial2, p.rdiag0, g, tc, H, omega);
     return 0;
+}
+
+template <int P, int EPI, int D, int MODE = 0, int CP = 0, bool XH = false, bool ST16 = true, bool JDOT = true>
+static int v5_launch_t1(const KronPtrs& p, const KronGeom& g, const ToepConst& tc, int H, double omega,
+                        hipStream_t st) {
+    bool same = true;   // the axis-1 / axis-2 Toeplitz rows, bitwise
+    for (int k = 0; k <= P; ++k)
+        same = same && tc.t1a[k] == tc.t2a[k] && tc.t1b[k] == tc.t2b[k];
+    if constexpr (MODE != 0) {   // diagnostic builds: the cubic headline grid only
+        if (!same) { set_error("v5 diag mode: needs equal axis-1 / axis-2 Toeplitz rows"); return 1; }
+        return v5_launch_t2<P, EPI, D, MODE, CP, XH, ST16, JDOT, true>(p, g, tc, H, omega, st);
+    }
+    return same ? v5_launch_t2<P, EPI, D, MODE, CP, XH, ST16, JDOT, true>(p, g, tc, H, omega, st)
+                : v5_launch_t2<P, EPI, D, MODE, CP, XH, ST16, JDOT, false>(p, g, tc, H, omega, st);
 }
 
 // 16-B stores only where every lane's store address is 16-B aligned
@@ -637,6 +666,18 @@ static int v5_launch_t(const KronPtrs& p, const KronGeom& g, const ToepConst& tc
                 : v5_launch_t1<P, EPI, D, MODE, CP, XHU, false>(p, g, tc, H, omega, st);
 }
 
+// y-store cache policy of the apply / Jacobi builds (tuning: POMS_V5_STORE = 0 nt,
+// 1 sc1, 2 sc0 sc1)
+static int store_policy() {
+    static int sp = -1;
+    if (sp < 0) {
+        const char* e = getenv("POMS_V5_STORE");
+        sp = e ? atoi(e) : 0;
+        if (sp < 0 || sp > 2) sp = 0;
+    }
+    return sp;
+}
+
 template <int P>
 static int v5_launch_p(int epi, const KronPtrs& p, const KronGeom& g, const ToepConst& tc, int H, double omega,
                        hipStream_t st) {
@@ -646,9 +687,15 @@ static int v5_launch_p(int epi, const KronPtrs& p, const KronGeom& g, const Toep
         // residual 713 -> 672, Jacobi 886 -> 777; nt x DMAs cost 15 %: the halo rows
         // are re-read by the neighbouring tiles)
         // apply: also nt on the x rows no other tile reads (variant 109: 568 -> 539 us)
-        case EPI_APPLY: return v5_launch_t<P, EPI_APPLY, 4, 0, 14>(p, g, tc, H, omega, st);
+        case EPI_APPLY:
+            if (store_policy() == 1) return v5_launch_t<P, EPI_APPLY, 4, 0, 10 | 16>(p, g, tc, H, omega, st);
+            if (store_policy() == 2) return v5_launch_t<P, EPI_APPLY, 4, 0, 10 | 32>(p, g, tc, H, omega, st);
+            return v5_launch_t<P, EPI_APPLY, 4, 0, 14>(p, g, tc, H, omega, st);
         case EPI_RESID: return v5_launch_t<P, EPI_RESID, 3, 0, 6>(p, g, tc, H, omega, st);
-        case EPI_JACOBI: return v5_launch_t<P, EPI_JACOBI, 3, 0, 6, true>(p, g, tc, H, omega, st);
+        case EPI_JACOBI:
+            if (store_policy() == 1) return v5_launch_t<P, EPI_JACOBI, 3, 0, 2 | 16, true>(p, g, tc, H, omega, st);
+            if (store_policy() == 2) return v5_launch_t<P, EPI_JACOBI, 3, 0, 2 | 32, true>(p, g, tc, H, omega, st);
+            return v5_launch_t<P, EPI_JACOBI, 3, 0, 6, true>(p, g, tc, H, omega, st);
         case EPI_APPLYDOT: return v5_launch_t<P, EPI_APPLYDOT, 4, 0, 6>(p, g, tc, H, omega, st);
         // x ring = b (read once, apply's policy), scaled in place to x1 after it lands;
         // y = x2 streamed

@@ -1,5 +1,8 @@
 set -u
 cd $GRAFT_REPO_ROOT
-timeout -k 10 200 python tools/kernel_bench.py --cells 256 --p 2 --reps 10 --rounds 2 --kinds from_zero,jacobi --variants 10,9 --flush > gpurun_out/kb_chk.log 2>&1
-timeout -k 10 200 python tools/kernel_bench.py --cells 512 --p 3 --reps 10 --rounds 2 --kinds apply,jacobi --variants 10 >> gpurun_out/kb_chk.log 2>&1
-timeout -k 10 1000 python -u -m pytest tests -m gpu -q -x --timeout 300 --timeout-method thread -p no:cacheprovider > gpurun_out/pt_chk.log 2>&1; echo rc=$? >> gpurun_out/pt_chk.log
+: > gpurun_out/kb_chk.log
+for sp in 0 1 2 0; do
+POMS_V5_STORE=$sp timeout -k 10 300 python tools/kernel_bench.py --cells 512 --p 3 --reps 10 --rounds 2 --kinds apply,jacobi --variants 10 | sed "s/^{/{\"sp\": $sp, /" >> gpurun_out/kb_chk.log || exit 1
+done
+POMS_V5_STORE=1 bash tools/pmc_traffic.sh j10sc1 "kron_v5_kernel<3, 2, 3, 0, 18," --cells 512 --p 3 --kinds jacobi --variants 10
+POMS_V5_STORE=1 bash tools/pmc_traffic.sh a10sc1 "kron_v5_kernel<3, 0, 4, 0, 26," --cells 512 --p 3 --kinds apply --variants 10
