@@ -33,7 +33,7 @@
 extern "C" {
 #endif
 
-#define POMS_ABI_VERSION 2
+#define POMS_ABI_VERSION 3
 
 /* operator forms (see poms_op_create) */
 #define POMS_FORM_SINGLE 0 /* y = F0 (x) F1 (x) F2 x                                  */
@@ -55,7 +55,12 @@ typedef struct poms_layout {
                       * A pitch that is a multiple of 16 together with a base
                       * pointer whose column pads[2] sits on a 128-B line makes
                       * every row segment of a 16k-column tile start on a line. */
+    int64_t flags;   /* bit 0 (POMS_LAYOUT_GHOST_DATA): the ghost rows / columns
+                      * of axes 1 and 2 may hold data (a block of a decomposition
+                      * of those axes, spl Cart): vector operations then touch
+                      * the interior only instead of whole interior planes.   */
 } poms_layout;
+#define POMS_LAYOUT_GHOST_DATA 1
 
 /* ---- library / context ---------------------------------------------------- */
 int         poms_abi_version(void);
@@ -126,19 +131,23 @@ int poms_op_set_chunk(poms_op* op, int chunk);
 int poms_op_set_tile_cols(poms_op* op, int cols);
 /* Kernel variant.  All variants compute the same operator:
  *   0 = general (any band rows, any pads);
- *   1-3 = v2 Toeplitz-interior kernels (4x4, 8x2, 8x4 waves x rows);
  *   4 = v3: axis-2 pass by DPP lane shifts, (a, b) tile in LDS, one barrier per plane;
- *   5 = v3 with 16 waves (32-row tile, p <= 3);   6 = v3 with x prefetched two planes ahead;
  *   7 = v4: axis-1-first, x planes DMA'd into an LDS ring (buffer_load ... lds),
  *       two columns per lane, symmetric Toeplitz pair sums;
  *   8 = auto (default when pads == pmax): the fastest measured kernel per epilogue;
  *   9 = v3 addressing each array through one buffer resource (arrays < 2 GiB);
  *  10 = v5: 128-column tiles (112 line-aligned output columns on an aligned
  *       layout), one row per wave, x DMA'd into an LDS ring, axis-1-first
- *       (3D FORM_SUM, arrays < 2 GiB; other operators and two-sweeps-from-zero
- *       run variant 9).
- * Variants 1-10 need storage pads == pmax on every used axis.                 */
+ *       (3D FORM_SUM, arrays < 2 GiB, not at odd p with ghost corners; other
+ *       operators and two-sweeps-from-zero at p = 3 run variant 9);
+ *  90-109 = diagnostic / tuning builds (memory-only, compute-only, cache policies).
+ * Variants 4-10 need storage pads == pmax on every used axis.                  */
 int poms_op_set_variant(poms_op* op, int variant);
+/* Declare that the ghost edges / corners of axes 1 and 2 may hold non-zero data:
+ * the vector is a block of a decomposition of axes 1 and 2 (spl Cart,
+ * `sources/tests/test_kron_dot.py:51-55`), not an axis-0 slab whose ghosts off
+ * axis 0 are zero.  Kernels that rely on zero corner ghosts are not selected.   */
+int poms_op_set_ghost_corners(poms_op* op, int yes);
 int poms_op_get_variant(poms_op* op, int* variant);
 /* The variant one launch of `epilogue` runs after automatic selection and
  * fall-backs: 0 apply, 1 residual, 2 Jacobi sweep, 3 two sweeps from zero,
@@ -215,11 +224,6 @@ int poms_op_from_zero_supported(poms_op* op, int* yes);
  * first damped-Jacobi sweep from x0 = 0 (A.0 = 0 exactly).                    */
 int poms_op_diag_scale(poms_op* op, double scale, const double* b, double* x,
                        int want_norm, void* stream);
-/* DIAGNOSTIC ONLY: run the s_memtime-stamped build of the kernel (3D p=3,
- * variants 1/2) and write 8 per-phase cycle sums per wave into dbg (device,
- * nwaves*8 uint64).  Stamps perturb the schedule: read shares, not times.    */
-int poms_op_profile_phases(poms_op* op, int jacobi, const double* b, const double* x,
-                           double* y, uint64_t* dbg, int64_t* nwaves, void* stream);
 /* Number of norm partials the last want_norm launch on this op produced. */
 int poms_op_last_partials(poms_op* op, int64_t* count);
 

@@ -19,6 +19,7 @@ HEADER_PATH = _HERE.parent / "include" / "poms_hip.h"
 
 FORM_SINGLE = 0
 FORM_SUM = 1
+LAYOUT_GHOST_DATA = 1
 
 
 class PomsError(RuntimeError):
@@ -26,15 +27,16 @@ class PomsError(RuntimeError):
 
 
 class Layout(C.Structure):
-    _fields_ = [("n", C.c_int64 * 3), ("pads", C.c_int64 * 3), ("pitch", C.c_int64)]
+    _fields_ = [("n", C.c_int64 * 3), ("pads", C.c_int64 * 3), ("pitch", C.c_int64), ("flags", C.c_int64)]
 
     @classmethod
-    def make(cls, n, pads, pitch=0):
+    def make(cls, n, pads, pitch=0, flags=0):
         lay = cls()
         for d in range(3):
             lay.n[d] = int(n[d])
             lay.pads[d] = int(pads[d])
         lay.pitch = int(pitch)
+        lay.flags = int(flags)
         return lay
 
 
@@ -96,7 +98,7 @@ _SIGS = {
     "poms_op_from_zero_supported": [_vp, C.POINTER(_i)],
     "poms_op_diag_scale": [_vp, _d, _vp, _vp, _i, _vp],
     "poms_op_last_partials": [_vp, C.POINTER(_i64)],
-    "poms_op_profile_phases": [_vp, _i, _vp, _vp, _vp, _vp, C.POINTER(_i64), _vp],
+    "poms_op_set_ghost_corners": [_vp, _i],
     "poms_kron_dot_2d": [_vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _i64, _vp, _i64],
     "poms_vec_axpby": [_vp, _LP, _d, _vp, _d, _vp, _vp, _vp],
     "poms_vec_scale": [_vp, _LP, _d, _vp, _vp, _vp],

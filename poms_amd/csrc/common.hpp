@@ -100,7 +100,6 @@ struct KronPtrs {
     double* partial;    // Jacobi: per-block sums of dr.dr (or null)
     double* partial2;   // Jacobi: per-block sums of x_out.b (or null)
     const double* rdiag0 = nullptr;  // 1/diag(A) per global plane inside the axis-1/2 Toeplitz interior
-    const double* ab0 = nullptr;     // axis-0 (A0, M0) band pairs, global plane j at pair row j + 2P (v6)
 };
 
 // Banded LU factors of one axis of a Kronecker solve (kron_solve.hip).

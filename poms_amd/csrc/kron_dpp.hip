@@ -540,8 +540,8 @@ static int v3_launch_p(bool is3d, int form, int epi, const KronPtrs& p, const Kr
                             : v3_launch_e<P, R, NW, false, FORM_SINGLE, PF, FLAT>(epi, p, g, tc, omega, st);
 }
 
-// variant 4: 8 waves x 2 rows (16 x (64-2P) tile, 2 WGs/CU);
-// variant 5: 16 waves x 2 rows (32 x (64-2P) tile, 1 WG/CU, less halo recompute)
+// variant 4: 8 waves x 2 rows (16 x (64-2P) tile, 2 WGs/CU); variant 9: the same
+// tile addressing each array through one buffer resource
 int kron_v3_launch(int variant, int pmax, bool is3d, int form, int epi, const KronPtrs& p,
                    const KronGeom& g, const ToepConst& tc, double omega, hipStream_t st) {
     if (variant == 90 || variant == 91) {   // DIAGNOSTIC: memory-only / compute-only apply, 3D SUM P=3
@@ -560,23 +560,6 @@ int kron_v3_launch(int variant, int pmax, bool is3d, int form, int epi, const Kr
                 case 4: return v3_launch_p<4, 2, 8, 1, true>(is3d, form, epi, p, g, tc, omega, st);
                 case 5: return v3_launch_p<5, 2, 8, 1, true>(is3d, form, epi, p, g, tc, omega, st);
             }
-        }
-    }
-    if (variant == 6) {
-        switch (pmax) {
-            case 1: return v3_launch_p<1, 2, 8, 2>(is3d, form, epi, p, g, tc, omega, st);
-            case 2: return v3_launch_p<2, 2, 8, 2>(is3d, form, epi, p, g, tc, omega, st);
-            case 3: return v3_launch_p<3, 2, 8, 2>(is3d, form, epi, p, g, tc, omega, st);
-            case 4: return v3_launch_p<4, 2, 8, 2>(is3d, form, epi, p, g, tc, omega, st);
-            case 5: return v3_launch_p<5, 2, 8, 2>(is3d, form, epi, p, g, tc, omega, st);
-        }
-    }
-    if (variant == 5) {
-        switch (pmax) {
-            case 1: return v3_launch_p<1, 2, 16>(is3d, form, epi, p, g, tc, omega, st);
-            case 2: return v3_launch_p<2, 2, 16>(is3d, form, epi, p, g, tc, omega, st);
-            case 3: return v3_launch_p<3, 2, 16>(is3d, form, epi, p, g, tc, omega, st);
-            default: break;  // P >= 4: the 32-row tile exceeds the LDS budget
         }
     }
     switch (pmax) {

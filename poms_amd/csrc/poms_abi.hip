@@ -14,8 +14,6 @@ void set_error(const std::string& msg) { g_err = msg; }
 
 int kron_launch(int pmax, bool is3d, int form, int epi, const KronPtrs& p, const KronGeom& g,
                 double omega, hipStream_t st);
-int kron_v2_launch(int variant, int pmax, bool is3d, int form, int epi, const KronPtrs& p,
-                   const KronGeom& g, const ToepConst& tc, double omega, hipStream_t st);
 int kron_v3_launch(int variant, int pmax, bool is3d, int form, int epi, const KronPtrs& p,
                    const KronGeom& g, const ToepConst& tc, double omega, hipStream_t st);
 int kron_v4_launch(int pmax, bool is3d, int form, int epi, const KronPtrs& p, const KronGeom& g,
@@ -23,11 +21,6 @@ int kron_v4_launch(int pmax, bool is3d, int form, int epi, const KronPtrs& p, co
 int kron_v5_launch(int pmax, int epi, const KronPtrs& p, const KronGeom& g, const ToepConst& tc, int H,
                    double omega, hipStream_t st, int diag_mode);
 void kron_v5_tile(int pmax, bool aligned, int* H, int* TO);
-int kron_v6_launch(int pmax, int epi, const KronPtrs& p, const KronGeom& g, const ToepConst& tc, int H,
-                   double omega, hipStream_t st, int diag_mode);
-int kron_v6_rows(int pmax, int epi);
-int kron_v2_stamps(int variant, int epi, const KronPtrs& p, const KronGeom& g, const ToepConst& tc,
-                   double omega, unsigned long long* dbg, hipStream_t st);
 int kron_tile_rows();
 int kron_tile_cols();
 int vec_launch(int op, const RowGeom& g, double a, double b, const double* x, const double* y,
@@ -81,9 +74,9 @@ struct poms_op {
     int64_t last_partials = 0;
     double *dg2a = nullptr, *dg2b = nullptr;  // contiguous axis-2 band diagonals
     double* rdiag0 = nullptr;                  // 1/diag(A) per global plane (Toeplitz interior of axes 1, 2)
-    double* ab0 = nullptr;                     // (A0, M0) pairs of at/bt interleaved: ab0[(j*W + s)*2 + {0,1}]
     int variant = 0;
-    bool v2_ok = false;
+    bool v2_ok = false;       // storage pads == pmax on every used axis (the Toeplitz kernels' precondition)
+    bool ghost_corners = false;   // ghost edges / corners of axes 1 and 2 may be non-zero (a Cart block)
     ToepConst tc{};
     double* coef = nullptr;   // FORM_STENCIL: (2p+1)^d coefficient planes of the owned rows
     int sp[3]{};              // FORM_STENCIL: stencil half-widths per axis
@@ -255,6 +248,7 @@ int poms_op_create(poms_ctx* ctx, int ndim, const poms_layout* layout, int form,
     o->L = *layout;
     o->g0 = is3d ? g0 : 0;
     o->n0g = is3d ? n0_global : 1;
+    o->ghost_corners = (layout->flags & POMS_LAYOUT_GHOST_DATA) != 0;
     int rc = 0;
     if (is3d) {
         // Transposed (column) bands of the axis-0 factors, padded by pmax rows on
@@ -270,15 +264,6 @@ int poms_op_create(poms_ctx* ctx, int ndim, const poms_layout* layout, int form,
             }
         rc |= upload(ta.data(), ta.size(), &o->a0t);
         if (sum) rc |= upload(tb.data(), tb.size(), &o->b0t);
-        // v6: pair row j + 2P of global plane j (P more zero rows in front, so the
-        // kernel's coefficient window, which starts P planes back, never starts
-        // before the table)
-        std::vector<double> tab(2 * (nrow + pmax) * W, 0.0);
-        for (int64_t e = 0; e < nrow * W; ++e) {
-            tab[2 * (e + pmax * W)] = ta[e];
-            tab[2 * (e + pmax * W) + 1] = tb[e];
-        }
-        rc |= upload(tab.data(), tab.size(), &o->ab0);
     }
     rc |= upload(f[2], (size_t)layout->n[1] * W, &o->a1);
     rc |= upload(f[4], (size_t)layout->n[2] * W, &o->a2);
@@ -477,16 +462,18 @@ int poms_op_stencil_data(poms_op* o, double* data_host) {
 
 int poms_op_destroy(poms_op* o) {
     if (!o) return 0;
-    for (double* p : {o->a0t, o->b0t, o->a1, o->b1, o->a2, o->b2, o->dg2a, o->dg2b, o->rdiag0, o->ab0, o->coef})
+    for (double* p : {o->a0t, o->b0t, o->a1, o->b1, o->a2, o->b2, o->dg2a, o->dg2b, o->rdiag0, o->coef})
         if (p) (void)hipFree(p);
     delete o;
     return 0;
 }
 
 int poms_op_set_variant(poms_op* op, int variant) {
-    if (!op || variant < 0 || (variant > 11 && (variant < 90 || variant > 112))) { set_error("poms_op_set_variant: bad argument"); return 1; }
+    // 90/91, 92-100, 101-109: diagnostic / tuning builds of v3, v4, v5
+    const bool known = variant == 0 || variant == 4 || (variant >= 7 && variant <= 10) ||
+                       (variant >= 90 && variant <= 109);
+    if (!op || !known) { set_error("poms_op_set_variant: bad argument (0, 4, 7, 8, 9, 10; 90-109 diagnostic)"); return 1; }
     if (variant > 0 && !op->v2_ok) { set_error("poms_op_set_variant: variant needs pads == pmax"); return 1; }
-    if (variant == 5 && op->pmax > 3) variant = 4;  // 32-row tile does not fit LDS at p >= 4
     op->variant = variant;
     return 0;
 }
@@ -544,10 +531,15 @@ static int auto_chunk(int nz, int tiles, int p, double slots = 512.0) {
     return best_chunk;
 }
 
-// v5 (variant 10) runs 3D FORM_SUM operators, p <= 3, pads == pmax, arrays < 2 GiB
+// v5 (variant 10) runs 3D FORM_SUM operators, p <= 3, pads == pmax, arrays < 2 GiB.
+// At odd p its x-row DMA pairs straddle storage column 0, and the pair holding
+// column 0 of storage row 0 (the corner ghost of each plane) fails the buffer range
+// check: zero, as the ghost always is unless axes 1 and 2 both have a lower
+// neighbour -- then (ghost_corners) the operator runs v3.
 static bool v5_ok(const poms_op* o) {
     const int64_t bytes = (int64_t)(o->L.n[0] + 2 * o->L.pads[0]) * row_geom(&o->L).s0 * 8;
-    return o->ndim == 3 && o->form == FORM_SUM && o->v2_ok && o->pmax <= 3 && bytes < 0x7ffffff0LL;
+    return o->ndim == 3 && o->form == FORM_SUM && o->v2_ok && o->pmax <= 3 && bytes < 0x7ffffff0LL &&
+           !(o->ghost_corners && (o->pmax & 1));
 }
 
 // v5 tiles are line-aligned when the row pitch is a multiple of 16 doubles and
@@ -555,23 +547,6 @@ static bool v5_ok(const poms_op* o) {
 static bool v5_aligned(const poms_op* o, const double* x) {
     const int64_t pitch = row_geom(&o->L).s1;
     return pitch % 16 == 0 && (reinterpret_cast<uintptr_t>(x + o->L.pads[2]) & 127) == 0;
-}
-
-// v6 (variant 11): one 512-thread workgroup per CU; the critical path of nc
-// chunks per tile is ceil(nc tiles / 256) rounds of (chunk + 2p) planes
-static int auto_chunk_v6(int nz, int tiles, int p) {
-    if (nz <= 0) return 1;
-    tiles = std::max(tiles, 1);
-    double best = 1e300;
-    int best_chunk = nz;
-    for (int nc = 1; nc <= std::max(1, nz / 4); ++nc) {
-        const int ch = (nz + nc - 1) / nc;
-        const int ncu = (nz + ch - 1) / ch;
-        const double rounds = std::ceil((double)ncu * tiles / 256.0);
-        const double cost = rounds * (ch + 2 * p);
-        if (cost < best - 1e-9) { best = cost; best_chunk = ch; }
-    }
-    return best_chunk;
 }
 
 static int op_geom(poms_op* o, int64_t zb, int64_t ze, KronGeom& g, int v = -1, int v5_to = 0,
@@ -585,10 +560,9 @@ static int op_geom(poms_op* o, int64_t zb, int64_t ze, KronGeom& g, int v = -1, 
     g.pd0 = r.pd0; g.pd1 = r.pd1; g.pd2 = r.pd2;
     g.g0 = (int)o->g0;
     g.tiles2 = (int)((o->L.n[2] + kron_tile_cols() - 1) / kron_tile_cols());
-    const int trows = v == 11 ? kron_v6_rows(o->pmax, epi)
-                    : (v == 3 || v == 5 || v == 10) ? (v == 10 ? 16 : 32) : kron_tile_rows();
+    const int trows = v == 10 ? 16 : kron_tile_rows();
     g.tiles1 = (int)((o->L.n[1] + trows - 1) / trows);
-    g.tout = (v == 10 || v == 11) ? v5_to : (o->tout > 0 ? o->tout : 64 - 2 * o->pmax);
+    g.tout = v == 10 ? v5_to : (o->tout > 0 ? o->tout : 64 - 2 * o->pmax);
     if (v >= 4) g.tiles2 = (int)((o->L.n[2] + g.tout - 1) / g.tout);
     if (!is3d) {
         g.z_begin = 0; g.z_end = 1; g.chunk = 1; g.nchunks = 1; g.nch1 = 1; g.z2_begin = g.z2_end = 0;
@@ -614,8 +588,7 @@ static int op_geom(poms_op* o, int64_t zb, int64_t ze, KronGeom& g, int v = -1, 
     const int nz = (int)(ze - zb) + (int)(ze2 - zb2);
     int chunk = o->chunk;
     if (chunk <= 0)
-        chunk = v == 11 ? auto_chunk_v6(nz, g.tiles2 * g.tiles1, o->pmax)
-                        : auto_chunk(nz, g.tiles2 * g.tiles1, o->pmax, v == 10 ? 256.0 : 512.0);
+        chunk = auto_chunk(nz, g.tiles2 * g.tiles1, o->pmax, v == 10 ? 256.0 : 512.0);
     chunk = std::max(1, std::min(chunk, std::max(nz, 1)));
     g.chunk = chunk;
     g.nch1 = (int)((ze - zb + chunk - 1) / chunk);
@@ -625,7 +598,7 @@ static int op_geom(poms_op* o, int64_t zb, int64_t ze, KronGeom& g, int v = -1, 
 
 // variants whose Jacobi epilogue also accumulates x_out . b (v3 and v4 kernels)
 static bool fused_dot_ok(const poms_op* o) {
-    return o->form == FORM_STENCIL || (o->variant >= 4 && o->variant <= 11);
+    return o->form == FORM_STENCIL || (o->variant >= 4 && o->variant <= 10);
 }
 
 // General-stencil launch (FORM_STENCIL): the epilogues of op_run plus EPI_DIAG.
@@ -664,8 +637,6 @@ static int resolve_variant(const poms_op* o, int epi) {
         else
             v = ((epi == EPI_APPLY || epi == EPI_RESID) && o->pmax <= 3) ? 7 : 9;
     }
-    if (v == 11 && (!v5_ok(o) || epi == EPI_JACOBI0))   // v6: no two-sweeps-from-zero epilogue
-        v = (v5_ok(o) && (epi != EPI_JACOBI0 || o->pmax <= 2)) ? 10 : 9;
     // v5 two-sweeps-from-zero: p <= 2 (at p = 3 the build still spills)
     if (v == 10 && (!v5_ok(o) || (epi == EPI_JACOBI0 && o->pmax > 2))) v = 9;
     return v;
@@ -678,16 +649,15 @@ static int op_run(poms_op* o, int epi, double omega, const double* x, double* y,
     if (epi != EPI_APPLY && !b) { set_error("null right-hand side"); return 1; }
     if (o->form == FORM_STENCIL)
         return stencil_run(o, epi, omega, x, y, b, zb, ze, want_norm, stream, want_dot, zb2, ze2);
-    if (epi == EPI_APPLYDOT && !(o->variant == 4 || o->variant == 5 || o->variant == 6 || o->variant == 8 ||
-                                 o->variant == 9 || o->variant == 10 || o->variant == 11)) {
-        set_error("apply + x.y: kernel variants 4, 5, 6, 8, 9, 10, 11 only");
+    if (epi == EPI_APPLYDOT && !(o->variant == 4 || o->variant == 8 || o->variant == 9 || o->variant == 10)) {
+        set_error("apply + x.y: kernel variants 4, 8, 9, 10 only");
         return 1;
     }
     if (want_dot && ((epi != EPI_JACOBI && epi != EPI_JACOBI0 && epi != EPI_APPLYDOT) || !fused_dot_ok(o))) {
-        set_error("fused x_out.b needs a Jacobi sweep on kernel variants 4-9");
+        set_error("fused x_out.b needs a Jacobi sweep on kernel variants 4-10");
         return 1;
     }
-    if (epi == EPI_JACOBI0 && !(o->variant == 8 || o->variant == 9 || o->variant == 10 || o->variant == 11)) {
+    if (epi == EPI_JACOBI0 && !(o->variant == 8 || o->variant == 9 || o->variant == 10)) {
         set_error("two sweeps from zero: kernel variant 8, 9 or 10 only");
         return 1;
     }
@@ -701,30 +671,23 @@ static int op_run(poms_op* o, int epi, double omega, const double* x, double* y,
     int v = resolve_variant(o, epi);
     const int v5_diag = (v >= 101 && v <= 109) ? v - 100 : 0;   // v5 diagnostic / tuning builds
     if (v5_diag) v = 10;
-    const int v6_diag = (v == 111 || v == 112) ? v - 110 : 0;   // v6 diagnostic builds
-    if (v6_diag) v = 11;
     int v5_h = 0, v5_to = 0;
-    if (v == 10 || v == 11) kron_v5_tile(o->pmax, v5_aligned(o, x), &v5_h, &v5_to);
+    if (v == 10) kron_v5_tile(o->pmax, v5_aligned(o, x), &v5_h, &v5_to);
     KronGeom g;
     if (op_geom(o, zb, ze, g, v, v5_to, zb2, ze2, epi)) return 1;
     const int64_t nblk = (int64_t)g.tiles2 * g.tiles1 * g.nchunks;
     if (nblk == 0) { o->last_partials = 0; return 0; }
     if ((want_norm || want_dot) && 2 * nblk > kScratch) { set_error("too many blocks for the partial-sum scratch"); return 1; }
     KronPtrs p{x, y, b, o->a0t, o->b0t, o->a1, o->b1, o->a2, o->b2,
-               want_norm ? o->ctx->scratch : nullptr, want_dot ? o->ctx->scratch + nblk : nullptr, o->rdiag0,
-               o->ab0};
-    const int rc = v == 11
-        ? kron_v6_launch(o->pmax, epi, p, g, o->tc, v5_h, omega, as_stream(stream), v6_diag)
-        : v == 10
+               want_norm ? o->ctx->scratch : nullptr, want_dot ? o->ctx->scratch + nblk : nullptr, o->rdiag0};
+    const int rc = v == 10
         ? kron_v5_launch(o->pmax, epi, p, g, o->tc, v5_h, omega, as_stream(stream), v5_diag)
         : v == 0
         ? kron_launch(o->pmax, o->ndim == 3, o->form, epi, p, g, omega, as_stream(stream))
         : (v == 7 || (v >= 92 && v <= 100))
         ? kron_v4_launch(o->pmax, o->ndim == 3, o->form, epi, p, g, o->tc, omega, as_stream(stream),
                          v == 7 ? 0 : v - 91)
-        : v >= 4
-        ? kron_v3_launch(v, o->pmax, o->ndim == 3, o->form, epi, p, g, o->tc, omega, as_stream(stream))
-        : kron_v2_launch(v, o->pmax, o->ndim == 3, o->form, epi, p, g, o->tc, omega, as_stream(stream));
+        : kron_v3_launch(v, o->pmax, o->ndim == 3, o->form, epi, p, g, o->tc, omega, as_stream(stream));
     if (rc) return 1;
     POMS_HIP_CHECK(hipGetLastError());
     o->last_partials = (want_norm || want_dot) ? nblk : 0;
@@ -760,7 +723,7 @@ int poms_op_apply_dot(poms_op* op, const double* x, double* y, int64_t zb, int64
 int poms_op_apply_dot_supported(poms_op* op, int* yes) {
     if (!op || !yes) { set_error("poms_op_apply_dot_supported: null argument"); return 1; }
     const int v = op->variant;
-    *yes = (op->form == FORM_STENCIL || v == 4 || v == 5 || v == 6 || v == 8 || v == 9 || v == 10 || v == 11) ? 1 : 0;
+    *yes = (op->form == FORM_STENCIL || v == 4 || v == 8 || v == 9 || v == 10) ? 1 : 0;
     return 0;
 }
 
@@ -775,7 +738,7 @@ int poms_op_jacobi_from_zero(poms_op* op, double omega, const double* b, double*
 int poms_op_from_zero_supported(poms_op* op, int* yes) {
     if (!op || !yes) { set_error("poms_op_from_zero_supported: null argument"); return 1; }
     const int64_t bytes = (int64_t)(op->L.n[0] + 2 * op->L.pads[0]) * row_geom(&op->L).s0 * 8;
-    *yes = (op->ndim == 3 && op->form != FORM_STENCIL && (op->variant == 8 || op->variant == 9 || op->variant == 10 || op->variant == 11) &&
+    *yes = (op->ndim == 3 && op->form != FORM_STENCIL && (op->variant == 8 || op->variant == 9 || op->variant == 10) &&
             bytes < 0x7ffffff0LL) ? 1 : 0;
     return 0;
 }
@@ -801,21 +764,9 @@ int poms_op_diag_scale(poms_op* o, double scale, const double* b, double* x, int
     return 0;
 }
 
-int poms_op_profile_phases(poms_op* o, int jacobi, const double* b, const double* x, double* y,
-                           uint64_t* dbg, int64_t* nwaves, void* stream) {
-    if (!o || !x || !y || !dbg || !nwaves || (jacobi && !b)) { set_error("profile: null argument"); return 1; }
-    if (o->ndim != 3 || o->form != FORM_SUM || o->pmax != 3 || (o->variant != 1 && o->variant != 2)) {
-        set_error("profile: diagnostic build exists for 3D FORM_SUM p=3, variants 1/2");
-        return 1;
-    }
-    KronGeom g;
-    if (op_geom(o, 0, o->L.n[0], g)) return 1;
-    const int64_t nblk = (int64_t)g.tiles2 * g.tiles1 * g.nchunks;
-    *nwaves = nblk * (o->variant == 2 ? 8 : 4);
-    KronPtrs p{x, y, b, o->a0t, o->b0t, o->a1, o->b1, o->a2, o->b2, nullptr, nullptr};
-    kron_v2_stamps(o->variant, jacobi ? EPI_JACOBI : EPI_APPLY, p, g, o->tc, 2.0 / 3.0,
-                   reinterpret_cast<unsigned long long*>(dbg), as_stream(stream));
-    POMS_HIP_CHECK(hipGetLastError());
+int poms_op_set_ghost_corners(poms_op* op, int yes) {
+    if (!op) { set_error("poms_op_set_ghost_corners: null operator"); return 1; }
+    op->ghost_corners = yes != 0;
     return 0;
 }
 
@@ -943,10 +894,12 @@ static int vec_common(poms_ctx* ctx, const poms_layout* L, int op, double a, dou
     int nb = 0;
     const bool red = (op == V_DOT || op == V_PCGUPD || op == V_RUPD);
     // whole interior planes as one flat range (ghost rows / columns are zero in every
-    // vector and stay zero); the per-row kernel for fills and mixed alignments
+    // vector and stay zero -- unless the layout says they hold a neighbour's data);
+    // the per-row kernel for fills, mixed alignments and ghost data
     const int64_t off = (int64_t)g.pd0 * g.s0, count = (int64_t)g.n0 * g.s0;
     auto at = [&](const double* v) { return v ? v + off : nullptr; };
-    const bool flat = vec_flat_launch(op, count, a, b, at(x), at(y), const_cast<double*>(at(z)),
+    const bool flat = !(L->flags & POMS_LAYOUT_GHOST_DATA) &&
+                      vec_flat_launch(op, count, a, b, at(x), at(y), const_cast<double*>(at(z)),
                                       const_cast<double*>(at(w)), at(q), red ? ctx->scratch : nullptr,
                                       as_stream(stream), &nb, ab_dev) == 0;
     if (!flat && vec_launch(op, g, a, b, x, y, z, w, q, red ? ctx->scratch : nullptr, as_stream(stream), &nb,

@@ -18,6 +18,7 @@ from __future__ import annotations
 import os
 from dataclasses import dataclass
 
+import numpy as np
 import torch
 
 
@@ -156,6 +157,159 @@ class SlabDistribution:
             return r
         import torch.distributed as dist
         return dist.get_global_rank(self.group, r)
+
+
+def dims_create(world: int, ndim: int) -> tuple[int, ...]:
+    """Balanced process grid of ``world`` ranks over ``ndim`` axes, non-increasing
+    (``MPI_Dims_create``'s rule, which spl's ``Cart`` uses when the caller gives
+    no grid): prime factors, largest first, each to the currently smallest axis."""
+    if world < 1 or ndim < 1:
+        raise ValueError("bad world/ndim")
+    f, n, q = [], world, 2
+    while q * q <= n:
+        while n % q == 0:
+            f.append(q)
+            n //= q
+        q += 1
+    if n > 1:
+        f.append(n)
+    dims = [1] * ndim
+    for q in sorted(f, reverse=True):
+        dims[dims.index(min(dims))] *= q
+    return tuple(sorted(dims, reverse=True))
+
+
+class CartDistribution:
+    """Block decomposition of every axis over a process grid (spl ``Cart``).
+
+    The reference builds ``Cart(npts, pads, periods, reorder, comm)``
+    (`sources/tests/test_kron_dot.py:51-55, 89-93`; `slides/content.tex:200-223`):
+    a Cartesian communicator whose rank owns the block ``[starts[d], ends[d]]`` of
+    each axis and exchanges ``pads[d]``-wide ghost layers with its two neighbours
+    along every decomposed axis.  Here: ranks in C order over ``dims`` (rank =
+    ((c0 d1) + c1) d2 + c2, MPI_Cart_create without reordering), each axis split
+    as :func:`slab_bounds`, and :meth:`exchange` fills the ghost layers axis by
+    axis -- axis d's faces span the full padded extents of the other axes, so the
+    edge and corner ghosts arrive through the later axes (the same scheme as
+    spl's per-direction subarray exchange, `pyccel/kron_product.py:21-41`).
+
+    The slab decomposition (:class:`SlabDistribution`) is the ``dims = (w, 1, 1)``
+    case with the native RCCL schedule; this general grid moves its faces with
+    ``torch.distributed`` (RCCL device-to-device with ``nccl``, host-staged with
+    gloo) and one blocking exchange per operator call.
+    """
+
+    native = None   # no native communicator: faces move through torch.distributed
+
+    def __init__(self, npts, dims, rank: int, group=None, cuda_transport: bool = True,
+                 device_reductions: bool | None = None):
+        self.npts = tuple(int(n) for n in npts)
+        self.dims = tuple(int(d) for d in dims)
+        self.ndim = len(self.npts)
+        if len(self.dims) != self.ndim or any(d < 1 for d in self.dims):
+            raise ValueError("dims must give one positive grid extent per axis")
+        self.world = int(np.prod(self.dims))
+        if not 0 <= rank < self.world:
+            raise ValueError(f"rank {rank} outside a grid of {self.world}")
+        self.rank, self.group = int(rank), group
+        self.cuda_transport = cuda_transport
+        self.device_reductions = cuda_transport if device_reductions is None else device_reductions
+        self.coords = self.coords_of(self.rank)
+        b = [slab_bounds(n, d, c) for n, d, c in zip(self.npts, self.dims, self.coords)]
+        self.starts = tuple(s for s, _ in b)
+        self.ends = tuple(e for _, e in b)   # exclusive
+        for d, (s, e) in enumerate(b):
+            if e <= s:
+                raise ValueError(f"axis {d}: rank {rank} owns no points ({self.npts[d]} over {self.dims[d]})")
+        self.prev = tuple(self.rank_of(self._shift(d, -1)) if self.coords[d] > 0 else None
+                          for d in range(self.ndim))
+        self.next = tuple(self.rank_of(self._shift(d, 1)) if self.coords[d] + 1 < self.dims[d] else None
+                          for d in range(self.ndim))
+
+    def coords_of(self, rank: int) -> tuple[int, ...]:
+        out = []
+        for d in reversed(self.dims):
+            out.append(rank % d)
+            rank //= d
+        return tuple(reversed(out))
+
+    def rank_of(self, coords) -> int:
+        r = 0
+        for c, d in zip(coords, self.dims):
+            r = r * d + c
+        return r
+
+    def _shift(self, axis: int, step: int):
+        c = list(self.coords)
+        c[axis] += step
+        return c
+
+    @property
+    def n_local(self) -> tuple[int, ...]:
+        return tuple(e - s for s, e in zip(self.starts, self.ends))
+
+    @property
+    def transport(self) -> str:
+        return "none" if self.world == 1 else "torch"
+
+    @classmethod
+    def from_process_group(cls, npts, dims=None, group=None,
+                           device_reductions: bool | None = None) -> "CartDistribution":
+        """Block of this rank; ``dims`` defaults to :func:`dims_create`."""
+        import torch.distributed as dist
+        world = dist.get_world_size(group)
+        dims = dims_create(world, len(npts)) if dims is None else tuple(dims)
+        if int(np.prod(dims)) != world:
+            raise ValueError(f"process grid {dims} does not hold {world} ranks")
+        return cls(npts, dims, dist.get_rank(group), group, cuda_transport=(dist.get_backend(group) == "nccl"),
+                   device_reductions=device_reductions)
+
+    def _peer(self, r: int) -> int:
+        if self.group is None:
+            return r
+        import torch.distributed as dist
+        return dist.get_global_rank(self.group, r)
+
+    def exchange(self, data: torch.Tensor, pads, widths=None) -> None:
+        """Fill the ghost layers of the padded local block ``data`` (shape
+        ``n_local[d] + 2 pads[d]`` per axis; strided views allowed) from the
+        neighbours, ``widths[d]`` (default ``pads[d]``) layers per decomposed axis.
+        Ghosts past the global boundary are left untouched (zero)."""
+        import torch.distributed as dist
+        nd = self.ndim
+        widths = tuple(pads) if widths is None else tuple(widths)
+        staged = not self.cuda_transport and data.device.type != "cpu"
+        for ax in range(nd):
+            if self.dims[ax] == 1 or widths[ax] == 0:
+                continue
+            w, p, n = widths[ax], pads[ax], self.n_local[ax]
+            if w > p:
+                raise ValueError("ghost width exceeds storage pad")
+            if n < w:
+                raise ValueError(f"axis {ax}: block of {n} points is thinner than the ghost width {w}")
+
+            def face(lo, hi):
+                idx = [slice(None)] * nd
+                idx[ax] = slice(lo, hi)
+                return data[tuple(idx)]
+
+            ops, recvs = [], []
+            for nbr, send, ghost in ((self.prev[ax], face(p, p + w), face(p - w, p)),
+                                     (self.next[ax], face(p + n - w, p + n), face(p + n, p + n + w))):
+                if nbr is None:
+                    continue
+                sbuf = send.contiguous()
+                if staged:
+                    sbuf = sbuf.cpu()
+                rbuf = torch.empty(ghost.shape, dtype=data.dtype, device="cpu" if staged else data.device)
+                ops.append(dist.P2POp(dist.isend, sbuf, self._peer(nbr), self.group))
+                ops.append(dist.P2POp(dist.irecv, rbuf, self._peer(nbr), self.group))
+                recvs.append((ghost, rbuf))
+            if ops:
+                for wk in dist.batch_isend_irecv(ops):
+                    wk.wait()
+            for ghost, rbuf in recvs:
+                ghost.copy_(rbuf)
 
 
 class NativeComm:

@@ -121,6 +121,9 @@ class KronSolver:
         if Y.space is not V and (Y.space.npts != V.npts or Y.space.pads != V.pads
                                  or Y.space.layout.pitch != V.layout.pitch):
             raise ValueError("vector is not in the solver's space")
+        if V.is_distributed and V.is_cart:
+            raise NotImplementedError("the distributed Kronecker solve transposes axis-0 slabs; "
+                                      "use a SlabDistribution")
         X = V.empty() if out is None else out
         st = rt.stream_handle()
         if not V.is_distributed:

@@ -38,7 +38,7 @@ def knots_to_insert(Tf, nf, pf, Tc, nc, pc):
 
 class KronTransfer:
     """Restriction / prolongation between a fine :class:`StencilVectorSpace`
-    (possibly a slab) and a dense, replicated coarse vector of ``prod(nc)`` doubles."""
+    (possibly a slab or a Cart block) and a dense, replicated coarse vector of ``prod(nc)`` doubles."""
 
     def __init__(self, V: StencilVectorSpace, P: Sequence[np.ndarray]):
         nd = V.ndim
@@ -51,10 +51,18 @@ class KronTransfer:
                 raise ValueError(f"axis {d}: P has {p.shape[0]} rows, space has {V.npts[d]} points")
         self.nc = tuple(p.shape[1] for p in self.P)
         lead = 3 - nd
-        nf3 = (1,) * lead + tuple(V.npts)
+        # rows of this rank: axis 0 of a 3D space whole (global offset g0), the other
+        # axes of a Cart block sliced to the owned rows
+        Pl = list(self.P)
+        nfl = list(V.npts)
+        if V.is_cart:
+            for d in range(1 if nd == 3 else 0, nd):
+                Pl[d] = np.ascontiguousarray(self.P[d][V.starts[d]:V.ends[d] + 1])
+                nfl[d] = Pl[d].shape[0]
+        nf3 = (1,) * lead + tuple(nfl)
         nc3 = (1,) * lead + self.nc
         ones = np.ones((1, 1))
-        P3 = [ones] * lead + self.P
+        P3 = [ones] * lead + Pl
         self._keep = P3
         nf_arr = (C.c_int64 * 3)(*nf3)
         nc_arr = (C.c_int64 * 3)(*nc3)

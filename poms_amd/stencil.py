@@ -27,7 +27,7 @@ import torch
 
 from . import _lib
 from . import runtime as rt
-from .dist import SlabDistribution
+from .dist import CartDistribution, SlabDistribution
 
 F64 = torch.float64
 
@@ -38,11 +38,12 @@ class StencilVectorSpace:
     ``npts``: global number of coefficients per axis; ``pads``: ghost width per
     axis (the spline degree).  Non-periodic only -- every driver of the
     reference is non-periodic (`sources/mg_jac.py`).  With
-    ``dist`` the slowest axis is split into slabs (3D only).
+    ``dist`` a :class:`SlabDistribution` splits the slowest axis into slabs (3D
+    only); a :class:`CartDistribution` splits every axis into blocks (spl ``Cart``).
     """
 
     def __init__(self, npts: Sequence[int], pads: Sequence[int], periods=None, *,
-                 dist: SlabDistribution | None = None, device=None, align: bool = False):
+                 dist: SlabDistribution | CartDistribution | None = None, device=None, align: bool = False):
         npts, pads = tuple(int(v) for v in npts), tuple(int(v) for v in pads)
         if not 1 <= len(npts) <= 3 or len(pads) != len(npts):
             raise ValueError("npts/pads must have 1..3 equal-length entries")
@@ -50,7 +51,14 @@ class StencilVectorSpace:
             raise NotImplementedError("periodic spaces are not supported (reference drivers are non-periodic)")
         if any(n < 1 for n in npts) or any(p < 0 for p in pads):
             raise ValueError("bad npts/pads")
-        if dist is not None:
+        self.is_cart = isinstance(dist, CartDistribution)
+        if self.is_cart:
+            if dist.npts != npts:
+                raise ValueError(f"distribution npts {dist.npts} do not match {npts}")
+            for d, (nl, p, g) in enumerate(zip(dist.n_local, pads, dist.dims)):
+                if g > 1 and nl < p:
+                    raise ValueError(f"axis {d}: block of {nl} points is thinner than the pad {p}")
+        elif dist is not None:
             if len(npts) != 3:
                 raise NotImplementedError("slab distribution is implemented for 3D spaces")
             if dist.n0_global != npts[0]:
@@ -58,9 +66,13 @@ class StencilVectorSpace:
         self.npts, self.pads, self.ndim = npts, pads, len(npts)
         self.periods = (False,) * self.ndim
         self.dist = dist
-        s0, e0 = (dist.start, dist.end - 1) if dist is not None else (0, npts[0] - 1)
-        self.starts = (s0,) + (0,) * (self.ndim - 1)
-        self.ends = (e0,) + tuple(n - 1 for n in npts[1:])
+        if self.is_cart:
+            self.starts = tuple(dist.starts)
+            self.ends = tuple(e - 1 for e in dist.ends)
+        else:
+            s0, e0 = (dist.start, dist.end - 1) if dist is not None else (0, npts[0] - 1)
+            self.starts = (s0,) + (0,) * (self.ndim - 1)
+            self.ends = (e0,) + tuple(n - 1 for n in npts[1:])
         self.local_npts = tuple(e - s + 1 for s, e in zip(self.starts, self.ends))
         lead = 3 - self.ndim
         self.n3 = (1,) * lead + self.local_npts
@@ -83,7 +95,10 @@ class StencilVectorSpace:
         self.strides = tuple(int(np.prod(lead_shape[i + 1:])) * self.pitch for i in range(len(lead_shape))) + (1,)
         self.plane_elems = self.strides[0] if self.ndim == 3 else int(np.prod(lead_shape)) * self.pitch
         self.store_elems = self.padded_shape[0] * self.strides[0] + self.shift + (16 if self.aligned else 0)
-        self.layout = _lib.Layout.make(self.n3, self.p3, self.pitch if self.aligned else 0)
+        # a Cart block's ghost rows / columns (axes 1, 2) hold the neighbours' data
+        ghost_data = self.is_cart and any(g > 1 for g in dist.dims[-2:])
+        self.layout = _lib.Layout.make(self.n3, self.p3, self.pitch if self.aligned else 0,
+                                       _lib.LAYOUT_GHOST_DATA if ghost_data else 0)
         self.dimension = int(np.prod(npts))
         self.device = rt.device_index(device)
         self.ctx = rt.ctx(self.device)
@@ -379,6 +394,13 @@ class StencilVector:
 
     def update_ghost_regions(self, direction=None) -> None:
         V = self._space
+        if V.is_distributed and V.is_cart:
+            if direction is None:
+                V.dist.exchange(self._data, V.pads)
+                self._ghost_valid = True
+            else:   # one axis only (spl's per-direction update)
+                V.dist.exchange(self._data, V.pads, [V.pads[d] if d == direction else 0 for d in range(V.ndim)])
+            return
         if V.is_distributed and (direction is None or direction == 0):
             V.dist.exchange(V.planes(self._store), width=V.pads[0], pad=V.pads[0])
             self._ghost_valid = True
@@ -527,16 +549,29 @@ class KronOperator:
             keep.append(a)
             return a.ctypes.data_as(C.c_void_p)
 
+        # factor rows of this rank: axis 0 of a 3D space is passed whole (the device
+        # tables are indexed by global plane, g0); with a Cart block the rows of the
+        # other axes are sliced to the owned block (its neighbours' rows act through
+        # the exchanged ghosts)
+        role_axis = {"A1": nd - 2, "B1": nd - 2, "F1": nd - 2, "M2": nd - 1, "K2": nd - 1, "F2": nd - 1}
+
+        def rows(name):
+            b = bands[name]
+            ax = role_axis.get(name, -1)
+            if not V.is_cart or ax < 0 or b.shape[0] == 1:
+                return b
+            return b[V.starts[ax]:V.ends[ax] + 1]
+
         f = [None] * 6
         if form == "sum":
             if nd == 3:
                 f[0], f[1] = arr(bands["A0"]), arr(bands["M0"])
-            f[2], f[3], f[4], f[5] = arr(bands["A1"]), arr(bands["B1"]), arr(bands["M2"]), arr(bands["K2"])
+            f[2], f[3], f[4], f[5] = arr(rows("A1")), arr(rows("B1")), arr(rows("M2")), arr(rows("K2"))
             cform = _lib.FORM_SUM
         else:
             if nd == 3:
                 f[0] = arr(bands["F0"])
-            f[2], f[4] = arr(bands["F1"]), arr(bands["F2"])
+            f[2], f[4] = arr(rows("F1")), arr(rows("F2"))
             cform = _lib.FORM_SINGLE
         farr = (C.c_void_p * 6)(*f)
         g0 = V.starts[0] if nd == 3 else 0
@@ -616,7 +651,7 @@ class KronOperator:
         _lib.call("poms_op_set_tile_cols", self._h, int(cols))
 
     def set_variant(self, variant: int) -> None:
-        """0 = general kernel, 1/2 = Toeplitz-interior kernels (see poms_hip.h)."""
+        """0 general, 4/9 v3, 7 v4, 10 v5, 8 auto (see poms_hip.h)."""
         _lib.call("poms_op_set_variant", self._h, int(variant))
 
     @property
@@ -652,6 +687,10 @@ class KronOperator:
         if V.is_distributed and V.dist.native is not None:
             self._run_native(kind, x, y, b, omega, norm_out, dot_out)
             return
+        if V.is_distributed and V.is_cart and not x._ghost_valid:
+            # block decomposition: every decomposed axis' ghosts, then one launch
+            V.dist.exchange(x._data, V.pads)
+            x._ghost_valid = True
         n0 = V.local_npts[0] if V.ndim == 3 else 1
         st = _stream()
         ranges = ((0, n0, 0, 0),)
@@ -813,6 +852,11 @@ class KronOperator:
 
     @property
     def from_zero_supported(self) -> bool:
+        V = self.space
+        if V.is_distributed and V.is_cart:
+            # x1 = omega b / diag on the ghost rows of axes 1, 2 would need the
+            # neighbours' diagonal: damped_jacobi forms x1 with diag_scale instead
+            return False
         v = C.c_int()
         _lib.call("poms_op_from_zero_supported", self._h, C.byref(v))
         return bool(v.value)
@@ -828,6 +872,8 @@ class KronOperator:
         if x_out is b:
             raise ValueError("x_out must not alias b")
         V = self.space
+        if not self.from_zero_supported:
+            raise NotImplementedError("jacobi_from_zero is not supported by this operator / decomposition")
         nb = V.scalar_buffer()
         if lazy and want_norm and V.is_distributed and V.dist.native is not None:
             from .dist import LazyNative

@@ -6,6 +6,9 @@ slab-local Kronecker apply using the exchanged ghosts that must equal the
 global oracle apply restricted to the slab (the decomposition is exact), plus
 the restriction partial-sum + allreduce.
 
+mode "cart_cpu" / "cart_gpu": the same over a Cart block decomposition of every
+axis (POMS_TEST_CART_DIMS, e.g. "2x2x1"), 4 ranks.
+
 mode "gpu": gloo (host-staged exchange) with every rank on cuda:0 -- the
 distributed KronOperator / vector algebra / transfer / two-level V-cycle of
 poms_amd against the global single-process oracle.
@@ -203,11 +206,232 @@ def run_gpu_ksolve():
     check(rel(y.to_local_numpy(), xg[d.start:d.end]) <= 1e-12, "distributed kron solve in place")
 
 
+def _cart_dims():
+    return tuple(int(v) for v in os.environ["POMS_TEST_CART_DIMS"].split("x"))
+
+
+def block_apply_local(ext, Ms, Ks, starts, ends, p, c=1.0):
+    """c M⊗M(⊗M) + the stiffness terms applied to the owned block of a Cart rank.
+
+    ``ext`` holds x on the window ``[starts[d] - p, ends[d] + p)`` of every axis
+    (ghosts from the neighbours, zeros past the global boundary); factor rows are
+    the owned rows, columns that window."""
+    nd = len(starts)
+
+    def loc(F, d):
+        n = F.shape[0]
+        Fd = band_to_dense(F)
+        cols = np.arange(starts[d] - p, ends[d] + p)
+        valid = (cols >= 0) & (cols < n)
+        G = np.zeros((ends[d] - starts[d], len(cols)))
+        G[:, valid] = Fd[starts[d]:ends[d]][:, cols[valid]]
+        return G
+
+    def ap(F, X, axis):
+        return np.moveaxis(np.tensordot(F, X, axes=([1], [axis])), 0, axis)
+
+    Ml = [loc(M, d) for d, M in enumerate(Ms)]
+    Kl = [loc(K, d) for d, K in enumerate(Ks)]
+    y = ext
+    for d in range(nd):
+        y = ap(Ml[d], y, d)
+    y = c * y
+    for k in range(nd):
+        t = ext
+        for d in range(nd):
+            t = ap(Kl[d] if d == k else Ml[d], t, d)
+        y = y + t
+    return y
+
+
+def run_cart_cpu():
+    """Cart block decomposition on CPU tensors: the ghost layers of every decomposed
+    axis (edges and corners included) equal the neighbours' owned entries, and a
+    block-local apply on them equals the global oracle's rows."""
+    from poms_amd.dist import CartDistribution
+    rank, world = dist.get_rank(), dist.get_world_size()
+    dims = _cart_dims()
+    nd = len(dims)
+    p, N = 3, 9
+    n = N + p
+    M, K = assemble_1d(uniform_knots(p, N), p)
+    rng = np.random.default_rng(5)
+    xg = rng.standard_normal((n,) * nd)
+    d = CartDistribution.from_process_group((n,) * nd, dims)
+    check(d.dims == dims and d.world == world and d.rank_of(d.coords) == rank, "grid")
+    for ax in range(nd):
+        b = [slab_bounds(n, dims[ax], c) for c in range(dims[ax])]
+        check((d.starts[ax], d.ends[ax]) == b[d.coords[ax]], f"axis {ax} bounds")
+    # every owned point exactly once over the ranks
+    own = torch.zeros((n,) * nd, dtype=torch.float64)
+    own[tuple(slice(s, e) for s, e in zip(d.starts, d.ends))] = 1.0
+    dist.all_reduce(own)
+    check(bool((own == 1.0).all()), "blocks tile the grid")
+    shape = tuple(nl + 2 * p for nl in d.n_local)
+    loc = torch.full(shape, float("nan"), dtype=torch.float64)
+    inner = tuple(slice(p, p + nl) for nl in d.n_local)
+    loc[inner] = torch.from_numpy(xg[tuple(slice(s, e) for s, e in zip(d.starts, d.ends))])
+    # ghosts past the global boundary are zero; the rest come from the exchange
+    for ax in range(nd):
+        for side, nbr in ((0, d.prev[ax]), (1, d.next[ax])):
+            if nbr is None:
+                idx = [slice(None)] * nd
+                idx[ax] = slice(0, p) if side == 0 else slice(p + d.n_local[ax], None)
+                loc[tuple(idx)] = 0.0
+    d.exchange(loc, (p,) * nd)
+    arr = loc.numpy()
+    check(not np.isnan(arr).any(), "every ghost (edges, corners) received")
+    want = np.zeros(shape)
+    src = tuple(slice(max(s - p, 0), min(e + p, n)) for s, e in zip(d.starts, d.ends))
+    dst = tuple(slice(max(s - p, 0) - (s - p), min(e + p, n) - (s - p)) for s, e in zip(d.starts, d.ends))
+    want[dst] = xg[src]
+    check(np.array_equal(arr, want), "ghost layers equal the neighbours' owned entries")
+    y = block_apply_local(arr, [M] * nd, [K] * nd, d.starts, d.ends, p)
+    Ag = orc.kron_sum_apply(xg, [M] * nd, [K] * nd) if nd == 3 else None
+    if Ag is None:
+        Md, Kd = band_to_dense(M), band_to_dense(K)
+        Ag = Md @ xg @ Md.T + Kd @ xg @ Md.T + Md @ xg @ Kd.T
+    own_sl = tuple(slice(s, e) for s, e in zip(d.starts, d.ends))
+    check(rel(y, Ag[own_sl]) <= 1e-14, f"block apply {rel(y, Ag[own_sl])}")
+
+
+def _cart_ops(d, nd, p, N, align):
+    """Operator, sweep, reductions and transfer on one Cart space vs the oracle."""
+    from poms_amd.multilevels import KronTransfer
+    from poms_amd.stencil import KronOperator, StencilVectorSpace
+    n = N + p
+    tag = f"p={p} align={align}"
+    M, K = assemble_1d(uniform_knots(p, N), p)
+    rng = np.random.default_rng(3)
+    xg, bg = rng.standard_normal((n,) * nd), rng.standard_normal((n,) * nd)
+    V = StencilVectorSpace([n] * nd, [p] * nd, dist=d, align=align)
+    check(V.is_cart and V.starts == d.starts, "space block")
+    A = KronOperator.laplace(V, [M] * nd, [K] * nd)
+    check(not A.from_zero_supported, "no from-zero sweeps on a Cart block")
+    x, b = V.zeros().from_numpy(xg), V.zeros().from_numpy(bg)
+    sl = tuple(slice(s, e) for s, e in zip(d.starts, d.ends))
+    Md, Kd = band_to_dense(M), band_to_dense(K)
+    if nd == 3:
+        Ag = orc.kron_sum_apply(xg, [M] * 3, [K] * 3)
+        D = orc.kron_sum_diag([M] * 3, [K] * 3).reshape((n,) * 3)
+    else:
+        Ag = Md @ xg @ Md.T + Kd @ xg @ Md.T + Md @ xg @ Kd.T
+        dm, dk = np.diag(Md), np.diag(Kd)
+        D = np.outer(dm, dm) + np.outer(dk, dm) + np.outer(dm, dk)
+    y = A.dot(x).to_local_numpy()
+    # the exchanged padded block equals the global window (zeros past the boundary)
+    win = np.zeros(tuple(nl + 2 * p for nl in d.n_local))
+    src = tuple(slice(max(s - p, 0), min(e + p, n)) for s, e in zip(d.starts, d.ends))
+    dst = tuple(slice(max(s - p, 0) - (s - p), min(e + p, n) - (s - p)) for s, e in zip(d.starts, d.ends))
+    win[dst] = xg[src]
+    check(np.array_equal(x._data.cpu().numpy(), win), f"{tag}: device ghost layers")
+    check(rel(y, Ag[sl]) <= 1e-14, f"{tag}: Cart apply {rel(y, Ag[sl])}")
+    # every kernel variant reads the exchanged ghosts of the decomposed axes
+    v0 = A.variant
+    errs = {}
+    for v in (0, 4, 7, 9, 10):
+        A.set_variant(v)
+        yv = A.dot(V.zeros().from_numpy(xg)).to_local_numpy()
+        errs[(v, A.kernel_variant("apply"))] = rel(yv, Ag[sl])
+        bad = np.argwhere(np.abs(yv - Ag[sl]) > 1e-12 * np.abs(Ag).max())
+        if len(bad):
+            print(f"rank {dist.get_rank()} {tag} variant {v}: {len(bad)} bad points, first {bad[:6].tolist()}",
+                  flush=True)
+    A.set_variant(v0)
+    check(all(e <= 1e-14 for e in errs.values()), f"{tag}: Cart apply by variant {errs}")
+    r = A.residual(b, x)
+    check(rel(r.to_local_numpy(), (bg - Ag)[sl]) <= 1e-14, f"{tag}: Cart residual")
+    xo = V.zeros()
+    nrm = A.jacobi_sweep(b, x, xo, 2.0 / 3.0, want_norm=True)
+    dr = 2.0 / 3.0 * (bg - Ag) / D
+    check(rel(xo.to_local_numpy(), (xg + dr)[sl]) <= 1e-14, f"{tag}: Cart jacobi sweep")
+    check(abs(nrm - float(np.vdot(dr, dr))) <= 1e-12 * float(np.vdot(dr, dr)), f"{tag}: global sweep norm")
+    z = V.zeros()
+    nz = A.diag_scale(b, z, 2.0 / 3.0, want_norm=True)
+    zr = 2.0 / 3.0 * bg / D
+    check(rel(z.to_local_numpy(), zr[sl]) <= 1e-15, f"{tag}: Cart diag_scale {rel(z.to_local_numpy(), zr[sl])}")
+    check(abs(nz - float(np.vdot(zr, zr))) <= 1e-12 * float(np.vdot(zr, zr)), f"{tag}: diag_scale norm")
+    nrm2, dot2 = A.jacobi_sweep(b, x, xo, 2.0 / 3.0, want_norm=True, want_dot=True)
+    want = float(np.vdot(xg + dr, bg))
+    check(abs(dot2 - want) <= 1e-12 * abs(want), f"{tag}: sweep + fused dot")
+    pq = A.dot_inner(x, xo)
+    want = float(np.vdot(xg, Ag))
+    check(abs(pq - want) <= 1e-12 * abs(want), f"{tag}: Cart apply + fused dot")
+    g = x.dot(b)
+    check(abs(g - float(np.vdot(xg, bg))) <= 1e-12 * abs(float(np.vdot(xg, bg))) + 1e-12, f"{tag}: global dot")
+    # spl-style single-axis ghost updates, then an apply on the already-valid ghosts
+    x2 = V.zeros().from_numpy(xg)
+    for ax in range(nd):
+        x2.update_ghost_regions(direction=ax)
+    x2._ghost_valid = True
+    check(rel(A.dot(x2).to_local_numpy(), Ag[sl]) <= 1e-14, f"{tag}: apply after per-axis updates")
+    # transfer: block restriction + allreduce, prolongation on the owned block
+    from poms_amd.mg import two_level_setup_1d
+    Tc, Tf = uniform_knots(p, N // 2), uniform_knots(p, N)
+    _, _, P1 = two_level_setup_1d(p, Tf, Tc)
+    tr = KronTransfer(V, [P1] * nd)
+    rc = tr.restrict(x).cpu().numpy()
+    if nd == 3:
+        full = np.einsum("ia,jb,kc,ijk->abc", P1, P1, P1, xg).reshape(-1)
+    else:
+        full = (P1.T @ xg @ P1).reshape(-1)
+    check(rel(rc, full) <= 1e-14, f"{tag}: Cart restriction")
+    nc = P1.shape[1]
+    xc = rng.standard_normal(nc ** nd)
+    z = V.zeros()
+    tr.prolong_add(torch.from_numpy(xc).cuda(), z)
+    if nd == 3:
+        pz = np.einsum("ia,jb,kc,abc->ijk", P1, P1, P1, xc.reshape((nc,) * 3))
+    else:
+        pz = P1 @ xc.reshape(nc, nc) @ P1.T
+    check(rel(z.to_local_numpy(), pz[sl]) <= 1e-14, f"{tag}: Cart prolongation")
+
+
+def run_cart_gpu():
+    """The device operator, vector algebra, transfer and two-level V-cycle over a
+    Cart block decomposition (gloo, every rank on cuda:0) against the global oracle."""
+    from poms_amd.dist import CartDistribution
+    from poms_amd.mg import TwoLevelVCycle
+    torch.cuda.set_device(0)
+    dims = _cart_dims()
+    nd = len(dims)
+    for p, N, align in ((3, 14, False), (3, 14, True), (2, 16, True), (1, 10, False)):
+        d = CartDistribution.from_process_group((N + p,) * nd, dims, device_reductions=True)
+        check(d.transport == "torch", "transport")
+        _cart_ops(d, nd, p, N, align)
+    # two-level V-cycle (p=2) over the blocks vs the global oracle
+    nf = 18
+    errs = []
+    for devred in (False, True):
+        mg = TwoLevelVCycle(2, 16, 4, ndim=nd, dist=CartDistribution.from_process_group(
+            (nf,) * nd, dims, device_reductions=devred))
+        bf = mg.rhs_ones()
+        xf2, ipre, ipos = mg.cycle(bf)
+        got = torch.from_numpy(xf2.toarray())
+        dist.all_reduce(got)
+        ones = np.ones((mg.n,) * nd)
+        xr, ipre_r, ipos_r = orc.vcycle_two_level([mg.M1d] * nd, [mg.K1d] * nd, mg.P1, ones)
+        xr2, _, _ = orc.vcycle_two_level([mg.M1d] * nd, [mg.K1d] * nd, mg.P1, ones, reorder=True)
+        tol = max(1e-9, 20 * rel(xr2, xr))
+        err = rel(got.numpy().reshape(xr.shape), xr)
+        errs.append((devred, err, tol, ipre["niter"], ipre_r["niter"], ipos["niter"], ipos_r["niter"]))
+    # the same V-cycle on one rank (no decomposition) through the same code
+    from poms_amd.stencil import StencilVectorSpace
+    mg1 = TwoLevelVCycle(2, 16, 4, ndim=nd)
+    x1, _, _ = mg1.cycle(mg1.rhs_ones())
+    errs.append(("single", rel(x1.toarray().reshape(xr.shape), xr)))
+    for e in errs[:2]:
+        devred, err, tol = e[:3]
+        check(err <= tol, f"Cart V-cycle (device reductions {devred}) {err} > {tol}; all {errs}")
+        check(e[3] == e[4] and e[5] == e[6], f"iteration counts {errs}")
+
+
 def main():
     mode = sys.argv[1]
     dist.init_process_group("gloo")
     try:
-        {"cpu": run_cpu, "gpu": run_gpu, "gpu_ksolve": run_gpu_ksolve}[mode]()
+        {"cpu": run_cpu, "gpu": run_gpu, "gpu_ksolve": run_gpu_ksolve, "cart_cpu": run_cart_cpu,
+         "cart_gpu": run_cart_gpu}[mode]()
         dist.barrier()
         print(f"rank {dist.get_rank()} ok", flush=True)
     finally:

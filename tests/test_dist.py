@@ -5,9 +5,10 @@ import subprocess
 import sys
 from pathlib import Path
 
+import numpy as np
 import pytest
 
-from poms_amd.dist import slab_bounds
+from poms_amd.dist import CartDistribution, dims_create, slab_bounds
 
 WORKER = Path(__file__).with_name("dist_worker.py")
 
@@ -35,8 +36,14 @@ def _launch(mode, world=2, timeout=300, extra_env=None):
         for p in procs:
             if p.poll() is None:
                 p.kill()
+    failed = [(r, rc, out) for r, (rc, out) in enumerate(outs) if rc != 0]
+    if failed:
+        # the rank whose own check failed first, not a peer that lost its connection
+        failed.sort(key=lambda f: "AssertionError" not in f[2])
+        r, rc, out = failed[0]
+        others = [ln for _, _, o in failed[1:] for ln in o.splitlines() if "AssertionError" in ln]
+        raise AssertionError(f"rank {r} failed (rc={rc}):\n{out[-4000:]}\nother ranks:\n" + "\n".join(others))
     for r, (rc, out) in enumerate(outs):
-        assert rc == 0, f"rank {r} failed (rc={rc}):\n{out[-4000:]}"
         assert f"rank {r} ok" in out
 
 
@@ -94,3 +101,49 @@ def test_distributed_kron_solve_gpu(world):
     import torch
     assert torch.cuda.device_count() >= 1, "GPU test selected but no GPU visible"
     _launch("gpu_ksolve", world=world)
+
+
+@pytest.mark.parametrize("world,nd,want", [(1, 3, (1, 1, 1)), (4, 3, (2, 2, 1)), (8, 3, (2, 2, 2)),
+                                           (6, 2, (3, 2)), (12, 3, (3, 2, 2)), (7, 2, (7, 1))])
+def test_dims_create(world, nd, want):
+    assert dims_create(world, nd) == want
+
+
+def test_cart_distribution_grid():
+    """C-order ranks, per-axis blocks (slab_bounds) and neighbours of a 2x3x2 grid."""
+    npts = (11, 13, 9)
+    seen = np.zeros(npts, dtype=int)
+    for r in range(12):
+        d = CartDistribution(npts, (2, 3, 2), r)
+        assert d.rank_of(d.coords) == r
+        assert d.coords == (r // 6, (r // 2) % 3, r % 2)
+        for ax in range(3):
+            c = list(d.coords)
+            if d.prev[ax] is not None:
+                c[ax] -= 1
+                assert d.prev[ax] == d.rank_of(c)
+                c[ax] += 1
+            if d.next[ax] is not None:
+                c[ax] += 1
+                assert d.next[ax] == d.rank_of(c)
+            assert (d.prev[ax] is None) == (d.coords[ax] == 0)
+            assert (d.next[ax] is None) == (d.coords[ax] == d.dims[ax] - 1)
+        seen[tuple(slice(s, e) for s, e in zip(d.starts, d.ends))] += 1
+    assert (seen == 1).all()
+    with pytest.raises(ValueError):
+        CartDistribution((3, 8), (4, 1), 3)   # 3 points over 4 ranks: rank 3 owns none
+
+
+@pytest.mark.parametrize("dims", ["2x2x1", "1x2x2", "2x1x2", "2x2"])
+def test_four_rank_cart_exchange_and_block_apply_cpu(dims):
+    _launch("cart_cpu", world=4, extra_env={"POMS_TEST_CART_DIMS": dims})
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("dims", ["2x2x1", "1x2x2", "2x2"])
+def test_four_rank_cart_operator_and_vcycle_gpu(dims):
+    """spl Cart over a 2x2 process grid (axes 0/1, axes 1/2, and 2D): device
+    operator, sweeps, reductions, transfer and the V-cycle against the oracle."""
+    import torch
+    assert torch.cuda.device_count() >= 1, "GPU test selected but no GPU visible"
+    _launch("cart_gpu", world=4, extra_env={"POMS_TEST_CART_DIMS": dims})

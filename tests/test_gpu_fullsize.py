@@ -130,7 +130,7 @@ def test_variants_agree_full_size(gpu, cfg):
     x._mark_written()
     A.set_variant(0)
     ref = A.dot(x)._data.clone()
-    for v in (1, 2, 3, 4, 5, 7, 9, 10):
+    for v in (4, 7, 9, 10):
         A.set_variant(v)
         y = A.dot(x)
         assert trel(y._data, ref) <= 1e-14, v
