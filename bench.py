@@ -1,5 +1,6 @@
 #!/usr/bin/env python3
-"""Benchmark: two-level B-spline multigrid V-cycle, 3D -Δu+u, p=3, 512^3 cells.
+"""Benchmark: two-level B-spline multigrid V-cycle, 3D -Δu+u, p=3, 512^3 cells
+(``--ndim 2``: BASELINE config 2, 2D p=3 on a 1024^2 grid).
 
 Contract (see the repo's task statement): ``python bench.py --gpus N --steps K
 --warmup W``; for N > 1 launched by ``torch.distributed.run`` with one rank per
@@ -16,6 +17,11 @@ Reported beside the headline ``value`` (V-cycle DOF/s, whole job):
 * ``kron_spmv`` -- the plain Kron mat-vec (16 B/DOF) timed in isolation;
 * ``cpu_baseline`` -- the C/OpenMP restatement of the reference loop nests
   running the same V-cycle on the host (rank 0, N = 1), bounded sample.
+
+With ``--ndim 2`` the grid is 2D (N > 1: a Cart block decomposition, torch
+transport) and the isolated mat-vec is timed after a 512 MiB MALL flush per launch
+(a 1027^2 vector is 8.4 MB: without the flush it would be served from the
+256 MB MALL / L2, not HBM).
 """
 from __future__ import annotations
 
@@ -39,8 +45,11 @@ def parse():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=3)
     ap.add_argument("--warmup", type=int, default=1)
+    ap.add_argument("--ndim", type=int, default=3, choices=(2, 3))
     ap.add_argument("--p", type=int, default=3)
-    ap.add_argument("--cells", type=int, default=512)
+    ap.add_argument("--cells", type=int, default=None, help="cells per axis (default 512 in 3D, 1024 in 2D)")
+    ap.add_argument("--flush-mall", type=int, default=None,
+                    help="MiB written between the isolated mat-vec launches (default 512 in 2D, 0 in 3D)")
     ap.add_argument("--coarse", type=int, default=8)
     ap.add_argument("--chunk", type=int, default=0)
     ap.add_argument("--kron-reps", type=int, default=30)
@@ -54,7 +63,16 @@ def parse():
                     help="tools/pmc_traffic.py summary of a separate rocprofv3 --pmc pass "
                          "(FETCH_SIZE x2 + WRITE_SIZE per launch) used for roofline.traffic; used only "
                          "when its recorded p and kernel variant are this run's")
-    return ap.parse_args()
+    a = ap.parse_args()
+    if a.cells is None:
+        a.cells = 512 if a.ndim == 3 else 1024
+    if a.flush_mall is None:
+        a.flush_mall = 512 if a.ndim == 2 else 0
+    if a.ndim == 2 and a.cpu_cells == 160:
+        a.cpu_cells = a.cells         # the 2D bench size runs on the host in seconds
+    if a.ndim == 2 and a.cpu_cells_1core == 64:
+        a.cpu_cells_1core = 256
+    return a
 
 
 def main():
@@ -71,14 +89,21 @@ def main():
     if world > 1:
         dist.init_process_group("nccl", device_id=torch.device(f"cuda:{local}"))
 
-    from poms_amd.dist import SlabDistribution
+    from poms_amd.dist import CartDistribution, SlabDistribution
     from poms_amd.mg import TwoLevelVCycle
 
+    nd = args.ndim
     n = args.cells + args.p
-    # N > 1: the library's RCCL communicator, or an exception (no silent fall-back)
-    slab = SlabDistribution.from_process_group(n) if world > 1 else None
-    transport = slab.transport if slab is not None else "none"
-    mg = TwoLevelVCycle(args.p, args.cells, args.coarse, ndim=3, dist=slab, chunk=args.chunk)
+    if world == 1:
+        dd = None
+    elif nd == 3:
+        # N > 1: the library's RCCL communicator, or an exception (no silent fall-back)
+        dd = SlabDistribution.from_process_group(n)
+    else:
+        dd = CartDistribution.from_process_group((n, n))
+    transport = dd.transport if dd is not None else "none"
+    parallelism = (f"slab{world}" if nd == 3 else "cart" + "x".join(map(str, dd.dims))) if dd is not None else "slab1"
+    mg = TwoLevelVCycle(args.p, args.cells, args.coarse, ndim=nd, dist=dd, chunk=args.chunk)
     bf = mg.rhs_ones()
     A = mg.A
     local_dof = 1
@@ -135,11 +160,15 @@ def main():
     yk = mg.space.empty()
     for _ in range(3):
         A.dot(xv, out=yk)
+    flush = torch.empty(args.flush_mall * (1 << 17), dtype=torch.float64, device="cuda") if args.flush_mall else None
     barrier()
     A.timer = []
-    for _ in range(args.kron_reps):
+    for i in range(args.kron_reps):
+        if flush is not None:
+            flush.fill_(float(i))   # evict x, y and the factors from L2 / MALL (not timed)
         A.dot(xv, out=yk)
     barrier()
+    del flush
     # the isolated apply: median over the launches (robust to the first launches after
     # the V-cycle, which run slower); the mean is reported beside it
     kron_s, _ = per_call(A.timer, "apply", "median")
@@ -155,7 +184,8 @@ def main():
     if args.pmc_json and Path(args.pmc_json).exists():
         pm = json.loads(Path(args.pmc_json).read_text())
         # per-DOF HBM bytes of the SAME kernel (order p, variant) scaled to this rank's slab
-        if pm.get("bytes_per_dof") and pm.get("p") == args.p and pm.get("variant") == jac_v:
+        if pm.get("bytes_per_dof") and pm.get("p") == args.p and pm.get("variant") == jac_v and \
+                pm.get("ndim", 3) == nd:
             traffic = pm["bytes_per_dof"] * local_dof
 
     cpu = None
@@ -164,30 +194,31 @@ def main():
             from oracle import cpu_baseline as cb
             host = cb.host_info()
             threads = host["nproc"]   # every CPU this process may use (GNU nproc)
-            r = cb.time_vcycle(N=args.cpu_cells, p=args.p, Nc=args.coarse, cycles=args.cpu_cycles, threads=threads)
-            r1 = cb.time_vcycle(N=args.cpu_cells_1core, p=args.p, Nc=args.coarse, cycles=1, threads=1)
-            full = cb.time_apply(N=args.cells, p=args.p, threads=threads, reps=2)
+            r = cb.time_vcycle(N=args.cpu_cells, p=args.p, Nc=args.coarse, cycles=args.cpu_cycles, threads=threads,
+                               ndim=nd)
+            r1 = cb.time_vcycle(N=args.cpu_cells_1core, p=args.p, Nc=args.coarse, cycles=1, threads=1, ndim=nd)
+            full = cb.time_apply(N=args.cells, p=args.p, threads=threads, reps=2, ndim=nd)
             cpu = {"value": r["dof_per_s"], "unit": "DOF/s", "cores": r["threads"], "kind": "port",
                    "nproc": host["nproc"], "os_cpu_count": host["os_cpu_count"], "cpu_model": host["cpu_model"],
                    "sample": (f"{args.cpu_cycles} full two-level V-cycles (same schedule, incl. the reference's "
-                              f"discarded mat-vec) at {args.cpu_cells}^3 cells p={args.p} ({r['dof']} DOF) on "
+                              f"discarded mat-vec) at {args.cpu_cells}^{nd} cells p={args.p} ({r['dof']} DOF) on "
                               f"{r['threads']} threads, C/OpenMP restatement of the reference loop nests "
                               f"(oracle/kron_cpu.c), {r['seconds_per_cycle']:.2f} s per cycle; a bench-size "
-                              f"({args.cells}^3) CPU V-cycle is ~{r['seconds_per_cycle'] * (args.cells + args.p) ** 3 / r['dof']:.0f} s "
-                              f"at this rate, outside the bounded sample"),
+                              f"({args.cells}^{nd}) CPU V-cycle is ~{r['seconds_per_cycle'] * (args.cells + args.p) ** nd / r['dof']:.1f} s "
+                              f"at this rate" + (", outside the bounded sample" if args.cpu_cells != args.cells else "")),
                    "single_core": {"value": r1["dof_per_s"], "unit": "DOF/s", "cores": 1,
-                                   "sample": f"1 V-cycle at {args.cpu_cells_1core}^3 cells ({r1['dof']} DOF), "
+                                   "sample": f"1 V-cycle at {args.cpu_cells_1core}^{nd} cells ({r1['dof']} DOF), "
                                              f"{r1['seconds_per_cycle']:.2f} s"},
                    "kron_apply_full_size": {"value": full["gbps"], "unit": "GB/s (16 B/DOF)",
                                             "cores": full["threads"], "seconds_per_apply": full["seconds_per_apply"],
-                                            "sample": f"{args.cells}^3 cells ({full['dof']} DOF), the bench size"}}
+                                            "sample": f"{args.cells}^{nd} cells ({full['dof']} DOF), the bench size"}}
         except Exception as e:  # baseline is informative only
             cpu = {"value": None, "unit": "DOF/s", "cores": 0, "kind": "port", "sample": f"failed: {e!r}"}
 
     if rank == 0:
         gdof = mg.ndof
         out = {
-            "metric": METRIC,
+            "metric": METRIC if nd == 3 else METRIC.replace("3D Poisson p=3", f"2D Poisson p={args.p}"),
             "value": gdof / sec_per_cycle,
             "unit": "DOF/s",
             "n_gpus": world,
@@ -200,20 +231,21 @@ def main():
             "dtype": "f64",
             "data": "synthetic: b = 1 RHS (sources/mg_jac.py:57-62), uniform open knots, assembled -Δu+u factors",
             "config": {
-                "workload": (f"two-level V-cycle, 3D -Δu+u, p={args.p}, {args.cells}^3 cells ({n}^3 DOF), "
-                             f"coarse {args.coarse}^3 cells, pre/post pcg(tol=1e-6, maxiter=10) + damped Jacobi"),
-                "global_dof": gdof, "p": args.p, "cells": args.cells, "coarse_cells": args.coarse,
-                "parallelism": f"slab{world}",
+                "workload": (f"two-level V-cycle, {nd}D -Δu+u, p={args.p}, {args.cells}^{nd} cells ({n}^{nd} DOF), "
+                             f"coarse {args.coarse}^{nd} cells, pre/post pcg(tol=1e-6, maxiter=10) + damped Jacobi"),
+                "global_dof": gdof, "ndim": nd, "p": args.p, "cells": args.cells, "coarse_cells": args.coarse,
+                "parallelism": parallelism,
             },
             "comm": transport,
             "roofline": {
-                "kernel": f"{KERNEL_NAMES.get(jac_v, f'variant {jac_v}')}<P={args.p},3D,SUM,JACOBI> (Kron apply + damped-Jacobi update)",
+                "kernel": f"{KERNEL_NAMES.get(jac_v, f'variant {jac_v}')}<P={args.p},{nd}D,SUM,JACOBI> (Kron apply + damped-Jacobi update)",
                 "bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBPS, "unit": "GB/s",
                 "frac": achieved / HBM_PEAK_GBPS, "traffic": traffic,
                 "algorithmic_bytes_per_launch": bytes_sweep, "avg_launch_us": sweep_s * 1e6,
                 "launches_timed": n_sweeps,
             },
-            "kron_spmv": {"kernel": f"{KERNEL_NAMES.get(app_v, f'variant {app_v}')}<P={args.p},3D,SUM,APPLY>",
+            "kron_spmv": {"kernel": f"{KERNEL_NAMES.get(app_v, f'variant {app_v}')}<P={args.p},{nd}D,SUM,APPLY>",
+                          "mall_flush_mib": args.flush_mall,
                           "achieved": kron_gbps, "unit": "GB/s", "frac": kron_gbps / HBM_PEAK_GBPS,
                           "median_launch_us": kron_s * 1e6, "mean_launch_us": kron_mean_s * 1e6,
                           "bytes_per_dof": 16, "launches": args.kron_reps},

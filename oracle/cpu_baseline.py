@@ -37,6 +37,9 @@ def _load():
     lib.oracle_kron_sum_3d.argtypes = [i64, i64, i64, i64, dp, dp, dp, dp, dp, dp, dp, dp, dp, C.c_int, d,
                                        dp, dp, dp, dp]
     lib.oracle_kron_sum_3d.restype = d
+    lib.oracle_kron_sum_3d_b0.argtypes = [i64, i64, i64, i64, i64, dp, dp, dp, dp, dp, dp, dp, dp, dp, C.c_int, d,
+                                          dp, dp, dp, dp]
+    lib.oracle_kron_sum_3d_b0.restype = d
     lib.oracle_axpby_3d.argtypes = [i64, i64, i64, i64, d, dp, d, dp, dp]
     lib.oracle_dot_3d.argtypes = [i64, i64, i64, i64, dp, dp]
     lib.oracle_dot_3d.restype = d
@@ -61,32 +64,47 @@ def _p(a: np.ndarray):
 
 
 class CpuLaplace3D:
-    """-Δu + c u on a single 3D padded grid, C kernels (global = local)."""
+    """-Δu + c u on a single padded grid, C kernels (global = local).  ``ndim = 2``
+    runs the 2D operator c M⊗M + K⊗M + M⊗K as the 3D loop nest with one axis-0
+    plane whose factors are the scalars (c, 1, 0): same kernel, same loop order."""
 
-    def __init__(self, M, K, p: int, c: float = 1.0):
+    def __init__(self, M, K, p: int, c: float = 1.0, ndim: int = 3):
         self.n = M.shape[0]
         self.p = p
+        self.ndim = ndim
         n, W = self.n, 2 * p + 1
-        assert M.shape == (n, W)
-        self.A0 = np.ascontiguousarray(c * M + K)
+        assert M.shape == (n, W) and ndim in (2, 3)
         self.M = np.ascontiguousarray(M)
         self.K = np.ascontiguousarray(K)
+        if ndim == 3:
+            self.A0 = np.ascontiguousarray(c * M + K)
+            self.M0 = self.M
+            self.n3 = (n, n, n)
+        else:
+            self.A0 = np.zeros((1, W))
+            self.A0[0, p] = c
+            self.M0 = np.zeros((1, W))
+            self.M0[0, p] = 1.0
+            self.n3 = (1, n, n)
+        n0 = self.n3[0]
         P = n + 2 * p
-        self.shape = (P, P, P)
-        self.ta = np.zeros(P * P * n)
-        self.tb = np.zeros(P * P * n)
-        self.tc = np.zeros(P * n * n)
-        self.td = np.zeros(P * n * n)
-        self.ndof = n ** 3
+        self.shape = (n0 + 2 * p, P, P)
+        self.ta = np.zeros((n0 + 2 * p) * P * n)
+        self.tb = np.zeros((n0 + 2 * p) * P * n)
+        self.tc = np.zeros((n0 + 2 * p) * n * n)
+        self.td = np.zeros((n0 + 2 * p) * n * n)
+        self.ndof = n0 * n * n
+        self.interior = tuple(slice(p, p + m) for m in self.n3)
 
     def zeros(self):
         return np.zeros(self.shape)
 
     def _run(self, x, b, y, mode, omega=0.0):
-        n, p = self.n, self.p
-        return lib().oracle_kron_sum_3d(n, n, n, p, _p(self.A0), _p(self.M), _p(self.M), _p(self.K), _p(self.M),
-                                        _p(self.K), _p(x), _p(b) if b is not None else None, _p(y), mode,
-                                        omega, _p(self.ta), _p(self.tb), _p(self.tc), _p(self.td))
+        (n0, n1, n2), p = self.n3, self.p
+        return lib().oracle_kron_sum_3d_b0(n0, n1, n2, p, p if self.ndim == 3 else 0, _p(self.A0), _p(self.M0),
+                                           _p(self.M), _p(self.K), _p(self.M), _p(self.K), _p(x),
+                                           _p(b) if b is not None else None, _p(y), mode, omega, _p(self.ta),
+                                           _p(self.tb), _p(self.tc), _p(self.td))
 
     def dot(self, x):
         y = self.zeros()
@@ -104,13 +122,13 @@ class CpuLaplace3D:
         return y, nrm
 
     def vdot(self, a, b):
-        n, p = self.n, self.p
-        return lib().oracle_dot_3d(n, n, n, p, _p(a), _p(b))
+        (n0, n1, n2), p = self.n3, self.p
+        return lib().oracle_dot_3d(n0, n1, n2, p, _p(a), _p(b))
 
     def axpby(self, a, x, b, y):
-        n, p = self.n, self.p
+        (n0, n1, n2), p = self.n3, self.p
         z = self.zeros()
-        lib().oracle_axpby_3d(n, n, n, p, a, _p(x), b, _p(y), _p(z))
+        lib().oracle_axpby_3d(n0, n1, n2, p, a, _p(x), b, _p(y), _p(z))
         return z
 
 
@@ -149,7 +167,8 @@ def pcg(A: CpuLaplace3D, b, x0=None, tol=1e-6, maxiter=10):
     return x, {"niter": k, "success": nrmr < tol * nrmr0, "res_norm": sqrt(nrmr)}
 
 
-def time_vcycle(N: int = 96, p: int = 3, Nc: int = 8, cycles: int = 1, threads: int | None = None):
+def time_vcycle(N: int = 96, p: int = 3, Nc: int = 8, cycles: int = 1, threads: int | None = None,
+                ndim: int = 3):
     """Time the reference-shaped two-level V-cycle on the host; returns a dict."""
     import sys
     sys.path.insert(0, str(HERE.parent))
@@ -166,27 +185,40 @@ def time_vcycle(N: int = 96, p: int = 3, Nc: int = 8, cycles: int = 1, threads: 
     if P1.shape[0] != nf:
         raise ValueError(f"coarse knots ({Nc} cells) are not nested in the fine ones ({N} cells)")
     M, K = assemble_1d(Tf, p)
-    A = CpuLaplace3D(M, K, p)
+    A = CpuLaplace3D(M, K, p, ndim=ndim)
     Md, Kd = band_to_dense(M), band_to_dense(K)
     Mc, Kc = P1.T @ Md @ P1, P1.T @ Kd @ P1
-    kr = lambda a, b, c: np.kron(np.kron(a, b), c)
-    Ac = kr(Mc, Mc, Mc) + kr(Kc, Mc, Mc) + kr(Mc, Kc, Mc) + kr(Mc, Mc, Kc)
+    if ndim == 3:
+        kr = lambda a, b, c: np.kron(np.kron(a, b), c)
+        Ac = kr(Mc, Mc, Mc) + kr(Kc, Mc, Mc) + kr(Mc, Kc, Mc) + kr(Mc, Mc, Kc)
+    else:
+        Ac = np.kron(Mc, Mc) + np.kron(Kc, Mc) + np.kron(Mc, Kc)
     lu = sla.lu_factor(Ac)
-    n = A.n
     b = A.zeros()
-    b[p:p + n, p:p + n, p:p + n] = 1.0
-    sl = (slice(p, p + n),) * 3
+    sl = A.interior
+    b[sl] = 1.0
+
+    def restrict(r):
+        if ndim == 3:
+            return np.einsum("ia,jb,kc,ijk->abc", P1, P1, P1, r[sl], optimize=True).reshape(-1)
+        return (P1.T @ r[sl][0] @ P1).reshape(-1)
+
+    def prolong(xc):
+        if ndim == 3:
+            return np.einsum("ia,jb,kc,abc->ijk", P1, P1, P1, xc.reshape((nc,) * 3), optimize=True)
+        return (P1 @ xc.reshape(nc, nc) @ P1.T)[None]
+
     t0 = time.perf_counter()
     for _ in range(cycles):
         xf, ipre = pcg(A, b)
         rf = A.residual(b, xf)
-        rc = np.einsum("ia,jb,kc,ijk->abc", P1, P1, P1, rf[sl], optimize=True).reshape(-1)
-        xc = sla.lu_solve(lu, rc).reshape((nc,) * 3)
-        xf[sl] += np.einsum("ia,jb,kc,abc->ijk", P1, P1, P1, xc, optimize=True)
+        xc = sla.lu_solve(lu, restrict(rf))
+        xf[sl] += prolong(xc)
         xf2, ipos = pcg(A, b, x0=xf)
     dt = (time.perf_counter() - t0) / cycles
-    return {"seconds_per_cycle": dt, "dof": n ** 3, "dof_per_s": n ** 3 / dt,
-            "threads": lib().oracle_num_threads(), "info_pre": ipre, "info_pos": ipos, "N": N, "p": p}
+    return {"seconds_per_cycle": dt, "dof": A.ndof, "dof_per_s": A.ndof / dt,
+            "threads": lib().oracle_num_threads(), "info_pre": ipre, "info_pos": ipos, "N": N, "p": p,
+            "ndim": ndim}
 
 
 def host_info() -> dict:
@@ -208,7 +240,7 @@ def host_info() -> dict:
     return {"nproc": nproc, "os_cpu_count": os.cpu_count(), "cpu_model": model}
 
 
-def time_apply(N: int, p: int = 3, threads: int | None = None, reps: int = 2) -> dict:
+def time_apply(N: int, p: int = 3, threads: int | None = None, reps: int = 2, ndim: int = 3) -> dict:
     """The sum-factorised -Δu+u apply (the reference kernel's loop nest) at N^3
     cells on the host: seconds per apply and algorithmic GB/s (16 B/DOF)."""
     import sys
@@ -218,9 +250,9 @@ def time_apply(N: int, p: int = 3, threads: int | None = None, reps: int = 2) ->
     if threads:
         lib().oracle_set_num_threads(int(threads))
     M, K = assemble_1d(uniform_knots(p, N), p)
-    A = CpuLaplace3D(M, K, p)
+    A = CpuLaplace3D(M, K, p, ndim=ndim)
     x = A.zeros()
-    x[p:-p, p:-p, p:-p] = np.random.default_rng(0).uniform(-1, 1, (A.n,) * 3)
+    x[A.interior] = np.random.default_rng(0).uniform(-1, 1, A.n3)
     y = A.zeros()
     A._run(x, None, y, 0)   # first touch of the temporaries
     t0 = time.perf_counter()

@@ -54,19 +54,23 @@ void oracle_kron_dot_pyccel_2d(const int64_t* starts, const int64_t* ends, const
  * returns sum(dr^2) for mode 2.
  * Work arrays: ta, tb of (n0+2p)*(n1+2p)*n2 doubles; tc, td of (n0+2p)*n1*n2.
  */
-double oracle_kron_sum_3d(int64_t n0, int64_t n1, int64_t n2, int64_t p,
-                          const double* A0, const double* M0, const double* M1, const double* K1,
-                          const double* M2, const double* K2, const double* x, const double* b,
-                          double* y, int mode, double omega,
-                          double* ta, double* tb, double* tc, double* td) {
+/* b0: half-width of the axis-0 bands actually used (p for 3D; 0 when a 2D
+ * operator runs as one axis-0 plane with scalar A0 = c, M0 = 1): passes 1 and 2
+ * then skip the ghost planes no band reaches. */
+double oracle_kron_sum_3d_b0(int64_t n0, int64_t n1, int64_t n2, int64_t p, int64_t b0,
+                             const double* A0, const double* M0, const double* M1, const double* K1,
+                             const double* M2, const double* K2, const double* x, const double* b,
+                             double* y, int mode, double omega,
+                             double* ta, double* tb, double* tc, double* td) {
     const int64_t W = 2 * p + 1;
     const int64_t P0 = n0 + 2 * p, P1 = n1 + 2 * p, P2 = n2 + 2 * p;
     const int64_t xs1 = P2, xs0 = P1 * P2;            /* padded x / y / b */
     const int64_t as1 = n2, as0 = P1 * n2;             /* ta, tb */
     const int64_t cs1 = n2, cs0 = n1 * n2;             /* tc, td */
+    const int64_t jlo = p - b0, jhi = P0 - (p - b0); /* planes the axis-0 bands reach */
     /* pass 1: last axis, all planes and rows incl. ghosts */
-#pragma omp parallel for schedule(static)
-    for (int64_t j0 = 0; j0 < P0; ++j0)
+#pragma omp parallel for collapse(2) schedule(static)
+    for (int64_t j0 = jlo; j0 < jhi; ++j0)
         for (int64_t j1 = 0; j1 < P1; ++j1)
             for (int64_t i2 = 0; i2 < n2; ++i2) {
                 double sa = 0.0, sb = 0.0;
@@ -79,8 +83,8 @@ double oracle_kron_sum_3d(int64_t n0, int64_t n1, int64_t n2, int64_t p,
                 tb[IDX3(j0, j1, i2, as0, as1)] = sb;
             }
     /* pass 2: middle axis, all planes incl. ghosts, owned rows */
-#pragma omp parallel for schedule(static)
-    for (int64_t j0 = 0; j0 < P0; ++j0)
+#pragma omp parallel for collapse(2) schedule(static)
+    for (int64_t j0 = jlo; j0 < jhi; ++j0)
         for (int64_t i1 = 0; i1 < n1; ++i1)
             for (int64_t i2 = 0; i2 < n2; ++i2) {
                 double sc = 0.0, sd = 0.0;
@@ -95,12 +99,12 @@ double oracle_kron_sum_3d(int64_t n0, int64_t n1, int64_t n2, int64_t p,
             }
     /* pass 3: first axis, owned planes */
     double nrm = 0.0;
-#pragma omp parallel for schedule(static) reduction(+ : nrm)
+#pragma omp parallel for collapse(2) schedule(static) reduction(+ : nrm)
     for (int64_t i0 = 0; i0 < n0; ++i0)
         for (int64_t i1 = 0; i1 < n1; ++i1)
             for (int64_t i2 = 0; i2 < n2; ++i2) {
                 double s = 0.0;
-                for (int64_t k = 0; k < W; ++k)
+                for (int64_t k = p - b0; k <= p + b0; ++k)
                     s += A0[i0 * W + k] * tc[IDX3(i0 + k, i1, i2, cs0, cs1)]
                        + M0[i0 * W + k] * td[IDX3(i0 + k, i1, i2, cs0, cs1)];
                 const int64_t o = IDX3(i0 + p, i1 + p, i2 + p, xs0, xs1);
@@ -118,6 +122,14 @@ double oracle_kron_sum_3d(int64_t n0, int64_t n1, int64_t n2, int64_t p,
                 }
             }
     return nrm;
+}
+
+double oracle_kron_sum_3d(int64_t n0, int64_t n1, int64_t n2, int64_t p,
+                          const double* A0, const double* M0, const double* M1, const double* K1,
+                          const double* M2, const double* K2, const double* x, const double* b,
+                          double* y, int mode, double omega,
+                          double* ta, double* tb, double* tc, double* td) {
+    return oracle_kron_sum_3d_b0(n0, n1, n2, p, p, A0, M0, M1, K1, M2, K2, x, b, y, mode, omega, ta, tb, tc, td);
 }
 
 /* ---- vector algebra on the padded interior -------------------------------- */

@@ -1,0 +1,93 @@
+#!/usr/bin/env python3
+"""One-slab proxy of the 8-GPU V-cycle on ONE GPU.
+
+Rank r of the 8-rank bench owns 64-65 of the 515 axis-0 planes.  This runs the
+same V-cycle schedule (pcg + damped Jacobi, residual, restriction, coarse solve,
+prolongation, post pcg) on a single-GPU grid of (planes x 515 x 515) DOF: the
+per-rank kernel work without the ghost exchange and all-reduces, i.e. a lower
+bound on the 8-GPU cycle time.  Comparing the wall time per cycle with the sum of
+kernel durations (rocprofv3 --kernel-trace --stats on this script) gives the
+host-issue floor: the time the GPU waits for the Python host.
+
+    python tools/slab_proxy.py --planes 67 --steps 3
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import sys
+import time
+from pathlib import Path
+
+ROOT = Path(__file__).resolve().parents[1]
+sys.path.insert(0, str(ROOT))
+
+
+def build(planes_cells: int, cells: int, p: int, coarse: int):
+    import numpy as np
+    import scipy.linalg as sla
+    import torch
+    from poms_amd.mg import TwoLevelVCycle, two_level_setup_1d
+    from poms_amd.multilevels import KronTransfer
+    from poms_amd.splines import assemble_1d, band_to_dense, uniform_knots
+    from poms_amd.stencil import F64, KronOperator, StencilVectorSpace
+
+    cells3 = (planes_cells, cells, cells)
+    Ms, Ks, Ps, Mcs, Kcs = [], [], [], [], []
+    for N in cells3:
+        T, _, P1 = two_level_setup_1d(p, uniform_knots(p, N), uniform_knots(p, coarse))
+        M, K = assemble_1d(T, p)
+        Ms.append(M), Ks.append(K), Ps.append(P1)
+        Md, Kd = band_to_dense(M), band_to_dense(K)
+        Mcs.append(P1.T @ Md @ P1), Kcs.append(P1.T @ Kd @ P1)
+    npts = [m.shape[0] for m in Ms]
+    mg = TwoLevelVCycle.__new__(TwoLevelVCycle)
+    mg.p, mg.ndim, mg.glt, mg.tol, mg.maxiter, mg.post_smoother = p, 3, None, 1e-6, 10, "jacobi"
+    mg.space = StencilVectorSpace(npts, [p] * 3, align=True)
+    mg.A = KronOperator.laplace(mg.space, Ms, Ks)
+    mg.transfer = KronTransfer(mg.space, Ps)
+    kr = lambda a, b, c: np.kron(np.kron(a, b), c)
+    Ac = kr(Mcs[0], Mcs[1], Mcs[2])
+    for d in range(3):
+        Ac = Ac + kr(*[Kcs[e] if e == d else Mcs[e] for e in range(3)])
+    Ainv = sla.lu_solve(sla.lu_factor(Ac), np.eye(Ac.shape[0]))
+    mg.Ainv = torch.from_numpy(np.ascontiguousarray(Ainv)).to(f"cuda:{mg.space.device}")
+    mg.rc = torch.empty(Ac.shape[0], dtype=F64, device=mg.Ainv.device)
+    mg.xc = torch.empty(Ac.shape[0], dtype=F64, device=mg.Ainv.device)
+    return mg, npts
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--planes", type=int, default=67, help="axis-0 DOF planes (p + cells, nested in the coarse grid)")
+    ap.add_argument("--cells", type=int, default=512)
+    ap.add_argument("--p", type=int, default=3)
+    ap.add_argument("--coarse", type=int, default=8)
+    ap.add_argument("--steps", type=int, default=3)
+    ap.add_argument("--warmup", type=int, default=1)
+    a = ap.parse_args()
+    import torch
+    torch.cuda.set_device(0)
+    mg, npts = build(a.planes - a.p, a.cells, a.p, a.coarse)
+    bf = mg.rhs_ones()
+    for _ in range(a.warmup):
+        mg.cycle(bf)
+    torch.cuda.synchronize()
+    mg.A.timer = []
+    t0 = time.perf_counter()
+    for _ in range(a.steps):
+        x, ipre, ipos = mg.cycle(bf)
+    torch.cuda.synchronize()
+    dt = (time.perf_counter() - t0) / a.steps
+    # operator launches only (the dominant kernels), their GPU time per cycle
+    op_s = sum(e0.elapsed_time(e1) for _, e0, e1, _ in mg.A.timer) * 1e-3 / a.steps
+    n_op = len(mg.A.timer) / a.steps
+    mg.A.timer = None
+    print(json.dumps({"proxy": f"{npts[0]}x{npts[1]}x{npts[2]} DOF (one slab of the 8-GPU bench + halo-free)",
+                      "ms_per_cycle": dt * 1e3, "operator_launches_per_cycle": n_op,
+                      "operator_gpu_ms_per_cycle": op_s * 1e3,
+                      "info_pre": ipre, "info_pos": ipos}), flush=True)
+
+
+if __name__ == "__main__":
+    main()
