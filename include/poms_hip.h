@@ -404,6 +404,43 @@ int poms_op_run_dist(poms_op* op, poms_comm* comm, int epilogue, double omega, c
                      int want_norm, int want_dot, double* norm_dev, double* dot_dev,
                      int lazy_count, double* host_dst, int* ticket, void* stream);
 
+/* ---- native smoother loop ----------------------------------------------------- */
+/* pcg(A, damped_jacobi, b, x0, tol, maxiter) of `sources/solvers.py:69-135` with the
+ * damped-Jacobi preconditioner of :167-235 (omega, jtol, jmaxiter), as ONE host call:
+ * the launches, device-side scalars (alpha = s.r / p.q, beta = s.r / s.r_old) and stop
+ * tests of poms_amd.solvers.pcg -- bitwise the same iterates -- without a Python round
+ * trip per launch; each norm is read one launch after the next one is queued.  The
+ * V-cycle's pre/post smoothing (`sources/mg_jac.py:88,104`).
+ * comm != NULL: the slab-distributed form (ghost exchange per operator call through
+ * poms_op_run_dist with neighbours prev / next, sums all-reduced).
+ * x: in = x0 when has_x0, out = the solution (current ghosts not required).
+ * work: 5 vectors of the operator's layout with zero ghosts (r, q and three
+ * preconditioner buffers), not aliasing b or x.                                  */
+typedef struct poms_pcg_opts {
+    double tol;      /* pcg: stop when r.r < tol * ||r0|| (the reference's mixed norms) */
+    int maxiter;
+    double jtol;     /* damped Jacobi: stop when dr.dr < jtol^2                         */
+    int jmaxiter;
+    double omega;    /* 2/3                                                             */
+    int prev, next;  /* slab neighbours (comm != NULL), -1: none                        */
+} poms_pcg_opts;
+typedef struct poms_pcg_info {
+    int niter;
+    int success;
+    double res_norm;
+} poms_pcg_info;
+int poms_pcg_jacobi(poms_op* op, poms_comm* comm, const poms_pcg_opts* opts, const double* b, double* x,
+                    int has_x0, double* const* work, poms_pcg_info* info, void* stream);
+/* Launch timing: with enable, operator launches on this op (any caller, including
+ * poms_pcg_jacobi) of `epilogue` (-1: all; see poms_op_kernel_variant), every
+ * `every`-th one, are bracketed by HIP events on their stream; enabling clears the
+ * record and pre-creates `reserve` event pairs (an event record costs the host a
+ * few microseconds: sample to keep the timed work unperturbed).
+ * poms_op_timing_read sums the recorded launches of one epilogue: total
+ * milliseconds, launch count and output DOFs (synchronises on the events).      */
+int poms_op_timing(poms_op* op, int enable, int epilogue, int every, int reserve);
+int poms_op_timing_read(poms_op* op, int epilogue, double* total_ms, int64_t* launches, int64_t* dofs);
+
 #ifdef __cplusplus
 }
 #endif

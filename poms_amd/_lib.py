@@ -40,6 +40,15 @@ class Layout(C.Structure):
         return lay
 
 
+class PcgOpts(C.Structure):
+    _fields_ = [("tol", C.c_double), ("maxiter", C.c_int), ("jtol", C.c_double), ("jmaxiter", C.c_int),
+                ("omega", C.c_double), ("prev", C.c_int), ("next", C.c_int)]
+
+
+class PcgInfo(C.Structure):
+    _fields_ = [("niter", C.c_int), ("success", C.c_int), ("res_norm", C.c_double)]
+
+
 _vp = C.c_void_p
 _i64 = C.c_int64
 _d = C.c_double
@@ -124,6 +133,9 @@ _SIGS = {
     "poms_kron_solve_axis": [_vp, _i, _vp, _vp, _vp],
     "poms_kron_solve_axis0_dense": [_vp, _vp, _vp, _i64, _vp],
     "poms_kron_solve_bnd_2d": [_vp, _vp, _i64, _i, _i, _vp, _i64, _i, _i, _vp, _vp, _vp, _vp],
+    "poms_pcg_jacobi": [_vp, _vp, C.POINTER(PcgOpts), _vp, _vp, _i, C.POINTER(C.c_void_p), C.POINTER(PcgInfo), _vp],
+    "poms_op_timing": [_vp, _i, _i, _i, _i],
+    "poms_op_timing_read": [_vp, _i, C.POINTER(_d), C.POINTER(_i64), C.POINTER(_i64)],
     "poms_kron_solve_bnd_3d": [_vp, _vp, _i64, _i, _i, _vp, _i64, _i, _i, _vp, _i64, _i, _i, _vp, _vp, _vp,
                                _vp],
 }

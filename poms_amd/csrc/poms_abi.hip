@@ -3,6 +3,7 @@
 #include "../../include/poms_hip.h"
 
 #include <algorithm>
+#include <cmath>
 #include <cstdlib>
 #include <cstring>
 #include <vector>
@@ -80,6 +81,17 @@ struct poms_op {
     ToepConst tc{};
     double* coef = nullptr;   // FORM_STENCIL: (2p+1)^d coefficient planes of the owned rows
     int sp[3]{};              // FORM_STENCIL: stencil half-widths per axis
+    // native pcg loop (poms_pcg_jacobi): device scalars, their pinned host copies, events
+    double* sv_dev = nullptr;
+    double* sv_host = nullptr;
+    hipEvent_t sv_ev[8]{};
+    // launch timing (poms_op_timing): HIP events around every operator launch
+    struct TimedLaunch { int epi; int64_t ndof; hipEvent_t e0, e1; };
+    bool timing = false;
+    int t_epi = -1, t_every = 1;   // record launches of this epilogue only (-1: all), every n-th
+    int64_t t_seen = 0;
+    std::vector<TimedLaunch> tl;
+    size_t tl_used = 0;
 };
 
 static int resolve_variant(const poms_op* o, int epi);
@@ -462,8 +474,15 @@ int poms_op_stencil_data(poms_op* o, double* data_host) {
 
 int poms_op_destroy(poms_op* o) {
     if (!o) return 0;
-    for (double* p : {o->a0t, o->b0t, o->a1, o->b1, o->a2, o->b2, o->dg2a, o->dg2b, o->rdiag0, o->coef})
+    for (double* p : {o->a0t, o->b0t, o->a1, o->b1, o->a2, o->b2, o->dg2a, o->dg2b, o->rdiag0, o->coef, o->sv_dev})
         if (p) (void)hipFree(p);
+    if (o->sv_host) (void)hipHostFree(o->sv_host);
+    for (hipEvent_t e : o->sv_ev)
+        if (e) (void)hipEventDestroy(e);
+    for (auto& t : o->tl) {
+        (void)hipEventDestroy(t.e0);
+        (void)hipEventDestroy(t.e1);
+    }
     delete o;
     return 0;
 }
@@ -680,6 +699,20 @@ static int op_run(poms_op* o, int epi, double omega, const double* x, double* y,
     if ((want_norm || want_dot) && 2 * nblk > kScratch) { set_error("too many blocks for the partial-sum scratch"); return 1; }
     KronPtrs p{x, y, b, o->a0t, o->b0t, o->a1, o->b1, o->a2, o->b2,
                want_norm ? o->ctx->scratch : nullptr, want_dot ? o->ctx->scratch + nblk : nullptr, o->rdiag0};
+    poms_op::TimedLaunch* tlh = nullptr;
+    if (o->timing && (o->t_epi < 0 || o->t_epi == epi) && (o->t_seen++ % o->t_every) == 0) {
+        // events on the launch stream around this launch (a sample: every t_every-th)
+        if (o->tl_used == o->tl.size()) {
+            poms_op::TimedLaunch t{};
+            POMS_HIP_CHECK(hipEventCreate(&t.e0));
+            POMS_HIP_CHECK(hipEventCreate(&t.e1));
+            o->tl.push_back(t);
+        }
+        tlh = &o->tl[o->tl_used++];
+        tlh->epi = epi;
+        tlh->ndof = (int64_t)((ze - zb) + (ze2 - zb2)) * g.n1 * g.n2;
+        POMS_HIP_CHECK(hipEventRecord(tlh->e0, as_stream(stream)));
+    }
     const int rc = v == 10
         ? kron_v5_launch(o->pmax, epi, p, g, o->tc, v5_h, omega, as_stream(stream), v5_diag)
         : v == 0
@@ -688,6 +721,7 @@ static int op_run(poms_op* o, int epi, double omega, const double* x, double* y,
         ? kron_v4_launch(o->pmax, o->ndim == 3, o->form, epi, p, g, o->tc, omega, as_stream(stream),
                          v == 7 ? 0 : v - 91)
         : kron_v3_launch(v, o->pmax, o->ndim == 3, o->form, epi, p, g, o->tc, omega, as_stream(stream));
+    if (tlh) POMS_HIP_CHECK(hipEventRecord(tlh->e1, as_stream(stream)));
     if (rc) return 1;
     POMS_HIP_CHECK(hipGetLastError());
     o->last_partials = (want_norm || want_dot) ? nblk : 0;
@@ -1373,3 +1407,249 @@ int poms_kron_solve_bnd_3d(poms_ctx* ctx, const double* A_bnd, int64_t lda, int 
 }
 
 }  // extern "C"
+
+// ---- native pcg + damped-Jacobi loop (poms_pcg_jacobi) ------------------------
+// The V-cycle's smoother (`sources/mg_jac.py:88,104` -> `sources/solvers.py:69-135`
+// with psolve = damped_jacobi, :167-235) as one C call: the same launches, device
+// scalars and stop tests as poms_amd.solvers._pcg_device, without a Python round
+// trip per launch.  The host reads a norm one launch after queuing the next one
+// (the GPU never waits for the host while the host waits for that norm).
+namespace {
+
+enum { SC_SR = 0, SC_PQ = 1, SC_ONE = 2, SC_ALPHA = 3, SC_ALPHA2 = 4, SC_BETA = 5, SC_SRN = 6, SC_RR = 7,
+       SC_RR0 = 8, SC_J0 = 9 /* 9, 10: ||x1||^2, ||dr2||^2 */, SC_JN = 11 /* 11, 12: sweep norm ring */,
+       SC_N = 16 };
+enum { H_RR0 = 0, H_RR = 1, H_J0 = 2 /* 2 slots */, H_JN = 4 /* 2 slots */ };
+
+__global__ void pcg_scalars_kernel(double* sc, int mode) {
+    if (threadIdx.x != 0) return;
+    if (mode == 0) {            // alpha = s.r / p.q; pairs [1, alpha] and [alpha, beta]
+        const double a = sc[SC_SR] / sc[SC_PQ];
+        sc[SC_ONE] = 1.0;
+        sc[SC_ALPHA] = a;
+        sc[SC_ALPHA2] = a;
+    } else {                    // beta = s.r / s.r_old; s.r_old <- s.r
+        sc[SC_BETA] = sc[SC_SRN] / sc[SC_SR];
+        sc[SC_SR] = sc[SC_SRN];
+    }
+}
+
+struct PcgRun {
+    poms_op* op;
+    poms_comm* comm;
+    const poms_pcg_opts* o;
+    hipStream_t st;
+    void* stv;
+    double* sc;
+    double* host;
+    int64_t n0 = 1;
+
+    int run(int epi, const double* x, double* y, const double* b, double* nrm, double* dot) {
+        if (comm) {
+            const RowGeom g = row_geom(&op->L);
+            int tk = -1;
+            return poms_op_run_dist(op, comm, epi, o->omega, x, y, b, const_cast<double*>(x), g.s0, op->L.n[0],
+                                    (int)op->L.pads[0], op->pmax, o->prev, o->next, 1, nrm ? 1 : 0, dot ? 1 : 0, nrm,
+                                    dot, 0, nullptr, &tk, stv);
+        }
+        return poms_op_run_reduce2(op, epi, o->omega, x, y, b, 0, n0, 0, 0, nrm, dot, 0, stv);
+    }
+    int allsum(double* d, int cnt) { return comm ? poms_allreduce_sum(comm, d, cnt, stv, 1) : 0; }
+    int post(int sc_idx, int cnt, int h) {   // device scalars -> pinned host slot, event after the copy
+        POMS_HIP_CHECK(hipMemcpyAsync(host + h, sc + sc_idx, cnt * sizeof(double), hipMemcpyDeviceToHost, st));
+        POMS_HIP_CHECK(hipEventRecord(op->sv_ev[h], st));
+        return 0;
+    }
+    double get(int h, int i = 0) {
+        (void)hipEventSynchronize(op->sv_ev[h]);
+        return host[h + i];
+    }
+    int dot(const double* a, const double* b, int sc_idx) {
+        if (poms_vec_dot(op->ctx, &op->L, a, b, sc + sc_idx, stv)) return 1;
+        return allsum(sc + sc_idx, 1);
+    }
+    int diag_scale_norm(const double* b, double* x, int sc_idx) {   // x = omega b / diag, ||x||^2
+        if (poms_op_diag_scale(op, o->omega, b, x, 1, stv)) return 1;
+        reduce_launch(op->ctx->scratch, (int)op->last_partials, sc + sc_idx, st);
+        return allsum(sc + sc_idx, 1);
+    }
+
+    // damped_jacobi(A, rhs) with x0 = None into buffers {A, B}; the last sweep also
+    // forms x . rhs into sc[dot_idx] (*dot_done = 1), else the caller forms it.
+    int damped_jacobi(const double* rhs, double* A, double* B, int dot_idx, double** out, int* dot_done) {
+        const double tol2 = o->jtol * o->jtol;
+        const int maxit = o->jmaxiter;
+        *dot_done = 0;
+        double *x = A, *xn = B;
+        int pend = 0;   // 0 none, 1 one sweep norm in host slot pend_h, 2 the from-zero pair
+        int pend_h = H_JN, ring = 0, k0;
+        int fz = 0;
+        if (op->ndim == 3 && maxit >= 2 && maxit != 2 && op->form != FORM_STENCIL) (void)poms_op_from_zero_supported(op, &fz);
+        if (fz) {   // sweeps 1, 2 from x = 0 in one pass over rhs
+            if (run(EPI_JACOBI0, rhs, A, rhs, sc + SC_J0 + 1, sc + SC_J0)) return 1;
+            if (allsum(sc + SC_J0, 2) || post(SC_J0, 2, H_J0)) return 1;
+            pend = 2;
+            k0 = 3;
+        } else {
+            if (maxit < 1) { set_error("pcg: jacobi maxiter < 1"); return 1; }
+            if (diag_scale_norm(rhs, A, SC_JN) || post(SC_JN, 1, H_JN)) return 1;
+            pend = 1;
+            pend_h = H_JN;
+            ring = 1;
+            k0 = 2;
+        }
+        auto settle = [&](bool& done, double*& res) {
+            done = false;
+            if (pend == 2) {
+                if (get(H_J0, 0) < tol2) {   // the reference stops after sweep 1: x1 itself
+                    if (poms_op_diag_scale(op, o->omega, rhs, xn, 0, stv)) return 1;
+                    done = true;
+                    res = xn;
+                } else if (get(H_J0, 1) < tol2) {
+                    done = true;
+                    res = x;
+                }
+            } else if (pend == 1 && get(pend_h) < tol2) {
+                done = true;
+                res = x;
+            }
+            pend = 0;
+            return 0;
+        };
+        for (int k = k0; k <= maxit; ++k) {
+            const bool last = k == maxit;
+            int h = -1;
+            if (last) {   // the last sweep's norm cannot change the result: x . rhs instead
+                if (run(EPI_JACOBI, x, xn, rhs, nullptr, sc + dot_idx) || allsum(sc + dot_idx, 1)) return 1;
+            } else {
+                h = H_JN + ring;
+                if (run(EPI_JACOBI, x, xn, rhs, sc + SC_JN + ring, nullptr) || allsum(sc + SC_JN + ring, 1) ||
+                    post(SC_JN + ring, 1, h))
+                    return 1;
+                ring ^= 1;
+            }
+            if (pend) {   // stop test of the previous sweep, read after this one is queued
+                bool done;
+                double* res = nullptr;
+                if (settle(done, res)) return 1;
+                if (done) { *out = res; return 0; }
+            }
+            std::swap(x, xn);
+            if (last) { *dot_done = 1; break; }
+            pend = 1;
+            pend_h = h;
+        }
+        if (pend == 2) {   // maxiter == 2 from zero: sweep 1's test still open
+            bool done;
+            double* res = nullptr;
+            if (settle(done, res)) return 1;
+            if (done) { *out = res; return 0; }
+        }
+        *out = x;
+        return 0;
+    }
+};
+
+}  // namespace
+
+int poms_pcg_jacobi(poms_op* op, poms_comm* comm, const poms_pcg_opts* o, const double* b, double* x, int has_x0,
+                    double* const* work, poms_pcg_info* info, void* stream) {
+    if (!op || !o || !b || !x || !work || !info) { set_error("poms_pcg_jacobi: null argument"); return 1; }
+    for (int i = 0; i < 5; ++i)
+        if (!work[i]) { set_error("poms_pcg_jacobi: null work vector"); return 1; }
+    if (o->maxiter < 0 || o->jmaxiter < 1) { set_error("poms_pcg_jacobi: bad iteration counts"); return 1; }
+    POMS_HIP_CHECK(hipSetDevice(op->ctx->device));
+    if (!op->sv_dev) {
+        POMS_HIP_CHECK(hipMalloc(reinterpret_cast<void**>(&op->sv_dev), SC_N * sizeof(double)));
+        POMS_HIP_CHECK(hipMemset(op->sv_dev, 0, SC_N * sizeof(double)));
+        POMS_HIP_CHECK(hipHostMalloc(reinterpret_cast<void**>(&op->sv_host), 8 * sizeof(double), hipHostMallocDefault));
+        for (hipEvent_t& e : op->sv_ev) POMS_HIP_CHECK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+    }
+    PcgRun R{op, comm, o, as_stream(stream), stream, op->sv_dev, op->sv_host};
+    R.n0 = op->ndim == 3 ? op->L.n[0] : 1;
+    poms_ctx* ctx = op->ctx;
+    const poms_layout* L = &op->L;
+    double *r = work[0], *q = work[1];
+    double* z[3] = {work[2], work[3], work[4]};
+    // x0 = None: x = 0, r = b - A.0 = b exactly; else r = b - A x0
+    if (!has_x0) {
+        if (poms_vec_fill(ctx, L, 0.0, x, stream) || poms_vec_scale(ctx, L, 1.0, b, r, stream)) return 1;
+    } else if (R.run(EPI_RESID, x, r, b, nullptr, nullptr)) {
+        return 1;
+    }
+    if (R.dot(r, r, SC_RR0) || R.post(SC_RR0, 1, H_RR0)) return 1;
+    const double nrmr0 = std::sqrt(R.get(H_RR0));
+    double* s = nullptr;
+    int dd = 0;
+    if (R.damped_jacobi(r, z[0], z[1], SC_SR, &s, &dd)) return 1;
+    if (!dd && R.dot(s, r, SC_SR)) return 1;
+    double* p = s;   // p keeps this buffer; later psolves use the other two
+    double* fa = nullptr;
+    double* fb = nullptr;
+    for (double* c : z)
+        if (c != p) (fa ? fb : fa) = c;
+    int k = 0;
+    double nrmr = nrmr0 * nrmr0;
+    for (k = 1; k <= o->maxiter; ++k) {
+        if (R.run(EPI_APPLYDOT, p, q, p, nullptr, R.sc + SC_PQ) || R.allsum(R.sc + SC_PQ, 1)) return 1;
+        hipLaunchKernelGGL(pcg_scalars_kernel, dim3(1), dim3(64), 0, R.st, R.sc, 0);
+        if (poms_pcg_r_update_dev(ctx, L, R.sc + SC_ALPHA, r, q, R.sc + SC_RR, stream) || R.allsum(R.sc + SC_RR, 1) ||
+            R.post(SC_RR, 1, H_RR))
+            return 1;
+        double* sn = nullptr;
+        if (R.damped_jacobi(r, fa, fb, SC_SRN, &sn, &dd)) return 1;   // queued before the read
+        if (!dd && R.dot(sn, r, SC_SRN)) return 1;
+        nrmr = R.get(H_RR);
+        if (nrmr < o->tol * nrmr0) {   // the reference stops before psolve: that one is discarded
+            if (poms_vec_axpby_dev(ctx, L, R.sc + SC_ONE, x, p, x, stream)) return 1;
+            k -= 1;
+            break;
+        }
+        hipLaunchKernelGGL(pcg_scalars_kernel, dim3(1), dim3(64), 0, R.st, R.sc, 1);
+        if (poms_pcg_xp_update_dev(ctx, L, R.sc + SC_ALPHA2, x, p, sn, stream)) return 1;
+    }
+    if (k > o->maxiter) k = o->maxiter;
+    info->niter = k;
+    info->success = nrmr < o->tol * nrmr0 ? 1 : 0;
+    info->res_norm = std::sqrt(nrmr);
+    POMS_HIP_CHECK(hipGetLastError());
+    return 0;
+}
+
+int poms_op_timing(poms_op* op, int enable, int epilogue, int every, int reserve) {
+    if (!op || every < 1 || reserve < 0) { set_error("poms_op_timing: bad argument"); return 1; }
+    op->timing = enable != 0;
+    if (!op->timing) return 0;   // disabling keeps the record for poms_op_timing_read
+    op->tl_used = 0;
+    op->t_epi = epilogue;
+    op->t_every = every;
+    op->t_seen = 0;
+    POMS_HIP_CHECK(hipSetDevice(op->ctx->device));
+    while (op->tl.size() < (size_t)reserve) {   // create the events now, not inside the timed work
+        poms_op::TimedLaunch t{};
+        POMS_HIP_CHECK(hipEventCreate(&t.e0));
+        POMS_HIP_CHECK(hipEventCreate(&t.e1));
+        op->tl.push_back(t);
+    }
+    return 0;
+}
+
+int poms_op_timing_read(poms_op* op, int epilogue, double* total_ms, int64_t* launches, int64_t* dofs) {
+    if (!op || !total_ms || !launches || !dofs) { set_error("poms_op_timing_read: null argument"); return 1; }
+    double tot = 0.0;
+    int64_t n = 0, d = 0;
+    for (size_t i = 0; i < op->tl_used; ++i) {
+        const auto& t = op->tl[i];
+        if (t.epi != epilogue) continue;
+        POMS_HIP_CHECK(hipEventSynchronize(t.e1));
+        float ms = 0.0f;
+        POMS_HIP_CHECK(hipEventElapsedTime(&ms, t.e0, t.e1));
+        tot += ms;
+        ++n;
+        d += t.ndof;
+    }
+    *total_ms = tot;
+    *launches = n;
+    *dofs = d;
+    return 0;
+}

@@ -65,6 +65,8 @@ def pcg(A, psolve, b, x0=None, tol=1e-6, maxiter=100, verbose=False):
     V = b.space
     if (psolve is damped_jacobi and not verbose and V.lazy_reductions and A.apply_dot_supported
             and A.fused_dot_supported):
+        if _native_ok(A, V):
+            return _pcg_native(A, b, x0, tol, maxiter)
         return _pcg_device(A, b, x0, tol, maxiter)
     ctx, lay = V.ctx, V.layout
     if x0 is None:
@@ -159,6 +161,45 @@ def _pcg_device(A, b, x0, tol, maxiter):
         _pcg_xp_update_dev(V, torch.cat([alpha, beta]), x, p, s_next)
     info = {"niter": k, "success": nrmr < tol * nrmr0, "res_norm": sqrt(nrmr)}
     return x, info
+
+
+def _native_ok(A, V) -> bool:
+    """The whole pcg + damped-Jacobi loop runs in C (poms_pcg_jacobi) unless disabled
+    (POMS_NATIVE_PCG=0), the space is a Cart block (its ghost exchange is the torch
+    transport's) or a distributed space has no native communicator."""
+    import os
+    if os.environ.get("POMS_NATIVE_PCG", "1") == "0" or V.is_cart:
+        return False
+    return not V.is_distributed or V.dist.native is not None
+
+
+def _pcg_native(A, b, x0, tol, maxiter):
+    """pcg(A, damped_jacobi, b, x0, tol, maxiter) as one C call (``poms_pcg_jacobi``):
+    the launches, device scalars and stop tests of :func:`_pcg_device`, bitwise the
+    same iterates, without a Python round trip per launch."""
+    import ctypes as C
+    from . import _lib, runtime as rt
+    V = b.space
+    work = getattr(A, "_pcg_work", None)
+    if work is None or work[0].space is not V:
+        work = A._pcg_work = [V.empty() for _ in range(5)]
+    x = V.zeros() if x0 is None else x0.copy()
+    if x0 is not None:
+        assert x0.shape == (A.shape[0],)
+    d = V.dist if V.is_distributed else None
+    opts = _lib.PcgOpts(float(tol), int(maxiter), 1e-6, 10, OMEGA,
+                        -1 if d is None or d.prev is None else int(d.prev),
+                        -1 if d is None or d.next is None else int(d.next))
+    info = _lib.PcgInfo()
+    ptrs = (C.c_void_p * 5)(*[w._data.data_ptr() for w in work])
+    _lib.call("poms_pcg_jacobi", A._h, d.native.h if d is not None else None,
+              C.byref(opts), rt.ptr(b._data), rt.ptr(x._data), 0 if x0 is None else 1, ptrs, C.byref(info),
+              rt.stream_handle())
+    x._mark_written()
+    for w in work:
+        w._mark_written()
+    A._calls += 1
+    return x, {"niter": info.niter, "success": bool(info.success), "res_norm": info.res_norm}
 
 
 def _vec_dev(V, name, ab, xv, yv, zv):

@@ -662,6 +662,19 @@ class KronOperator:
 
     EPILOGUES = {"apply": 0, "residual": 1, "jacobi": 2, "jacobi_from_zero": 3, "apply_dot": 4}
 
+    def timing(self, enable: bool = True, epilogue: str | None = None, every: int = 1, reserve: int = 0) -> None:
+        """Bracket launches of this operator (any caller, the native pcg loop included)
+        with HIP events on their stream: those of ``epilogue`` (None: all), every
+        ``every``-th; enabling clears the record and pre-creates ``reserve`` event pairs."""
+        _lib.call("poms_op_timing", self._h, 1 if enable else 0, -1 if epilogue is None else self.EPILOGUES[epilogue],
+                  int(every), int(reserve))
+
+    def timing_read(self, epilogue: str):
+        """(seconds, launches, output DOFs) of the recorded launches of one epilogue."""
+        ms, n, d = C.c_double(), C.c_int64(), C.c_int64()
+        _lib.call("poms_op_timing_read", self._h, self.EPILOGUES[epilogue], C.byref(ms), C.byref(n), C.byref(d))
+        return ms.value * 1e-3, n.value, d.value
+
     def kernel_variant(self, epilogue: str) -> int:
         """Variant one launch of ``epilogue`` runs after auto-selection / fall-backs."""
         v = C.c_int()

@@ -318,3 +318,61 @@ def test_damped_jacobi_maxiter2_stops_after_sweep1(gpu, ndim, N, p):
         assert rel(x.reshape(-1), xr) <= 1e-12, frac
         if frac < 1:
             assert rel(x.reshape(-1), (2.0 / 3.0) * bs.reshape(-1) / D) <= 1e-14
+
+
+@pytest.mark.parametrize("ndim,N,p,scale,x0,tol,maxiter", [
+    (3, 20, 3, 1.0, False, 1e-6, 10),      # from-zero sweeps (3D), all iterations
+    (3, 20, 3, 1.0, True, 1e-6, 10),
+    (2, 64, 3, 1.0, False, 1e-6, 10),      # diagonal scaling first (2D)
+    (3, 16, 2, 1e-5, False, 1e-6, 10),     # damped Jacobi stops after a few sweeps
+    (3, 16, 3, 1e-9, False, 1e-6, 10),     # ... after sweep 1 (x1 re-formed)
+    (2, 40, 1, 1e-9, True, 1e-6, 10),
+    (3, 16, 3, 1.0, False, 0.5, 10),       # pcg stops early
+    (3, 12, 2, 1.0, True, 1e-6, 1),
+    (2, 24, 2, 1.0, False, 1e-6, 0),
+])
+def test_native_pcg_matches_python_loop(gpu, monkeypatch, ndim, N, p, scale, x0, tol, maxiter):
+    """poms_pcg_jacobi (the whole pcg + damped-Jacobi loop in C) == the Python device
+    loop, bitwise: same launches, same device scalars, same stop decisions."""
+    from poms_amd import solvers
+    from poms_amd.stencil import KronOperator, StencilVectorSpace
+    M, K = assemble_1d(uniform_knots(p, N), p)
+    n = N + p
+    V = StencilVectorSpace([n] * ndim, [p] * ndim)
+    A = KronOperator.laplace(V, [M] * ndim, [K] * ndim)
+    rng = np.random.default_rng(N + p)
+    b = V.zeros().from_numpy(scale * rng.standard_normal((n,) * ndim))
+    xi = V.zeros().from_numpy(rng.standard_normal((n,) * ndim)) if x0 else None
+    assert solvers._native_ok(A, V)
+    out = {}
+    for native in ("0", "1"):
+        monkeypatch.setenv("POMS_NATIVE_PCG", native)
+        x, info = solvers.pcg(A, solvers.damped_jacobi, b, x0=xi, tol=tol, maxiter=maxiter)
+        out[native] = (x.to_local_numpy(), info)
+    np.testing.assert_array_equal(out["1"][0], out["0"][0])
+    assert out["1"][1]["niter"] == out["0"][1]["niter"]
+    assert out["1"][1]["success"] == out["0"][1]["success"]
+    assert out["1"][1]["res_norm"] == out["0"][1]["res_norm"]
+
+
+def test_op_timing_counts_native_launches(gpu):
+    """poms_op_timing records every operator launch, including the native loop's."""
+    from poms_amd import solvers
+    from poms_amd.stencil import KronOperator, StencilVectorSpace
+    p, N = 3, 16
+    M, K = assemble_1d(uniform_knots(p, N), p)
+    V = StencilVectorSpace([N + p] * 3, [p] * 3)
+    A = KronOperator.laplace(V, [M] * 3, [K] * 3)
+    b = V.zeros().from_numpy(np.ones((N + p,) * 3))
+    A.timing(True)
+    solvers.pcg(A, solvers.damped_jacobi, b, tol=1e-6, maxiter=3)
+    A.timing(False)
+    t, n, d = A.timing_read("jacobi")
+    # 3 + 1 preconditioner calls, each from-zero (1 launch) + 8 sweeps
+    assert n == 4 * 8 and d == n * (N + p) ** 3 and t > 0
+    ta, na, _ = A.timing_read("apply_dot")
+    assert na == 3
+    A.timing(True, "jacobi", every=4, reserve=16)   # a sample of one epilogue
+    solvers.pcg(A, solvers.damped_jacobi, b, tol=1e-6, maxiter=3)
+    assert A.timing_read("jacobi")[1] == 8 and A.timing_read("apply_dot")[1] == 0
+    A.timing(False)
