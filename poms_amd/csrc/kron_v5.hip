@@ -86,9 +86,16 @@ __device__ __forceinline__ void v5_barrier() {
 // aligned layout): one 16-B store per lane, else two 8-B stores.
 // JDOT: the Jacobi sweep also accumulates x_out . b (only the last sweep of a
 // preconditioner call asks for it).
+// Waves per workgroup (= output rows per tile): 16 at p <= 3 (4 waves per SIMD,
+// 128 VGPRs).  p >= 4 needs more registers for its 2p+1 wide windows: 8 waves (2 per
+// SIMD, up to 256 VGPRs); the x tile is then 8 + 2p rows, up to 3 DMAs per wave.
+// (12 waves at 168 VGPRs fit the p = 5 apply but ran 254 us against 185 at 256^3,
+// profiles/r02/configs/kb_p5_waves12.log vs kb_p5_waves8.log.)
+constexpr int v5_waves(int P, int /*EPI*/) { return P <= 3 ? 16 : 8; }
+
 template <int P, int EPI, int D, int MODE = 0, int CP = 0, bool XH = false, bool ST16 = true, bool JDOT = true,
           bool SAME12 = false>
-__global__ void __launch_bounds__(1024, 1)
+__global__ void __launch_bounds__(64 * v5_waves(P, EPI), 1)
 kron_v5_kernel(const double* __restrict__ x, double* __restrict__ y, const double* __restrict__ bvec,
                const double* __restrict__ a0t, const double* __restrict__ b0t,
                const double* __restrict__ a1, const double* __restrict__ b1,
@@ -97,7 +104,7 @@ kron_v5_kernel(const double* __restrict__ x, double* __restrict__ y, const doubl
                const double* __restrict__ rdiag0, const KronGeom g, const ToepConst tc,
                const int H, const double omega) {
     constexpr int W = 2 * P + 1;
-    constexpr int NW = 16;
+    constexpr int NW = v5_waves(P, EPI);
     constexpr int T1 = NW;              // output rows per tile: one per wave
     constexpr int XR = T1 + 2 * P;      // x rows per plane tile
     constexpr int TC = 128;             // lane-columns per tile
@@ -116,6 +123,8 @@ kron_v5_kernel(const double* __restrict__ x, double* __restrict__ y, const doubl
     constexpr int XAUX = (CP & 1) ? 2 : 0, BAUX = (CP & 2) ? 2 : 0;
     constexpr int YAUX = (CP & 16) ? 16 : (CP & 32) ? 17 : (CP & 4) ? 2 : 0;
     constexpr int NWIN = 2 * P + 2;     // columns 2j-P .. 2j+1+P of a lane's pair
+    constexpr int NXM = (XR + NW - 1) / NW;   // most x-row DMAs one wave issues per plane
+    static_assert(NXM >= 2 && (NXM - 1) * NW < XR, "x tile rows vs waves");
     static_assert(D >= 3 || !HASB, "the b ring's wait count assumes x(t) was issued before b(t)");
     typedef double d2 __attribute__((ext_vector_type(2)));
 
@@ -243,7 +252,7 @@ kron_v5_kernel(const double* __restrict__ x, double* __restrict__ y, const doubl
     // storage column of lane-column 0 (pads == P): c0 - H + P
     const int colb = (c0 - H + P) * 8 + 16 * lane;
 
-    // ---- LDS-DMA issue (per wave per plane: x 1 or 2 rows, b 1 row) ----
+    // ---- LDS-DMA issue (per wave per plane: x NXM - 1 or NXM rows, b 1 row) ----
     auto dma_x = [&](int m, int slot) {
         if constexpr (MODE == 2) return;
         const int sp = m + g.pd0;
@@ -256,8 +265,11 @@ kron_v5_kernel(const double* __restrict__ x, double* __restrict__ y, const doubl
             dma16s<2>(rx, lds + XS_OFF + (slot * XR + wv) * TC, ok ? (r0 + wv) * s1 * 8 + colb : 0x7ffffff0, so);
         else
             dma16s<XAUX>(rx, lds + XS_OFF + (slot * XR + wv) * TC, ok ? (r0 + wv) * s1 * 8 + colb : 0x7ffffff0, so);
-        if (wv < XR - NW)
-            dma16s<XAUX>(rx, lds + XS_OFF + (slot * XR + NW + wv) * TC, ok ? (r0 + NW + wv) * s1 * 8 + colb : 0x7ffffff0, so);
+#pragma unroll
+        for (int i = 1; i < NXM; ++i)   // rows wv + i NW: every wave but the last on the tile's x rows
+            if (i < NXM - 1 || wv < XR - (NXM - 1) * NW)
+                dma16s<XAUX>(rx, lds + XS_OFF + (slot * XR + i * NW + wv) * TC,
+                             ok ? (r0 + i * NW + wv) * s1 * 8 + colb : 0x7ffffff0, so);
     };
     auto dma_b = [&](int zo, int slot) {
         const uint32_t so = (uint32_t)(zo + g.pd0) * plane8;
@@ -303,7 +315,7 @@ kron_v5_kernel(const double* __restrict__ x, double* __restrict__ y, const doubl
     for (int i = 0; i < PFX; ++i) dma_x(i < nplanes ? z0 - P + i : -(1 << 20), i);
     if constexpr (HASB) dma_b(zo_of(0), 0);
 
-    const bool xtra = wv < XR - NW;   // this wave issues 2 x DMAs per plane
+    const bool xtra = wv < XR - (NXM - 1) * NW;   // this wave issues NXM x DMAs per plane (else NXM - 1)
     for (int tb = 0; tb < nplanes; tb += NS) {
 #pragma unroll
         for (int q = 0; q < NS; ++q) {
@@ -318,12 +330,12 @@ kron_v5_kernel(const double* __restrict__ x, double* __restrict__ y, const doubl
                 // before it, PFX >= 2).
                 if constexpr (HASB) {
                     if (t == 0) v5_wait_vm<0>();
-                    else if (xtra) v5_wait_vm<2>();
-                    else v5_wait_vm<1>();
+                    else if (xtra) v5_wait_vm<NXM>();
+                    else v5_wait_vm<NXM - 1>();
                 } else {
                     if (t < PFX) v5_wait_vm<0>();
-                    else if (xtra) v5_wait_vm<(PFX - 1) * 2>();
-                    else v5_wait_vm<(PFX - 1) * 1>();
+                    else if (xtra) v5_wait_vm<(PFX - 1) * NXM>();
+                    else v5_wait_vm<(PFX - 1) * (NXM - 1)>();
                 }
                 if constexpr (J0) {
                     // x1 = omega b / diag: each wave scales the rows it DMA'd itself, once, in
@@ -340,8 +352,8 @@ kron_v5_kernel(const double* __restrict__ x, double* __restrict__ y, const doubl
                     }
                     double* xs0 = lds + XS_OFF + (t % D) * XR * TC + 2 * lane;
 #pragma unroll
-                    for (int r = 0; r < 2; ++r) {
-                        if (r == 1 && !xtra) break;
+                    for (int r = 0; r < NXM; ++r) {
+                        if (r == NXM - 1 && !xtra) break;
                         const int qr = wv + r * NW;
                         d2 v = *(const d2*)(xs0 + qr * TC);
                         if (tp) {
@@ -631,7 +643,7 @@ static int v5_launch_t2(const KronPtrs& p, const KronGeom& g, const ToepConst& t
         return 1;
     }
     const int nblk = g.tiles2 * g.tiles1 * g.nchunks;
-    hipLaunchKernelGGL((kron_v5_kernel<P, EPI, D, MODE, CP, XH, ST16, JDOT, SAME12>), dim3(nblk), dim3(1024), 0, st, p.x,
+    hipLaunchKernelGGL((kron_v5_kernel<P, EPI, D, MODE, CP, XH, ST16, JDOT, SAME12>), dim3(nblk), dim3(64 * v5_waves(P, EPI)), 0, st, p.x,
                        p.y, p.b, p.a0t, p.b0t, p.a1, p.b1, p.a2, p.b2, p.partial, p.partial2, p.rdiag0, g, tc, H, omega);
     return 0;
 }
@@ -753,13 +765,17 @@ int kron_v5_launch(int pmax, int epi, const KronPtrs& p, const KronGeom& g, cons
         set_error("v5 diag mode: bad mode / epilogue");
         return 1;
     }
-    switch (pmax) {   // p >= 4 does not fit 128 VGPRs without spilling: the host runs 7 / 9
+    switch (pmax) {
         case 1: return v5_launch_p<1>(epi, p, g, tc, H, omega, st);
         case 2: return v5_launch_p<2>(epi, p, g, tc, H, omega, st);
         case 3: return v5_launch_p<3>(epi, p, g, tc, H, omega, st);
+        case 4: return v5_launch_p<4>(epi, p, g, tc, H, omega, st);   // 8-wave tiles
+        case 5: return v5_launch_p<5>(epi, p, g, tc, H, omega, st);
     }
-    set_error("v5: pmax must be in 1..3");
+    set_error("v5: pmax must be in 1..5");
     return 1;
 }
+
+int kron_v5_rows(int pmax, int epi) { return v5_waves(pmax, epi); }
 
 }  // namespace poms

@@ -22,6 +22,7 @@ int kron_v4_launch(int pmax, bool is3d, int form, int epi, const KronPtrs& p, co
 int kron_v5_launch(int pmax, int epi, const KronPtrs& p, const KronGeom& g, const ToepConst& tc, int H,
                    double omega, hipStream_t st, int diag_mode);
 void kron_v5_tile(int pmax, bool aligned, int* H, int* TO);
+int kron_v5_rows(int pmax, int epi);
 int kron_tile_rows();
 int kron_tile_cols();
 int vec_launch(int op, const RowGeom& g, double a, double b, const double* x, const double* y,
@@ -557,7 +558,7 @@ static int auto_chunk(int nz, int tiles, int p, double slots = 512.0) {
 // neighbour -- then (ghost_corners) the operator runs v3.
 static bool v5_ok(const poms_op* o) {
     const int64_t bytes = (int64_t)(o->L.n[0] + 2 * o->L.pads[0]) * row_geom(&o->L).s0 * 8;
-    return o->ndim == 3 && o->form == FORM_SUM && o->v2_ok && o->pmax <= 3 && bytes < 0x7ffffff0LL &&
+    return o->ndim == 3 && o->form == FORM_SUM && o->v2_ok && o->pmax <= 5 && bytes < 0x7ffffff0LL &&
            !(o->ghost_corners && (o->pmax & 1));
 }
 
@@ -579,7 +580,7 @@ static int op_geom(poms_op* o, int64_t zb, int64_t ze, KronGeom& g, int v = -1, 
     g.pd0 = r.pd0; g.pd1 = r.pd1; g.pd2 = r.pd2;
     g.g0 = (int)o->g0;
     g.tiles2 = (int)((o->L.n[2] + kron_tile_cols() - 1) / kron_tile_cols());
-    const int trows = v == 10 ? 16 : kron_tile_rows();
+    const int trows = v == 10 ? kron_v5_rows(o->pmax, epi) : kron_tile_rows();
     g.tiles1 = (int)((o->L.n[1] + trows - 1) / trows);
     g.tout = v == 10 ? v5_to : (o->tout > 0 ? o->tout : 64 - 2 * o->pmax);
     if (v >= 4) g.tiles2 = (int)((o->L.n[2] + g.tout - 1) / g.tout);
@@ -650,7 +651,8 @@ static int resolve_variant(const poms_op* o, int epi) {
     if (v == 8) {
         const bool plain = epi == EPI_APPLY || epi == EPI_RESID || epi == EPI_JACOBI;
         if (o->ndim == 3 && v5_ok(o) && epi != EPI_JACOBI0)
-            v = 10;   // v5 (p <= 3): kernel_bench at 515^3, p = 3
+            v = 10;   // v5: kernel_bench at 515^3 p = 3; 8-wave tiles at 256^3 p = 4, 5
+                      // (profiles/r02/configs/kb_p5_waves8.log: apply 231 -> 185 us at p = 5)
         else if (o->ndim == 3)
             v = ((epi == EPI_APPLY && o->pmax >= 3) || (plain && o->pmax >= 4)) ? 7 : 9;
         else

@@ -27,7 +27,7 @@ if [[ "$what" == "bench" || "$what" == "all" ]]; then
 fi
 if [[ "$what" == "prof" || "$what" == "all" ]]; then
   export TMPDIR=/tmp
-  (cd /tmp && timeout -k 10 900 rocprofv3 --kernel-trace --stats -d "$OUT/prof" -o run -- \
+  (cd /tmp && timeout -k 10 900 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/prof" -o run -- \
       python3 "$ROOT/bench.py" --steps 1 --warmup 0 --no-cpu-baseline --kron-reps 5 "$@") > "$OUT/prof.log" 2>&1
   rc=$?; echo "rocprof rc=$rc"; tail -3 "$OUT/prof.log"
   [[ $rc -eq 0 ]] || stop "rocprof failed" $rc
