@@ -87,11 +87,12 @@ __device__ __forceinline__ void v5_barrier() {
 // JDOT: the Jacobi sweep also accumulates x_out . b (only the last sweep of a
 // preconditioner call asks for it).
 // Waves per workgroup (= output rows per tile): 16 at p <= 3 (4 waves per SIMD,
-// 128 VGPRs).  p >= 4 needs more registers for its 2p+1 wide windows: 8 waves (2 per
-// SIMD, up to 256 VGPRs); the x tile is then 8 + 2p rows, up to 3 DMAs per wave.
+// 128 VGPRs).  p >= 4 needs more registers for its 2p+1 wide windows, and the
+// two-sweeps-from-zero epilogue for its x1 scaling: 8 waves (2 per SIMD, up to 256
+// VGPRs); the x tile is then 8 + 2p rows, up to 3 DMAs per wave.
 // (12 waves at 168 VGPRs fit the p = 5 apply but ran 254 us against 185 at 256^3,
 // profiles/r02/configs/kb_p5_waves12.log vs kb_p5_waves8.log.)
-constexpr int v5_waves(int P, int /*EPI*/) { return P <= 3 ? 16 : 8; }
+constexpr int v5_waves(int P, int EPI) { return (P <= 3 && EPI != EPI_JACOBI0) ? 16 : 8; }
 
 template <int P, int EPI, int D, int MODE = 0, int CP = 0, bool XH = false, bool ST16 = true, bool JDOT = true,
           bool SAME12 = false>

@@ -239,7 +239,7 @@ def test_jacobi_from_zero(gpu, ndim, cells, p, variant):
     n = [N + p for N in cells]
     V = _space(n, [p] * ndim)
     A = KronOperator.laplace(V, [f[0] for f in F], [f[1] for f in F])
-    A.set_variant(variant)   # 10: v5 for p <= 3, falls back to 9 above
+    A.set_variant(variant)   # 10: v5, 8-wave tiles for the sweeps from zero
     assert A.from_zero_supported
     b = V.zeros().from_numpy(rng.standard_normal(n))
     x1, x2 = V.zeros(), V.zeros()
@@ -466,7 +466,7 @@ def test_v5_jacobi_from_zero_coverage(gpu, p, cells, align):
     V = StencilVectorSpace(n, [p] * 3, align=align)
     A = KronOperator.laplace(V, [f[0] for f in F], [f[1] for f in F])
     A.set_variant(10)
-    assert A.kernel_variant("jacobi_from_zero") == (10 if p <= 2 else 9)
+    assert A.kernel_variant("jacobi_from_zero") == 10   # 8-wave tiles at every p
     b = V.zeros().from_numpy(rng.standard_normal(n))
     x1, x2 = V.zeros(), V.zeros()
     n1 = A.diag_scale(b, x1, 2.0 / 3.0, want_norm=True)
