@@ -43,8 +43,8 @@ KERNEL_NAMES = {10: "kron_v5_kernel", 9: "kron_v3_kernel(flat)", 7: "kron_v4_ker
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=3)
-    ap.add_argument("--warmup", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=None, help="timed V-cycles (default 3 in 3D, 20 in 2D)")
+    ap.add_argument("--warmup", type=int, default=None, help="untimed V-cycles (default 1 in 3D, 5 in 2D)")
     ap.add_argument("--ndim", type=int, default=3, choices=(2, 3))
     ap.add_argument("--p", type=int, default=3)
     ap.add_argument("--cells", type=int, default=None, help="cells per axis (default 512 in 3D, 1024 in 2D)")
@@ -64,6 +64,10 @@ def parse():
                          "(FETCH_SIZE x2 + WRITE_SIZE per launch) used for roofline.traffic; used only "
                          "when its recorded p and kernel variant are this run's")
     a = ap.parse_args()
+    if a.steps is None:
+        a.steps = 3 if a.ndim == 3 else 20
+    if a.warmup is None:
+        a.warmup = 1 if a.ndim == 3 else 5
     if a.cells is None:
         a.cells = 512 if a.ndim == 3 else 1024
     if a.flush_mall is None:

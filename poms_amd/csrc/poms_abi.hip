@@ -3,6 +3,7 @@
 #include "../../include/poms_hip.h"
 
 #include <algorithm>
+#include <atomic>
 #include <cmath>
 #include <cstdlib>
 #include <cstring>
@@ -45,7 +46,8 @@ int stencil_launch(int epi, const StencilGeom& g, const double* coef, const doub
                    const double* b, double omega, double* partial, double* partial2, int max_blocks,
                    hipStream_t st, int* nblk_out);
 int transfer_pass_launch(bool restrict_dir, int ncm, const AxisPass& ps, const double* Pm,
-                         const double* in, double* out, hipStream_t st);
+                         const double* in, double* out, hipStream_t st, double* part);
+int transfer_split_scratch(int ncm, const AxisPass& ps);
 int transfer_band_launch(bool restrict_dir, const AxisPass& ps, const double* band, const int* lo, int w,
                          const double* in, double* out, hipStream_t st);
 
@@ -144,6 +146,8 @@ struct poms_transfer {
     int *jlo[3]{}, *ilo[3]{};
     int wP[3]{}, wR[3]{};
     double *t0 = nullptr, *t1 = nullptr;
+    double* part = nullptr;   // split-axis restriction partials (few lines)
+    int64_t part_n = 0;
 };
 
 struct poms_ksolve {
@@ -1124,7 +1128,7 @@ int poms_transfer_create(poms_ctx* ctx, int ndim, const poms_layout* fine, int64
 int poms_transfer_destroy(poms_transfer* t) {
     if (!t) return 0;
     for (double* p : {t->Pm[0], t->Pm[1], t->Pm[2], t->t0, t->t1, t->Pb[0], t->Pb[1], t->Pb[2], t->Rb[0],
-                      t->Rb[1], t->Rb[2]})
+                      t->Rb[1], t->Rb[2], t->part})
         if (p) (void)hipFree(p);
     for (int* p : {t->jlo[0], t->jlo[1], t->jlo[2], t->ilo[0], t->ilo[1], t->ilo[2]})
         if (p) (void)hipFree(p);
@@ -1134,9 +1138,26 @@ int poms_transfer_destroy(poms_transfer* t) {
 
 // one axis pass of a transfer: dense-P kernels for small coarse extents, banded
 // gather kernels otherwise
-static int tpass(const poms_transfer* t, bool restrict_dir, int d, const AxisPass& ps, const double* in,
+static int tpass(poms_transfer* t, bool restrict_dir, int d, const AxisPass& ps, const double* in,
                  double* out, hipStream_t st) {
-    if (!t->banded) return transfer_pass_launch(restrict_dir, t->ncm, ps, t->Pm[d], in, out, st);
+    if (!t->banded) {
+        double* part = nullptr;
+        if (restrict_dir) {   // split-axis partials (few lines): a buffer grown on first use
+            const int64_t need = transfer_split_scratch(t->ncm, ps);
+            if (need > t->part_n) {
+                if (t->part) (void)hipFree(t->part);
+                t->part = nullptr;
+                t->part_n = 0;
+                if (hipMalloc(reinterpret_cast<void**>(&t->part), need * sizeof(double)) != hipSuccess) {
+                    set_error("transfer: partial-sum buffer allocation failed");
+                    return 1;
+                }
+                t->part_n = need;
+            }
+            part = t->part;
+        }
+        return transfer_pass_launch(restrict_dir, t->ncm, ps, t->Pm[d], in, out, st, part);
+    }
     return restrict_dir ? transfer_band_launch(true, ps, t->Rb[d], t->ilo[d], t->wR[d], in, out, st)
                         : transfer_band_launch(false, ps, t->Pb[d], t->jlo[d], t->wP[d], in, out, st);
 }
@@ -1459,23 +1480,47 @@ struct PcgRun {
         return poms_op_run_reduce2(op, epi, o->omega, x, y, b, 0, n0, 0, 0, nrm, dot, 0, stv);
     }
     int allsum(double* d, int cnt) { return comm ? poms_allreduce_sum(comm, d, cnt, stv, 1) : 0; }
+    // A value the host reads: one rank -- the reduction kernel writes it straight
+    // into the pinned (coherent, device-mapped) host slot, armed with a sentinel the
+    // host spins on (~1-2 us after the kernel instead of an event wake-up, ~15 us:
+    // profiles/r02/sync_probe.log); with a communicator -- device scalar,
+    // all-reduce, copy and event.
+    bool direct() const { return comm == nullptr; }
+    double* hdst(int sc_idx, int h) { return direct() ? host + h : sc + sc_idx; }
+    void arm(int h, int cnt) {
+        if (!direct()) return;
+        for (int i = 0; i < cnt; ++i) reinterpret_cast<volatile double*>(host)[h + i] = -1.0;   // norms are >= 0
+    }
     int post(int sc_idx, int cnt, int h) {   // device scalars -> pinned host slot, event after the copy
+        if (direct()) return 0;
         POMS_HIP_CHECK(hipMemcpyAsync(host + h, sc + sc_idx, cnt * sizeof(double), hipMemcpyDeviceToHost, st));
         POMS_HIP_CHECK(hipEventRecord(op->sv_ev[h], st));
         return 0;
     }
     double get(int h, int i = 0) {
-        (void)hipEventSynchronize(op->sv_ev[h]);
-        return host[h + i];
+        if (!direct()) {
+            (void)hipEventSynchronize(op->sv_ev[h]);
+            return host[h + i];
+        }
+        const volatile double* v = reinterpret_cast<const volatile double*>(host) + h + i;
+        for (long n = 1; *v == -1.0; ++n) {
+            __builtin_ia32_pause();
+            if ((n & 4095) == 0 && hipStreamQuery(st) != hipErrorNotReady) {   // stream drained (or failed)
+                std::atomic_thread_fence(std::memory_order_seq_cst);
+                if (*v == -1.0) return std::nan("");   // never written: the launch failed
+            }
+        }
+        std::atomic_thread_fence(std::memory_order_acquire);
+        return *v;
     }
-    int dot(const double* a, const double* b, int sc_idx) {
-        if (poms_vec_dot(op->ctx, &op->L, a, b, sc + sc_idx, stv)) return 1;
-        return allsum(sc + sc_idx, 1);
+    int dot(const double* a, const double* b, double* dst) {
+        if (poms_vec_dot(op->ctx, &op->L, a, b, dst, stv)) return 1;
+        return allsum(dst, 1);
     }
-    int diag_scale_norm(const double* b, double* x, int sc_idx) {   // x = omega b / diag, ||x||^2
+    int diag_scale_norm(const double* b, double* x, double* dst) {   // x = omega b / diag, ||x||^2
         if (poms_op_diag_scale(op, o->omega, b, x, 1, stv)) return 1;
-        reduce_launch(op->ctx->scratch, (int)op->last_partials, sc + sc_idx, st);
-        return allsum(sc + sc_idx, 1);
+        reduce_launch(op->ctx->scratch, (int)op->last_partials, dst, st);
+        return allsum(dst, 1);
     }
 
     // damped_jacobi(A, rhs) with x0 = None into buffers {A, B}; the last sweep also
@@ -1490,13 +1535,15 @@ struct PcgRun {
         int fz = 0;
         if (op->ndim == 3 && maxit >= 2 && maxit != 2 && op->form != FORM_STENCIL) (void)poms_op_from_zero_supported(op, &fz);
         if (fz) {   // sweeps 1, 2 from x = 0 in one pass over rhs
-            if (run(EPI_JACOBI0, rhs, A, rhs, sc + SC_J0 + 1, sc + SC_J0)) return 1;
-            if (allsum(sc + SC_J0, 2) || post(SC_J0, 2, H_J0)) return 1;
+            arm(H_J0, 2);
+            if (run(EPI_JACOBI0, rhs, A, rhs, hdst(SC_J0 + 1, H_J0 + 1), hdst(SC_J0, H_J0))) return 1;
+            if (allsum(hdst(SC_J0, H_J0), 2) || post(SC_J0, 2, H_J0)) return 1;
             pend = 2;
             k0 = 3;
         } else {
             if (maxit < 1) { set_error("pcg: jacobi maxiter < 1"); return 1; }
-            if (diag_scale_norm(rhs, A, SC_JN) || post(SC_JN, 1, H_JN)) return 1;
+            arm(H_JN, 1);
+            if (diag_scale_norm(rhs, A, hdst(SC_JN, H_JN)) || post(SC_JN, 1, H_JN)) return 1;
             pend = 1;
             pend_h = H_JN;
             ring = 1;
@@ -1527,7 +1574,8 @@ struct PcgRun {
                 if (run(EPI_JACOBI, x, xn, rhs, nullptr, sc + dot_idx) || allsum(sc + dot_idx, 1)) return 1;
             } else {
                 h = H_JN + ring;
-                if (run(EPI_JACOBI, x, xn, rhs, sc + SC_JN + ring, nullptr) || allsum(sc + SC_JN + ring, 1) ||
+                arm(h, 1);
+                if (run(EPI_JACOBI, x, xn, rhs, hdst(SC_JN + ring, h), nullptr) || allsum(hdst(SC_JN + ring, h), 1) ||
                     post(SC_JN + ring, 1, h))
                     return 1;
                 ring ^= 1;
@@ -1566,7 +1614,10 @@ int poms_pcg_jacobi(poms_op* op, poms_comm* comm, const poms_pcg_opts* o, const 
     if (!op->sv_dev) {
         POMS_HIP_CHECK(hipMalloc(reinterpret_cast<void**>(&op->sv_dev), SC_N * sizeof(double)));
         POMS_HIP_CHECK(hipMemset(op->sv_dev, 0, SC_N * sizeof(double)));
-        POMS_HIP_CHECK(hipHostMalloc(reinterpret_cast<void**>(&op->sv_host), 8 * sizeof(double), hipHostMallocDefault));
+        // coherent (fine-grained) and device-mapped: reduction kernels write the
+        // host-read norms straight into it
+        POMS_HIP_CHECK(hipHostMalloc(reinterpret_cast<void**>(&op->sv_host), 8 * sizeof(double),
+                                     hipHostMallocMapped | hipHostMallocCoherent));
         for (hipEvent_t& e : op->sv_ev) POMS_HIP_CHECK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
     }
     PcgRun R{op, comm, o, as_stream(stream), stream, op->sv_dev, op->sv_host};
@@ -1581,12 +1632,13 @@ int poms_pcg_jacobi(poms_op* op, poms_comm* comm, const poms_pcg_opts* o, const 
     } else if (R.run(EPI_RESID, x, r, b, nullptr, nullptr)) {
         return 1;
     }
-    if (R.dot(r, r, SC_RR0) || R.post(SC_RR0, 1, H_RR0)) return 1;
+    R.arm(H_RR0, 1);
+    if (R.dot(r, r, R.hdst(SC_RR0, H_RR0)) || R.post(SC_RR0, 1, H_RR0)) return 1;
     const double nrmr0 = std::sqrt(R.get(H_RR0));
     double* s = nullptr;
     int dd = 0;
     if (R.damped_jacobi(r, z[0], z[1], SC_SR, &s, &dd)) return 1;
-    if (!dd && R.dot(s, r, SC_SR)) return 1;
+    if (!dd && R.dot(s, r, R.sc + SC_SR)) return 1;
     double* p = s;   // p keeps this buffer; later psolves use the other two
     double* fa = nullptr;
     double* fb = nullptr;
@@ -1597,12 +1649,13 @@ int poms_pcg_jacobi(poms_op* op, poms_comm* comm, const poms_pcg_opts* o, const 
     for (k = 1; k <= o->maxiter; ++k) {
         if (R.run(EPI_APPLYDOT, p, q, p, nullptr, R.sc + SC_PQ) || R.allsum(R.sc + SC_PQ, 1)) return 1;
         hipLaunchKernelGGL(pcg_scalars_kernel, dim3(1), dim3(64), 0, R.st, R.sc, 0);
-        if (poms_pcg_r_update_dev(ctx, L, R.sc + SC_ALPHA, r, q, R.sc + SC_RR, stream) || R.allsum(R.sc + SC_RR, 1) ||
-            R.post(SC_RR, 1, H_RR))
+        R.arm(H_RR, 1);
+        if (poms_pcg_r_update_dev(ctx, L, R.sc + SC_ALPHA, r, q, R.hdst(SC_RR, H_RR), stream) ||
+            R.allsum(R.hdst(SC_RR, H_RR), 1) || R.post(SC_RR, 1, H_RR))
             return 1;
         double* sn = nullptr;
         if (R.damped_jacobi(r, fa, fb, SC_SRN, &sn, &dd)) return 1;   // queued before the read
-        if (!dd && R.dot(sn, r, SC_SRN)) return 1;
+        if (!dd && R.dot(sn, r, R.sc + SC_SRN)) return 1;
         nrmr = R.get(H_RR);
         if (nrmr < o->tol * nrmr0) {   // the reference stops before psolve: that one is discarded
             if (poms_vec_axpby_dev(ctx, L, R.sc + SC_ONE, x, p, x, stream)) return 1;
