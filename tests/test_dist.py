@@ -134,16 +134,20 @@ def test_cart_distribution_grid():
         CartDistribution((3, 8), (4, 1), 3)   # 3 points over 4 ranks: rank 3 owns none
 
 
-@pytest.mark.parametrize("dims", ["2x2x1", "1x2x2", "2x1x2", "2x2"])
+@pytest.mark.parametrize("dims", ["2x2x1", "1x2x2", "2x1x2", "2x2", "2x2x2"])
 def test_four_rank_cart_exchange_and_block_apply_cpu(dims):
-    _launch("cart_cpu", world=4, extra_env={"POMS_TEST_CART_DIMS": dims})
+    """4 ranks (8 for 2x2x2: the triple corner of every interior block)."""
+    world = int(np.prod([int(v) for v in dims.split("x")]))
+    _launch("cart_cpu", world=world, extra_env={"POMS_TEST_CART_DIMS": dims})
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("dims", ["2x2x1", "1x2x2", "2x2"])
+@pytest.mark.parametrize("dims", ["2x2x1", "1x2x2", "2x2", "2x2x2"])
 def test_four_rank_cart_operator_and_vcycle_gpu(dims):
-    """spl Cart over a 2x2 process grid (axes 0/1, axes 1/2, and 2D): device
-    operator, sweeps, reductions, transfer and the V-cycle against the oracle."""
+    """spl Cart over a 2x2 process grid (axes 0/1, axes 1/2, and 2D) and 2x2x2 (8
+    ranks on one GPU): device operator, sweeps, reductions, transfer and the
+    V-cycle against the oracle."""
     import torch
     assert torch.cuda.device_count() >= 1, "GPU test selected but no GPU visible"
-    _launch("cart_gpu", world=4, extra_env={"POMS_TEST_CART_DIMS": dims})
+    world = int(np.prod([int(v) for v in dims.split("x")]))
+    _launch("cart_gpu", world=world, timeout=600, extra_env={"POMS_TEST_CART_DIMS": dims})
