@@ -87,12 +87,15 @@ __device__ __forceinline__ void v5_barrier() {
 // JDOT: the Jacobi sweep also accumulates x_out . b (only the last sweep of a
 // preconditioner call asks for it).
 // Waves per workgroup (= output rows per tile): 16 at p <= 3 (4 waves per SIMD,
-// 128 VGPRs).  p >= 4 needs more registers for its 2p+1 wide windows, and the
-// two-sweeps-from-zero epilogue for its x1 scaling: 8 waves (2 per SIMD, up to 256
-// VGPRs); the x tile is then 8 + 2p rows, up to 3 DMAs per wave.
+// 128 VGPRs).  p >= 4 needs more registers for its 2p+1 wide windows: 8 waves (2
+// per SIMD, up to 256 VGPRs); the x tile is then 8 + 2p rows, up to 3 DMAs per
+// wave.  The two-sweeps-from-zero build fits 16 waves at p = 3 once its x1
+// scaling happens in place in the ring and its two sums live in LDS (930 vs 945 us
+// for v3 at 515^3); at p <= 2 it keeps 8 waves (256^3 p = 2: 16 waves 154 us, 8
+// waves 136, v3 135-146; profiles/r02/j0_16wave/).
 // (12 waves at 168 VGPRs fit the p = 5 apply but ran 254 us against 185 at 256^3,
 // profiles/r02/configs/kb_p5_waves12.log vs kb_p5_waves8.log.)
-constexpr int v5_waves(int P, int EPI) { return (P <= 3 && EPI != EPI_JACOBI0) ? 16 : 8; }
+constexpr int v5_waves(int P, int EPI) { return (P == 3 || (P < 3 && EPI != EPI_JACOBI0)) ? 16 : 8; }
 
 template <int P, int EPI, int D, int MODE = 0, int CP = 0, bool XH = false, bool ST16 = true, bool JDOT = true,
           bool SAME12 = false>
@@ -143,7 +146,10 @@ kron_v5_kernel(const double* __restrict__ x, double* __restrict__ y, const doubl
     constexpr int RS_OFF = RCI_OFF + (RCIL ? T1 * TC : 0);
     constexpr int D2_OFF = RS_OFF + (J0 ? XR * TC : 0);
     constexpr int D1_OFF = D2_OFF + (J0 ? 2 * TC : 0);   // J0: axis-1 diagonal entries of the x-tile rows
-    constexpr int LDS_N = D1_OFF + (J0 ? 2 * XR : 0);
+    // J0: per-lane running sums (||dr_2||^2, ||x1||^2) in LDS, not VGPRs: the 4
+    // VGPRs they would pin for the whole march are what p = 3 lacks at 16 waves
+    constexpr int JS_OFF = (D1_OFF + (J0 ? 2 * XR : 0) + 1) & ~1;
+    constexpr int LDS_N = JS_OFF + (J0 ? 2 * NW * 64 : 0);
     __shared__ __attribute__((aligned(16))) double lds[LDS_N];
 
     // SAME12: axis 2's Toeplitz rows equal axis 1's bitwise (one knot vector on both
@@ -252,6 +258,15 @@ kron_v5_kernel(const double* __restrict__ x, double* __restrict__ y, const doubl
     auto zo_of = [&](int t) { return max(z0 - 2 * P + t, z0); };
     // storage column of lane-column 0 (pads == P): c0 - H + P
     const int colb = (c0 - H + P) * 8 + 16 * lane;
+    // Lane-columns no output point reads are not fetched: their voffset is pushed out
+    // of the buffer range (+2^31; arrays are < 2 GiB), so the DMA moves no bytes.  x
+    // needs the tile's columns H-P .. H+TO+P-1, b (and x_in, and the y stores) only
+    // the output columns H .. H+TO-1: on the aligned layout that drops the two
+    // half-lines of halo each b row fetched (8 of 64 lanes) and a quarter-line at
+    // each end of every x row.
+    // (J0 keeps every lane: the trim's extra VGPR makes its p = 3 build spill)
+    const uint32_t colbx = (uint32_t)colb + ((J0 || (2 * lane + 1 >= H - P && 2 * lane < H + TO + P)) ? 0u : 0x80000000u);
+    const uint32_t colbb = (uint32_t)colb + ((2 * lane + 1 >= H && 2 * lane < H + TO) ? 0u : 0x80000000u);
 
     // ---- LDS-DMA issue (per wave per plane: x NXM - 1 or NXM rows, b 1 row) ----
     auto dma_x = [&](int m, int slot) {
@@ -263,19 +278,20 @@ kron_v5_kernel(const double* __restrict__ x, double* __restrict__ y, const doubl
         const uint32_t so = ok ? (uint32_t)sp * plane8 : 0u;
         // x-tile row q = storage row r0 + q
         if ((CP & 8) && wv >= 2 * P)   // a row only this tile reads: stream it
-            dma16s<2>(rx, lds + XS_OFF + (slot * XR + wv) * TC, ok ? (r0 + wv) * s1 * 8 + colb : 0x7ffffff0, so);
+            dma16s<2>(rx, lds + XS_OFF + (slot * XR + wv) * TC, ok ? (int)((uint32_t)((r0 + wv) * s1 * 8) + colbx) : 0x7ffffff0, so);
         else
-            dma16s<XAUX>(rx, lds + XS_OFF + (slot * XR + wv) * TC, ok ? (r0 + wv) * s1 * 8 + colb : 0x7ffffff0, so);
+            dma16s<XAUX>(rx, lds + XS_OFF + (slot * XR + wv) * TC, ok ? (int)((uint32_t)((r0 + wv) * s1 * 8) + colbx) : 0x7ffffff0, so);
 #pragma unroll
         for (int i = 1; i < NXM; ++i)   // rows wv + i NW: every wave but the last on the tile's x rows
             if (i < NXM - 1 || wv < XR - (NXM - 1) * NW)
                 dma16s<XAUX>(rx, lds + XS_OFF + (slot * XR + i * NW + wv) * TC,
-                             ok ? (r0 + i * NW + wv) * s1 * 8 + colb : 0x7ffffff0, so);
+                             ok ? (int)((uint32_t)((r0 + i * NW + wv) * s1 * 8) + colbx) : 0x7ffffff0, so);
     };
     auto dma_b = [&](int zo, int slot) {
         const uint32_t so = (uint32_t)(zo + g.pd0) * plane8;
-        dma16s<BAUX>(rbv, lds + BS_OFF + (slot * T1 + wv) * TC, (orow + P) * s1 * 8 + colb, so);
-        if constexpr (XIN) dma16s<BAUX>(rx, lds + XI_OFF + (slot * T1 + wv) * TC, (orow + P) * s1 * 8 + colb, so);
+        const int vob = (int)((uint32_t)((orow + P) * s1 * 8) + colbb);
+        dma16s<BAUX>(rbv, lds + BS_OFF + (slot * T1 + wv) * TC, vob, so);
+        if constexpr (XIN) dma16s<BAUX>(rx, lds + XI_OFF + (slot * T1 + wv) * TC, vob, so);
     };
 
     double acc[NS][2];
@@ -298,6 +314,7 @@ kron_v5_kernel(const double* __restrict__ x, double* __restrict__ y, const doubl
     if constexpr (J0) {
         for (int e = tid; e < XR * TC; e += NW * 64)
             lds[RS_OFF + e] = j0_scale(e / TC, e % TC, tc.t0a[0], tc.t0b[0]);
+        *(d2*)(lds + JS_OFF + 2 * tid) = d2{0.0, 0.0};
         __syncthreads();
     }
     if constexpr (RCIL) {
@@ -525,14 +542,16 @@ kron_v5_kernel(const double* __restrict__ x, double* __restrict__ y, const doubl
                         sc[0] = j0_scale(wv + P, 2 * lane, d0a, d0b);
                         sc[1] = j0_scale(wv + P, 2 * lane + 1, d0a, d0b);
                     }
+                    d2 js = *(const d2*)(lds + JS_OFF + 2 * tid);   // this lane's own slot
 #pragma unroll
                     for (int e = 0; e < 2; ++e) {
                         const double x1 = xin[e];
                         const double dr = fma(-vo[e], sc[e], x1);
                         outv[e] = x1 + dr;
-                        nrm = ok[e] ? fma(dr, dr, nrm) : nrm;      // ||dr_2||^2
-                        dotp = ok[e] ? fma(x1, x1, dotp) : dotp;   // ||x1||^2 = ||dr_1||^2
+                        js[0] = ok[e] ? fma(dr, dr, js[0]) : js[0];   // ||dr_2||^2
+                        js[1] = ok[e] ? fma(x1, x1, js[1]) : js[1];   // ||x1||^2 = ||dr_1||^2
                     }
+                    *(d2*)(lds + JS_OFF + 2 * tid) = js;
                 } else {
                     const d2 bv = *(const d2*)(lds + BS_OFF + ((t & 1) * T1 + wv) * TC + 2 * lane);
                     if constexpr (EPI == EPI_RESID) {
@@ -593,6 +612,11 @@ kron_v5_kernel(const double* __restrict__ x, double* __restrict__ y, const doubl
         }
     }
     v5_wait_vm<0>();  // no LDS-DMA may outlive the workgroup
+    if constexpr (J0) {
+        const d2 js = *(const d2*)(lds + JS_OFF + 2 * tid);
+        nrm = js[0];
+        dotp = js[1];
+    }
 
     if constexpr (JAC || APD || J0) {
         if (partial != nullptr) {
@@ -667,8 +691,11 @@ static int v5_launch_t1(const KronPtrs& p, const KronGeom& g, const ToepConst& t
 template <int P, int EPI, int D, int MODE = 0, int CP = 0, bool XH = false>
 static int v5_launch_t(const KronPtrs& p, const KronGeom& g, const ToepConst& tc, int H, double omega,
                        hipStream_t st) {
+    // (the p = 3 two-sweeps-from-zero build always stores 8-B halves: with the 16-B
+    // store's aligned register quad it spills at 16 waves; so does its build with
+    // distinct axis-1 / axis-2 Toeplitz rows, which resolve_variant leaves to v3)
     const bool st16 = ((reinterpret_cast<uintptr_t>(p.y) + 8 * (int64_t)(g.pd2 - H)) & 15) == 0 &&
-                      g.s1 % 2 == 0 && g.s0 % 2 == 0;
+                      g.s1 % 2 == 0 && g.s0 % 2 == 0 && !(EPI == EPI_JACOBI0 && P == 3);
     // the Jacobi x_in history does not fit the VGPRs beside the split stores: the
     // unaligned build DMAs x_in next to b instead
     constexpr bool XHU = (EPI == EPI_JACOBI) ? false : XH;
@@ -738,6 +765,7 @@ int kron_v5_launch(int pmax, int epi, const KronPtrs& p, const KronGeom& g, cons
         set_error("v5: bad tile geometry");
         return 1;
     }
+#ifndef POMS_V5_QUICK   // (POMS_V5_QUICK: p = 3 production builds only, for quick tuning builds)
     if (diag_mode) {   // DIAGNOSTIC / tuning builds (p = 3)
         if (pmax != 3) { set_error("v5 diag mode: p = 3 only"); return 1; }
         if (diag_mode <= 2) {   // 1 = memory only, 2 = arithmetic only (apply)
@@ -766,12 +794,15 @@ int kron_v5_launch(int pmax, int epi, const KronPtrs& p, const KronGeom& g, cons
         set_error("v5 diag mode: bad mode / epilogue");
         return 1;
     }
+#endif
     switch (pmax) {
+#ifndef POMS_V5_QUICK
         case 1: return v5_launch_p<1>(epi, p, g, tc, H, omega, st);
         case 2: return v5_launch_p<2>(epi, p, g, tc, H, omega, st);
-        case 3: return v5_launch_p<3>(epi, p, g, tc, H, omega, st);
         case 4: return v5_launch_p<4>(epi, p, g, tc, H, omega, st);   // 8-wave tiles
         case 5: return v5_launch_p<5>(epi, p, g, tc, H, omega, st);
+#endif
+        case 3: return v5_launch_p<3>(epi, p, g, tc, H, omega, st);
     }
     set_error("v5: pmax must be in 1..5");
     return 1;

@@ -649,23 +649,31 @@ static int stencil_run(poms_op* o, int epi, double omega, const double* x, doubl
     return 0;
 }
 
+// axis 1 and axis 2 share their Toeplitz rows bitwise (v5's SAME12 builds)
+static bool same_toeplitz12(const poms_op* o) {
+    for (int k = 0; k <= o->pmax; ++k)
+        if (o->tc.t1a[k] != o->tc.t2a[k] || o->tc.t1b[k] != o->tc.t2b[k]) return false;
+    return true;
+}
+
 // The kernel variant one launch of epilogue `epi` runs (see op_run).
 static int resolve_variant(const poms_op* o, int epi) {
     int v = o->variant;
     if (v == 8) {
         const bool plain = epi == EPI_APPLY || epi == EPI_RESID || epi == EPI_JACOBI;
-        if (o->ndim == 3 && v5_ok(o) && (epi != EPI_JACOBI0 || o->pmax <= 2))
+        if (o->ndim == 3 && v5_ok(o) &&
+            (epi != EPI_JACOBI0 || o->pmax <= 2 || (o->pmax == 3 && same_toeplitz12(o))))
             v = 10;   // v5: kernel_bench at 515^3 p = 3; 8-wave tiles at 256^3 p = 4, 5
                       // (profiles/r02/configs/kb_p5_waves8.log: apply 231 -> 185 us at p = 5);
-                      // sweeps from zero (8-wave tiles) at p <= 2 only: 136 vs 146 us at 256^3
-                      // p = 2, but 1051 vs 996 us at 515^3 p = 3 (profiles/r02/kb_j0_8wave.log)
+                      // sweeps from zero at p <= 2 (8-wave tiles) and at p = 3 (16-wave
+                      // tiles, 930 vs 945 us for v3 at 515^3, profiles/r02/j0_16wave/) where
+                      // axes 1 and 2 share their rows (the other build spills)
         else if (o->ndim == 3)
             v = ((epi == EPI_APPLY && o->pmax >= 3) || (plain && o->pmax >= 4)) ? 7 : 9;
         else
             v = ((epi == EPI_APPLY || epi == EPI_RESID) && o->pmax <= 3) ? 7 : 9;
     }
-    // v5 two-sweeps-from-zero: p <= 2 (at p = 3 the build still spills)
-    if (v == 10 && !v5_ok(o)) v = 9;
+    if (v == 10 && (!v5_ok(o) || (epi == EPI_JACOBI0 && o->pmax == 3 && !same_toeplitz12(o)))) v = 9;
     return v;
 }
 
