@@ -133,8 +133,13 @@ kron_v5_kernel(const double* __restrict__ x, double* __restrict__ y, const doubl
     typedef double d2 __attribute__((ext_vector_type(2)));
 
     constexpr int XS_OFF = 0;
+    // CP bit 64 (B3): b DMA'd two planes ahead through a 3-deep ring, each iteration
+    // issuing x before b (so that b(t) landing still implies x(t), PFX = 2)
+    constexpr bool B3 = HASB && (CP & 64) && !XIN;   // (x_in DMA builds keep the 2-deep ring)
+    constexpr int NB = B3 ? 3 : 2;      // b ring depth
+    static_assert(!B3 || D == 3, "B3: x ring depth 3");
     constexpr int BS_OFF = XS_OFF + D * XR * TC;
-    constexpr int XI_OFF = BS_OFF + (HASB ? 2 * T1 * TC : 0);
+    constexpr int XI_OFF = BS_OFF + (HASB ? NB * T1 * TC : 0);
     constexpr int C2_OFF = XI_OFF + (XIN ? 2 * T1 * TC : 0);
     constexpr int RED_OFF = C2_OFF + 2 * W * TC;
     // Jacobi (register-history builds; the x_in ring leaves no room): 1/diag on the
@@ -332,6 +337,7 @@ kron_v5_kernel(const double* __restrict__ x, double* __restrict__ y, const doubl
 #pragma unroll
     for (int i = 0; i < PFX; ++i) dma_x(i < nplanes ? z0 - P + i : -(1 << 20), i);
     if constexpr (HASB) dma_b(zo_of(0), 0);
+    if constexpr (B3) dma_b(zo_of(1), 1);
 
     const bool xtra = wv < XR - (NXM - 1) * NW;   // this wave issues NXM x DMAs per plane (else NXM - 1)
     for (int tb = 0; tb < nplanes; tb += NS) {
@@ -346,7 +352,12 @@ kron_v5_kernel(const double* __restrict__ x, double* __restrict__ y, const doubl
                 // after the one waited for (stores never count): vmcnt <= that number
                 // implies the load has landed.  Waiting for b(t) also covers x(t) (issued
                 // before it, PFX >= 2).
-                if constexpr (HASB) {
+                if constexpr (B3) {
+                    // after b(t): x(t+1) and b(t+1) (the previous iteration's DMAs)
+                    if (t == 0) v5_wait_vm<0>();
+                    else if (xtra) v5_wait_vm<NXM + 1>();
+                    else v5_wait_vm<NXM>();
+                } else if constexpr (HASB) {
                     if (t == 0) v5_wait_vm<0>();
                     else if (xtra) v5_wait_vm<NXM>();
                     else v5_wait_vm<NXM - 1>();
@@ -387,8 +398,13 @@ kron_v5_kernel(const double* __restrict__ x, double* __restrict__ y, const doubl
                     __builtin_amdgcn_s_waitcnt(0xc07f);   // lgkmcnt(0): the scaled rows written
                 }
                 v5_barrier();
-                if constexpr (HASB) dma_b(zo_of(t + 1), (t + 1) & 1);
-                dma_x(t + PFX < nplanes ? z0 - P + t + PFX : -(1 << 20), (t + PFX) % D);
+                if constexpr (B3) {
+                    dma_x(t + PFX < nplanes ? z0 - P + t + PFX : -(1 << 20), (t + PFX) % D);
+                    dma_b(min(zo_of(t + 2), z1), (t + 2) % 3);   // (clamped: the plane past the chunk is a dummy)
+                } else {
+                    if constexpr (HASB) dma_b(zo_of(t + 1), (t + 1) & 1);
+                    dma_x(t + PFX < nplanes ? z0 - P + t + PFX : -(1 << 20), (t + PFX) % D);
+                }
 
                 // ---- axis 1: u = F1a x, v = F1b x on this wave's row, 2 columns per lane
                 const double* xs = lds + XS_OFF + (t % D) * XR * TC + 2 * lane;
@@ -553,7 +569,7 @@ kron_v5_kernel(const double* __restrict__ x, double* __restrict__ y, const doubl
                     }
                     *(d2*)(lds + JS_OFF + 2 * tid) = js;
                 } else {
-                    const d2 bv = *(const d2*)(lds + BS_OFF + ((t & 1) * T1 + wv) * TC + 2 * lane);
+                    const d2 bv = *(const d2*)(lds + BS_OFF + ((t % NB) * T1 + wv) * TC + 2 * lane);
                     if constexpr (EPI == EPI_RESID) {
                         outv[0] = bv[0] - vo[0];
                         outv[1] = bv[1] - vo[1];
@@ -727,15 +743,18 @@ static int v5_launch_p(int epi, const KronPtrs& p, const KronGeom& g, const Toep
         // residual 713 -> 672, Jacobi 886 -> 777; nt x DMAs cost 15 %: the halo rows
         // are re-read by the neighbouring tiles)
         // apply: also nt on the x rows no other tile reads (variant 109: 568 -> 539 us)
+        // residual / Jacobi: b two planes ahead through a 3-deep ring (CP bit 64; Jacobi
+        // 749 -> 739 us in kernel_bench, 731 -> 716 us inside the V-cycle at 515^3,
+        // profiles/r02/b3/)
         case EPI_APPLY:
             if (store_policy() == 1) return v5_launch_t<P, EPI_APPLY, 4, 0, 10 | 16>(p, g, tc, H, omega, st);
             if (store_policy() == 2) return v5_launch_t<P, EPI_APPLY, 4, 0, 10 | 32>(p, g, tc, H, omega, st);
             return v5_launch_t<P, EPI_APPLY, 4, 0, 14>(p, g, tc, H, omega, st);
-        case EPI_RESID: return v5_launch_t<P, EPI_RESID, 3, 0, 6>(p, g, tc, H, omega, st);
+        case EPI_RESID: return v5_launch_t<P, EPI_RESID, 3, 0, 6 | 64>(p, g, tc, H, omega, st);
         case EPI_JACOBI:
             if (store_policy() == 1) return v5_launch_t<P, EPI_JACOBI, 3, 0, 2 | 16, true>(p, g, tc, H, omega, st);
             if (store_policy() == 2) return v5_launch_t<P, EPI_JACOBI, 3, 0, 2 | 32, true>(p, g, tc, H, omega, st);
-            return v5_launch_t<P, EPI_JACOBI, 3, 0, 6, true>(p, g, tc, H, omega, st);
+            return v5_launch_t<P, EPI_JACOBI, 3, 0, 6 | 64, true>(p, g, tc, H, omega, st);
         case EPI_APPLYDOT: return v5_launch_t<P, EPI_APPLYDOT, 4, 0, 6>(p, g, tc, H, omega, st);
         // x ring = b (read once, apply's policy), scaled in place to x1 after it lands;
         // y = x2 streamed

@@ -17,6 +17,7 @@ for L in "$@" "$@"; do
   rc=$?; echo "$tag kb rc=$rc"; tail -3 $O/kb_$tag.log
   [ $rc -eq 0 ] || exit $rc
 done
+[ -n "${AB_NOBENCH:-}" ] && exit 0
 for L in "$@"; do
   tag=$(basename $L .so)
   POMS_HIP_LIB=$PWD/$L timeout -k 10 600 python -u bench.py --no-cpu-baseline > $O/bench_$tag.log 2>&1
