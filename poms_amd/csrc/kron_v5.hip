@@ -135,9 +135,8 @@ kron_v5_kernel(const double* __restrict__ x, double* __restrict__ y, const doubl
     constexpr int XS_OFF = 0;
     // CP bit 64 (B3): b DMA'd two planes ahead through a 3-deep ring, each iteration
     // issuing x before b (so that b(t) landing still implies x(t), PFX = 2)
-    constexpr bool B3 = HASB && (CP & 64) && !XIN;   // (x_in DMA builds keep the 2-deep ring)
+    constexpr bool B3 = HASB && (CP & 64) && !XIN && D == 3;   // (x_in DMA builds and deeper x rings keep the 2-deep b ring)
     constexpr int NB = B3 ? 3 : 2;      // b ring depth
-    static_assert(!B3 || D == 3, "B3: x ring depth 3");
     constexpr int BS_OFF = XS_OFF + D * XR * TC;
     constexpr int XI_OFF = BS_OFF + (HASB ? NB * T1 * TC : 0);
     constexpr int C2_OFF = XI_OFF + (XIN ? 2 * T1 * TC : 0);
@@ -715,11 +714,13 @@ static int v5_launch_t(const KronPtrs& p, const KronGeom& g, const ToepConst& tc
     // the Jacobi x_in history does not fit the VGPRs beside the split stores: the
     // unaligned build DMAs x_in next to b instead
     constexpr bool XHU = (EPI == EPI_JACOBI) ? false : XH;
+    // (the x_in DMA build has no LDS room for a 4th x plane at p = 3)
+    constexpr int DU = (EPI == EPI_JACOBI && D > 3) ? 3 : D;
     if (EPI == EPI_JACOBI && p.partial2 == nullptr)
         return st16 ? v5_launch_t1<P, EPI, D, MODE, CP, XH, true, false>(p, g, tc, H, omega, st)
-                    : v5_launch_t1<P, EPI, D, MODE, CP, XHU, false, false>(p, g, tc, H, omega, st);
+                    : v5_launch_t1<P, EPI, DU, MODE, CP, XHU, false, false>(p, g, tc, H, omega, st);
     return st16 ? v5_launch_t1<P, EPI, D, MODE, CP, XH, true>(p, g, tc, H, omega, st)
-                : v5_launch_t1<P, EPI, D, MODE, CP, XHU, false>(p, g, tc, H, omega, st);
+                : v5_launch_t1<P, EPI, DU, MODE, CP, XHU, false>(p, g, tc, H, omega, st);
 }
 
 // y-store cache policy of the apply / Jacobi builds (tuning: POMS_V5_STORE = 0 nt,
@@ -743,9 +744,12 @@ static int v5_launch_p(int epi, const KronPtrs& p, const KronGeom& g, const Toep
         // residual 713 -> 672, Jacobi 886 -> 777; nt x DMAs cost 15 %: the halo rows
         // are re-read by the neighbouring tiles)
         // apply: also nt on the x rows no other tile reads (variant 109: 568 -> 539 us)
-        // residual / Jacobi: b two planes ahead through a 3-deep ring (CP bit 64; Jacobi
-        // 749 -> 739 us in kernel_bench, 731 -> 716 us inside the V-cycle at 515^3,
-        // profiles/r02/b3/)
+        // residual: b two planes ahead through a 3-deep ring (CP bit 64; on the Jacobi
+        // sweep 749 -> 739 us in kernel_bench, 731 -> 716 us inside the V-cycle at 515^3,
+        // profiles/r02/b3/).  Jacobi: a 4-deep x ring (x three planes ahead) with the
+        // 2-deep b ring instead -- both do not fit the LDS -- 737-748 -> 729-735 us
+        // against the 3-deep b ring on one box (profiles/r02/ring_depth/); the unaligned
+        // x_in build keeps 3 x planes and the 3-deep b ring.
         case EPI_APPLY:
             if (store_policy() == 1) return v5_launch_t<P, EPI_APPLY, 4, 0, 10 | 16>(p, g, tc, H, omega, st);
             if (store_policy() == 2) return v5_launch_t<P, EPI_APPLY, 4, 0, 10 | 32>(p, g, tc, H, omega, st);
@@ -754,7 +758,7 @@ static int v5_launch_p(int epi, const KronPtrs& p, const KronGeom& g, const Toep
         case EPI_JACOBI:
             if (store_policy() == 1) return v5_launch_t<P, EPI_JACOBI, 3, 0, 2 | 16, true>(p, g, tc, H, omega, st);
             if (store_policy() == 2) return v5_launch_t<P, EPI_JACOBI, 3, 0, 2 | 32, true>(p, g, tc, H, omega, st);
-            return v5_launch_t<P, EPI_JACOBI, 3, 0, 6 | 64, true>(p, g, tc, H, omega, st);
+            return v5_launch_t<P, EPI_JACOBI, 4, 0, 6 | 64, true>(p, g, tc, H, omega, st);
         case EPI_APPLYDOT: return v5_launch_t<P, EPI_APPLYDOT, 4, 0, 6>(p, g, tc, H, omega, st);
         // x ring = b (read once, apply's policy), scaled in place to x1 after it lands;
         // y = x2 streamed
