@@ -750,10 +750,13 @@ static int v5_launch_p(int epi, const KronPtrs& p, const KronGeom& g, const Toep
         // 2-deep b ring instead -- both do not fit the LDS -- 737-748 -> 729-735 us
         // against the 3-deep b ring on one box (profiles/r02/ring_depth/); the unaligned
         // x_in build keeps 3 x planes and the 3-deep b ring.
+        // (round 2 closing: the default policy on those rows after all -- variant 104
+        // vs 10 interleaved on one box, median 548-550 vs 583-621 us, equal minima;
+        // the streamed rows made the apply's time scatter, profiles/r02/j0ab/)
         case EPI_APPLY:
-            if (store_policy() == 1) return v5_launch_t<P, EPI_APPLY, 4, 0, 10 | 16>(p, g, tc, H, omega, st);
-            if (store_policy() == 2) return v5_launch_t<P, EPI_APPLY, 4, 0, 10 | 32>(p, g, tc, H, omega, st);
-            return v5_launch_t<P, EPI_APPLY, 4, 0, 14>(p, g, tc, H, omega, st);
+            if (store_policy() == 1) return v5_launch_t<P, EPI_APPLY, 4, 0, 2 | 16>(p, g, tc, H, omega, st);
+            if (store_policy() == 2) return v5_launch_t<P, EPI_APPLY, 4, 0, 2 | 32>(p, g, tc, H, omega, st);
+            return v5_launch_t<P, EPI_APPLY, 4, 0, 6>(p, g, tc, H, omega, st);
         case EPI_RESID: return v5_launch_t<P, EPI_RESID, 3, 0, 6 | 64>(p, g, tc, H, omega, st);
         case EPI_JACOBI:
             if (store_policy() == 1) return v5_launch_t<P, EPI_JACOBI, 3, 0, 2 | 16, true>(p, g, tc, H, omega, st);

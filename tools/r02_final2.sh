@@ -17,6 +17,6 @@ export TMPDIR=/tmp
     python3 "$GRAFT_REPO_ROOT/bench.py" --steps 2 --warmup 1 --no-cpu-baseline) > $OUT/prof.log 2>&1 || exit 1
 bash tools/pmc_traffic.sh j10 "kron_v5_kernel<3, 2, 4, 0, 70," --cells 512 --p 3 --kinds jacobi --variants 10 > $OUT/pmc.log 2>&1 || exit 1
 python3 tools/pmc_traffic.py gpurun_out/pmct_j10 "kron_v5_kernel<3, 2, 4, 0, 70," 136590875 $OUT/pmc_traffic_jacobi.json 3 10 > /dev/null
-bash tools/pmc_traffic.sh a10 "kron_v5_kernel<3, 0, 4, 0, 14," --cells 512 --p 3 --kinds apply --variants 10 > $OUT/pmc_apply.log 2>&1 || exit 1
-python3 tools/pmc_traffic.py gpurun_out/pmct_a10 "kron_v5_kernel<3, 0, 4, 0, 14," 136590875 $OUT/pmc_traffic_apply.json 3 10 > /dev/null
+bash tools/pmc_traffic.sh a10 "kron_v5_kernel<3, 0, 4, 0, 6," --cells 512 --p 3 --kinds apply --variants 10 > $OUT/pmc_apply.log 2>&1 || exit 1
+python3 tools/pmc_traffic.py gpurun_out/pmct_a10 "kron_v5_kernel<3, 0, 4, 0, 6," 136590875 $OUT/pmc_traffic_apply.json 3 10 > /dev/null
 echo done
