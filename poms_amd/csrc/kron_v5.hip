@@ -152,8 +152,10 @@ kron_v5_kernel(const double* __restrict__ x, double* __restrict__ y, const doubl
     constexpr int D1_OFF = D2_OFF + (J0 ? 2 * TC : 0);   // J0: axis-1 diagonal entries of the x-tile rows
     // J0: per-lane running sums (||dr_2||^2, ||x1||^2) in LDS, not VGPRs: the 4
     // VGPRs they would pin for the whole march are what p = 3 lacks at 16 waves
+    // (p = 3 only: the 8-wave builds of p <= 2 keep them in VGPRs, which they have)
+    constexpr bool JSL = J0 && P == 3;
     constexpr int JS_OFF = (D1_OFF + (J0 ? 2 * XR : 0) + 1) & ~1;
-    constexpr int LDS_N = JS_OFF + (J0 ? 2 * NW * 64 : 0);
+    constexpr int LDS_N = JS_OFF + (JSL ? 2 * NW * 64 : 0);
     __shared__ __attribute__((aligned(16))) double lds[LDS_N];
 
     // SAME12: axis 2's Toeplitz rows equal axis 1's bitwise (one knot vector on both
@@ -318,7 +320,7 @@ kron_v5_kernel(const double* __restrict__ x, double* __restrict__ y, const doubl
     if constexpr (J0) {
         for (int e = tid; e < XR * TC; e += NW * 64)
             lds[RS_OFF + e] = j0_scale(e / TC, e % TC, tc.t0a[0], tc.t0b[0]);
-        *(d2*)(lds + JS_OFF + 2 * tid) = d2{0.0, 0.0};
+        if constexpr (JSL) *(d2*)(lds + JS_OFF + 2 * tid) = d2{0.0, 0.0};
         __syncthreads();
     }
     if constexpr (RCIL) {
@@ -557,7 +559,8 @@ kron_v5_kernel(const double* __restrict__ x, double* __restrict__ y, const doubl
                         sc[0] = j0_scale(wv + P, 2 * lane, d0a, d0b);
                         sc[1] = j0_scale(wv + P, 2 * lane + 1, d0a, d0b);
                     }
-                    d2 js = *(const d2*)(lds + JS_OFF + 2 * tid);   // this lane's own slot
+                    d2 js = {nrm, dotp};
+                    if constexpr (JSL) js = *(const d2*)(lds + JS_OFF + 2 * tid);   // this lane's own slot
 #pragma unroll
                     for (int e = 0; e < 2; ++e) {
                         const double x1 = xin[e];
@@ -566,7 +569,12 @@ kron_v5_kernel(const double* __restrict__ x, double* __restrict__ y, const doubl
                         js[0] = ok[e] ? fma(dr, dr, js[0]) : js[0];   // ||dr_2||^2
                         js[1] = ok[e] ? fma(x1, x1, js[1]) : js[1];   // ||x1||^2 = ||dr_1||^2
                     }
-                    *(d2*)(lds + JS_OFF + 2 * tid) = js;
+                    if constexpr (JSL) {
+                        *(d2*)(lds + JS_OFF + 2 * tid) = js;
+                    } else {
+                        nrm = js[0];
+                        dotp = js[1];
+                    }
                 } else {
                     const d2 bv = *(const d2*)(lds + BS_OFF + ((t % NB) * T1 + wv) * TC + 2 * lane);
                     if constexpr (EPI == EPI_RESID) {
@@ -627,7 +635,7 @@ kron_v5_kernel(const double* __restrict__ x, double* __restrict__ y, const doubl
         }
     }
     v5_wait_vm<0>();  // no LDS-DMA may outlive the workgroup
-    if constexpr (J0) {
+    if constexpr (JSL) {
         const d2 js = *(const d2*)(lds + JS_OFF + 2 * tid);
         nrm = js[0];
         dotp = js[1];
