@@ -15,9 +15,11 @@
 //     (H = 8, TO = 112 on the aligned layout; H = P rounded up to even,
 //     TO = 128 - 2H otherwise);
 //   * memory: each x plane tile (T1 + 2P rows x 128 columns) is DMA'd by
-//     buffer_load ... lds straight into a D-deep LDS ring, D-1 planes ahead;
-//     b (residual / Jacobi) through a 2-deep ring one plane ahead.  vmcnt is
-//     counted by hand, one barrier per plane;
+//     buffer_load ... lds straight into a D-deep LDS ring, D-1 planes ahead
+//     (D = 4 for apply and Jacobi, 3 for the residual); b (residual / Jacobi)
+//     through a 3-deep ring two planes ahead (residual) or a 2-deep ring one
+//     plane ahead (Jacobi: its 4th x plane leaves no LDS for a 3rd b plane).
+//     vmcnt is counted by hand, one barrier per plane;
 //   * axis 1 (first) on the wave's own row: u = F1a x, v = F1b x (symmetric
 //     Toeplitz pair sums inside the interior, per-row scalar coefficients
 //     outside); axis 2 with the column neighbours shifted in by DPP
