@@ -24,6 +24,9 @@ int kron_v5_launch(int pmax, int epi, const KronPtrs& p, const KronGeom& g, cons
                    double omega, hipStream_t st, int diag_mode);
 void kron_v5_tile(int pmax, bool aligned, int* H, int* TO);
 int kron_v5_rows(int pmax, int epi);
+int kron_v6_launch(int pmax, int epi, const KronPtrs& p, const KronGeom& g, const ToepConst& tc, hipStream_t st);
+int kron_v6_tile_cols();
+int kron_v6_rows();
 int kron_tile_rows();
 int kron_tile_cols();
 int vec_launch(int op, const RowGeom& g, double a, double b, const double* x, const double* y,
@@ -88,6 +91,15 @@ struct poms_op {
     double* sv_dev = nullptr;
     double* sv_host = nullptr;
     hipEvent_t sv_ev[8]{};
+    // poms_pcg_jacobi, one rank: ring of pinned host slots the reduction kernels
+    // write the host-read norms into.  sv_seq[i] = launch sequence number that armed
+    // slot i (-1: never); every launch numbered below sv_done is known complete (a
+    // value written by a later launch of the same stream has been read), so its slot
+    // can be re-armed without a stale write landing after the sentinel.
+    static constexpr int kSvRing = 48;
+    int sv_next = 0;
+    int64_t sv_seq_next = 0, sv_done = 0;
+    int64_t sv_seq[kSvRing];
     // launch timing (poms_op_timing): HIP events around every operator launch
     struct TimedLaunch { int epi; int64_t ndof; hipEvent_t e0, e1; };
     bool timing = false;
@@ -494,9 +506,9 @@ int poms_op_destroy(poms_op* o) {
 
 int poms_op_set_variant(poms_op* op, int variant) {
     // 90/91, 92-100, 101-109: diagnostic / tuning builds of v3, v4, v5
-    const bool known = variant == 0 || variant == 4 || (variant >= 7 && variant <= 10) ||
+    const bool known = variant == 0 || variant == 4 || (variant >= 7 && variant <= 11) ||
                        (variant >= 90 && variant <= 109);
-    if (!op || !known) { set_error("poms_op_set_variant: bad argument (0, 4, 7, 8, 9, 10; 90-109 diagnostic)"); return 1; }
+    if (!op || !known) { set_error("poms_op_set_variant: bad argument (0, 4, 7, 8, 9, 10, 11; 90-109 diagnostic)"); return 1; }
     if (variant > 0 && !op->v2_ok) { set_error("poms_op_set_variant: variant needs pads == pmax"); return 1; }
     op->variant = variant;
     return 0;
@@ -573,6 +585,14 @@ static bool v5_aligned(const poms_op* o, const double* x) {
     return pitch % 16 == 0 && (reinterpret_cast<uintptr_t>(x + o->L.pads[2]) & 127) == 0;
 }
 
+// v6 (variant 11, three columns per lane): the apply of 3D FORM_SUM operators at
+// p <= 3 on the line-aligned layout (x and y), arrays < 2 GiB
+static bool v6_ok(const poms_op* o, int epi, const double* x, const double* y) {
+    const int64_t bytes = (int64_t)(o->L.n[0] + 2 * o->L.pads[0]) * row_geom(&o->L).s0 * 8;
+    return epi == EPI_APPLY && o->ndim == 3 && o->form == FORM_SUM && o->v2_ok && o->pmax <= 3 &&
+           bytes < 0x7ffffff0LL && v5_aligned(o, x) && v5_aligned(o, y);
+}
+
 static int op_geom(poms_op* o, int64_t zb, int64_t ze, KronGeom& g, int v = -1, int v5_to = 0,
                    int64_t zb2 = 0, int64_t ze2 = 0, int epi = EPI_APPLY) {
     if (v < 0) v = o->variant;
@@ -584,9 +604,9 @@ static int op_geom(poms_op* o, int64_t zb, int64_t ze, KronGeom& g, int v = -1, 
     g.pd0 = r.pd0; g.pd1 = r.pd1; g.pd2 = r.pd2;
     g.g0 = (int)o->g0;
     g.tiles2 = (int)((o->L.n[2] + kron_tile_cols() - 1) / kron_tile_cols());
-    const int trows = v == 10 ? kron_v5_rows(o->pmax, epi) : kron_tile_rows();
+    const int trows = v == 10 ? kron_v5_rows(o->pmax, epi) : v == 11 ? kron_v6_rows() : kron_tile_rows();
     g.tiles1 = (int)((o->L.n[1] + trows - 1) / trows);
-    g.tout = v == 10 ? v5_to : (o->tout > 0 ? o->tout : 64 - 2 * o->pmax);
+    g.tout = v == 10 ? v5_to : v == 11 ? kron_v6_tile_cols() : (o->tout > 0 ? o->tout : 64 - 2 * o->pmax);
     if (v >= 4) g.tiles2 = (int)((o->L.n[2] + g.tout - 1) / g.tout);
     if (!is3d) {
         g.z_begin = 0; g.z_end = 1; g.chunk = 1; g.nchunks = 1; g.nch1 = 1; g.z2_begin = g.z2_end = 0;
@@ -612,7 +632,7 @@ static int op_geom(poms_op* o, int64_t zb, int64_t ze, KronGeom& g, int v = -1, 
     const int nz = (int)(ze - zb) + (int)(ze2 - zb2);
     int chunk = o->chunk;
     if (chunk <= 0)
-        chunk = auto_chunk(nz, g.tiles2 * g.tiles1, o->pmax, v == 10 ? 256.0 : 512.0);
+        chunk = auto_chunk(nz, g.tiles2 * g.tiles1, o->pmax, v >= 10 ? 256.0 : 512.0);
     chunk = std::max(1, std::min(chunk, std::max(nz, 1)));
     g.chunk = chunk;
     g.nch1 = (int)((ze - zb + chunk - 1) / chunk);
@@ -673,6 +693,7 @@ static int resolve_variant(const poms_op* o, int epi) {
         else
             v = ((epi == EPI_APPLY || epi == EPI_RESID) && o->pmax <= 3) ? 7 : 9;
     }
+    if (v == 11 && !(epi == EPI_APPLY && o->ndim == 3 && o->form == FORM_SUM && o->v2_ok && o->pmax <= 3)) v = 10;
     if (v == 10 && (!v5_ok(o) || (epi == EPI_JACOBI0 && o->pmax == 3 && !same_toeplitz12(o)))) v = 9;
     return v;
 }
@@ -706,6 +727,7 @@ static int op_run(poms_op* o, int epi, double omega, const double* x, double* y,
     int v = resolve_variant(o, epi);
     const int v5_diag = (v >= 101 && v <= 109) ? v - 100 : 0;   // v5 diagnostic / tuning builds
     if (v5_diag) v = 10;
+    if (v == 11 && !v6_ok(o, epi, x, y)) v = 10;   // (layout of these vectors: v5)
     int v5_h = 0, v5_to = 0;
     if (v == 10) kron_v5_tile(o->pmax, v5_aligned(o, x), &v5_h, &v5_to);
     KronGeom g;
@@ -729,7 +751,9 @@ static int op_run(poms_op* o, int epi, double omega, const double* x, double* y,
         tlh->ndof = (int64_t)((ze - zb) + (ze2 - zb2)) * g.n1 * g.n2;
         POMS_HIP_CHECK(hipEventRecord(tlh->e0, as_stream(stream)));
     }
-    const int rc = v == 10
+    const int rc = v == 11
+        ? kron_v6_launch(o->pmax, epi, p, g, o->tc, as_stream(stream))
+        : v == 10
         ? kron_v5_launch(o->pmax, epi, p, g, o->tc, v5_h, omega, as_stream(stream), v5_diag)
         : v == 0
         ? kron_launch(o->pmax, o->ndim == 3, o->form, epi, p, g, omega, as_stream(stream))
@@ -1492,12 +1516,32 @@ struct PcgRun {
     // into the pinned (coherent, device-mapped) host slot, armed with a sentinel the
     // host spins on (~1-2 us after the kernel instead of an event wake-up, ~15 us:
     // profiles/r02/sync_probe.log); with a communicator -- device scalar,
-    // all-reduce, copy and event.
+    // all-reduce, copy and event (fixed slots h: stream order covers those).
     bool direct() const { return comm == nullptr; }
     double* hdst(int sc_idx, int h) { return direct() ? host + h : sc + sc_idx; }
-    void arm(int h, int cnt) {
-        if (!direct()) return;
-        for (int i = 0; i < cnt; ++i) reinterpret_cast<volatile double*>(host)[h + i] = -1.0;   // norms are >= 0
+    // Arm `cnt` consecutive host slots for the next launch and return the first.
+    // Direct mode takes fresh slots from a ring: a launch the loop abandoned (an
+    // early damped-Jacobi stop leaves the next sweep queued) still writes ITS slot
+    // later, so a slot is re-armed only once that launch is known complete -- a value
+    // of a later launch has been read (launches of one stream finish in order) --
+    // else the stream is drained first (advisor finding, round 2).
+    int arm(int fixed_h, int cnt) {
+        if (!direct()) return fixed_h;
+        if (op->sv_next + cnt > poms_op::kSvRing) op->sv_next = 0;
+        const int h = op->sv_next;
+        op->sv_next += cnt;
+        for (int i = 0; i < cnt; ++i)
+            if (op->sv_seq[h + i] >= op->sv_done) {
+                (void)hipStreamSynchronize(st);
+                op->sv_done = op->sv_seq_next;
+                break;
+            }
+        for (int i = 0; i < cnt; ++i) {
+            reinterpret_cast<volatile double*>(host)[h + i] = -1.0;   // norms are >= 0
+            op->sv_seq[h + i] = op->sv_seq_next;
+        }
+        ++op->sv_seq_next;
+        return h;
     }
     int post(int sc_idx, int cnt, int h) {   // device scalars -> pinned host slot, event after the copy
         if (direct()) return 0;
@@ -1519,6 +1563,7 @@ struct PcgRun {
             }
         }
         std::atomic_thread_fence(std::memory_order_acquire);
+        op->sv_done = std::max(op->sv_done, op->sv_seq[h + i] + 1);   // that launch and all before it are done
         return *v;
     }
     int dot(const double* a, const double* b, double* dst) {
@@ -1538,33 +1583,32 @@ struct PcgRun {
         const int maxit = o->jmaxiter;
         *dot_done = 0;
         double *x = A, *xn = B;
-        int pend = 0;   // 0 none, 1 one sweep norm in host slot pend_h, 2 the from-zero pair
-        int pend_h = H_JN, ring = 0, k0;
+        int pend = 0;   // 0 none, 1 one sweep norm in host slot pend_h, 2 the from-zero pair in h0
+        int pend_h = H_JN, ring = 0, k0, h0 = H_J0;
         int fz = 0;
         if (op->ndim == 3 && maxit >= 2 && maxit != 2 && op->form != FORM_STENCIL) (void)poms_op_from_zero_supported(op, &fz);
         if (fz) {   // sweeps 1, 2 from x = 0 in one pass over rhs
-            arm(H_J0, 2);
-            if (run(EPI_JACOBI0, rhs, A, rhs, hdst(SC_J0 + 1, H_J0 + 1), hdst(SC_J0, H_J0))) return 1;
-            if (allsum(hdst(SC_J0, H_J0), 2) || post(SC_J0, 2, H_J0)) return 1;
+            h0 = arm(H_J0, 2);
+            if (run(EPI_JACOBI0, rhs, A, rhs, hdst(SC_J0 + 1, h0 + 1), hdst(SC_J0, h0))) return 1;
+            if (allsum(hdst(SC_J0, h0), 2) || post(SC_J0, 2, h0)) return 1;
             pend = 2;
             k0 = 3;
         } else {
             if (maxit < 1) { set_error("pcg: jacobi maxiter < 1"); return 1; }
-            arm(H_JN, 1);
-            if (diag_scale_norm(rhs, A, hdst(SC_JN, H_JN)) || post(SC_JN, 1, H_JN)) return 1;
+            pend_h = arm(H_JN, 1);
+            if (diag_scale_norm(rhs, A, hdst(SC_JN, pend_h)) || post(SC_JN, 1, pend_h)) return 1;
             pend = 1;
-            pend_h = H_JN;
             ring = 1;
             k0 = 2;
         }
         auto settle = [&](bool& done, double*& res) {
             done = false;
             if (pend == 2) {
-                if (get(H_J0, 0) < tol2) {   // the reference stops after sweep 1: x1 itself
+                if (get(h0, 0) < tol2) {   // the reference stops after sweep 1: x1 itself
                     if (poms_op_diag_scale(op, o->omega, rhs, xn, 0, stv)) return 1;
                     done = true;
                     res = xn;
-                } else if (get(H_J0, 1) < tol2) {
+                } else if (get(h0, 1) < tol2) {
                     done = true;
                     res = x;
                 }
@@ -1581,8 +1625,7 @@ struct PcgRun {
             if (last) {   // the last sweep's norm cannot change the result: x . rhs instead
                 if (run(EPI_JACOBI, x, xn, rhs, nullptr, sc + dot_idx) || allsum(sc + dot_idx, 1)) return 1;
             } else {
-                h = H_JN + ring;
-                arm(h, 1);
+                h = arm(H_JN + ring, 1);
                 if (run(EPI_JACOBI, x, xn, rhs, hdst(SC_JN + ring, h), nullptr) || allsum(hdst(SC_JN + ring, h), 1) ||
                     post(SC_JN + ring, 1, h))
                     return 1;
@@ -1624,8 +1667,9 @@ int poms_pcg_jacobi(poms_op* op, poms_comm* comm, const poms_pcg_opts* o, const 
         POMS_HIP_CHECK(hipMemset(op->sv_dev, 0, SC_N * sizeof(double)));
         // coherent (fine-grained) and device-mapped: reduction kernels write the
         // host-read norms straight into it
-        POMS_HIP_CHECK(hipHostMalloc(reinterpret_cast<void**>(&op->sv_host), 8 * sizeof(double),
+        POMS_HIP_CHECK(hipHostMalloc(reinterpret_cast<void**>(&op->sv_host), poms_op::kSvRing * sizeof(double),
                                      hipHostMallocMapped | hipHostMallocCoherent));
+        for (int64_t& q : op->sv_seq) q = -1;
         for (hipEvent_t& e : op->sv_ev) POMS_HIP_CHECK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
     }
     PcgRun R{op, comm, o, as_stream(stream), stream, op->sv_dev, op->sv_host};
@@ -1640,9 +1684,9 @@ int poms_pcg_jacobi(poms_op* op, poms_comm* comm, const poms_pcg_opts* o, const 
     } else if (R.run(EPI_RESID, x, r, b, nullptr, nullptr)) {
         return 1;
     }
-    R.arm(H_RR0, 1);
-    if (R.dot(r, r, R.hdst(SC_RR0, H_RR0)) || R.post(SC_RR0, 1, H_RR0)) return 1;
-    const double nrmr0 = std::sqrt(R.get(H_RR0));
+    const int hrr0 = R.arm(H_RR0, 1);
+    if (R.dot(r, r, R.hdst(SC_RR0, hrr0)) || R.post(SC_RR0, 1, hrr0)) return 1;
+    const double nrmr0 = std::sqrt(R.get(hrr0));
     double* s = nullptr;
     int dd = 0;
     if (R.damped_jacobi(r, z[0], z[1], SC_SR, &s, &dd)) return 1;
@@ -1657,14 +1701,14 @@ int poms_pcg_jacobi(poms_op* op, poms_comm* comm, const poms_pcg_opts* o, const 
     for (k = 1; k <= o->maxiter; ++k) {
         if (R.run(EPI_APPLYDOT, p, q, p, nullptr, R.sc + SC_PQ) || R.allsum(R.sc + SC_PQ, 1)) return 1;
         hipLaunchKernelGGL(pcg_scalars_kernel, dim3(1), dim3(64), 0, R.st, R.sc, 0);
-        R.arm(H_RR, 1);
-        if (poms_pcg_r_update_dev(ctx, L, R.sc + SC_ALPHA, r, q, R.hdst(SC_RR, H_RR), stream) ||
-            R.allsum(R.hdst(SC_RR, H_RR), 1) || R.post(SC_RR, 1, H_RR))
+        const int hrr = R.arm(H_RR, 1);
+        if (poms_pcg_r_update_dev(ctx, L, R.sc + SC_ALPHA, r, q, R.hdst(SC_RR, hrr), stream) ||
+            R.allsum(R.hdst(SC_RR, hrr), 1) || R.post(SC_RR, 1, hrr))
             return 1;
         double* sn = nullptr;
         if (R.damped_jacobi(r, fa, fb, SC_SRN, &sn, &dd)) return 1;   // queued before the read
         if (!dd && R.dot(sn, r, R.sc + SC_SRN)) return 1;
-        nrmr = R.get(H_RR);
+        nrmr = R.get(hrr);
         if (nrmr < o->tol * nrmr0) {   // the reference stops before psolve: that one is discarded
             if (poms_vec_axpby_dev(ctx, L, R.sc + SC_ONE, x, p, x, stream)) return 1;
             k -= 1;

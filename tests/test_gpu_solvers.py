@@ -330,6 +330,11 @@ def test_damped_jacobi_maxiter2_stops_after_sweep1(gpu, ndim, N, p):
     (3, 16, 3, 1.0, False, 0.5, 10),       # pcg stops early
     (3, 12, 2, 1.0, True, 1e-6, 1),
     (2, 24, 2, 1.0, False, 1e-6, 0),
+    # large grids: a damped-Jacobi early stop abandons a queued sweep that is still
+    # running when the next psolve re-arms host slots (advisor finding, round 2)
+    (3, 128, 2, 1e-8, False, 1e-6, 4),
+    (3, 128, 3, 1e-10, False, 1e-6, 3),
+    (3, 96, 3, 1e-7, True, 1e-6, 4),
 ])
 def test_native_pcg_matches_python_loop(gpu, monkeypatch, ndim, N, p, scale, x0, tol, maxiter):
     """poms_pcg_jacobi (the whole pcg + damped-Jacobi loop in C) == the Python device
