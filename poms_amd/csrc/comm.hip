@@ -238,7 +238,12 @@ int poms_halo_finish(poms_comm* c, void* stream) {
 // caller queues its device -> host copy (lazy norms: the next sweep never waits).
 int poms_allreduce_sum(poms_comm* c, double* buf, int64_t count, void* stream, int wait_back) {
     if (!c || !buf || count < 0) { set_error("poms_allreduce_sum: bad argument"); return 1; }
-    if (c->host) return host_allreduce(c, buf, count, cstream(stream));
+    if (c->host) {   // synchronous; the result is then also ordered on the communication stream
+        if (host_allreduce(c, buf, count, cstream(stream))) return 1;
+        POMS_HIP_CHECK(hipEventRecord(c->ev_in, cstream(stream)));
+        POMS_HIP_CHECK(hipStreamWaitEvent(c->cs, c->ev_in, 0));
+        return 0;
+    }
     POMS_HIP_CHECK(hipEventRecord(c->ev_in, cstream(stream)));
     POMS_HIP_CHECK(hipStreamWaitEvent(c->cs, c->ev_in, 0));
     POMS_NCCL_CHECK(ncclAllReduce(buf, buf, (size_t)count, ncclDouble, ncclSum, c->comm, c->cs));
@@ -270,10 +275,15 @@ int poms_allreduce_to_host(poms_comm* c, int ticket, int count, double* host_dst
         return 1;
     }
     double* slot = c->ring + 2 * ticket;
-    if (c->host) {
+    if (c->host) {   // synchronous: host_dst holds the sums on return
         if (host_allreduce(c, slot, count, cstream(stream))) return 1;
         POMS_HIP_CHECK(hipMemcpy(host_dst, slot, count * sizeof(double), hipMemcpyDeviceToHost));
-        POMS_HIP_CHECK(hipEventRecord(c->ring_ev[ticket], cstream(stream)));
+        // the ticket's event on the communication stream, ordered after the caller's
+        // stream, as on the RCCL path (work queued on poms_comm_stream after this call
+        // is then ordered after the result)
+        POMS_HIP_CHECK(hipEventRecord(c->ev_in, cstream(stream)));
+        POMS_HIP_CHECK(hipStreamWaitEvent(c->cs, c->ev_in, 0));
+        POMS_HIP_CHECK(hipEventRecord(c->ring_ev[ticket], c->cs));
         return 0;
     }
     POMS_HIP_CHECK(hipEventRecord(c->ev_in, cstream(stream)));

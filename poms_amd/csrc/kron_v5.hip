@@ -32,7 +32,10 @@
 //     re-read (the x_in DMA next to b, kept as a tuning build, costs 8 B/DOF);
 //   * y stores and b DMAs are non-temporal (streamed once); x DMAs are not
 //     (the halo rows are re-read by the neighbouring tiles).
-// Preconditions (host): 3D, FORM_SUM, P <= 3, storage pads == P, array < 2 GiB.
+// Preconditions (host, v5_ok): 3D, FORM_SUM, P <= 5 (16-wave tiles at P <= 3, 8-wave
+// tiles at P >= 4 and for the p <= 2 sweeps from zero: v5_waves), storage pads == P,
+// array < 2 GiB, and no odd P on layouts with data in the corner ghosts (the x-row
+// DMA pair holding storage column 0 of storage row 0 fails the range check there).
 #include "common.hpp"
 
 #include <cstdlib>

@@ -24,9 +24,6 @@ int kron_v5_launch(int pmax, int epi, const KronPtrs& p, const KronGeom& g, cons
                    double omega, hipStream_t st, int diag_mode);
 void kron_v5_tile(int pmax, bool aligned, int* H, int* TO);
 int kron_v5_rows(int pmax, int epi);
-int kron_v6_launch(int pmax, int epi, const KronPtrs& p, const KronGeom& g, const ToepConst& tc, hipStream_t st);
-int kron_v6_tile_cols();
-int kron_v6_rows();
 int kron_tile_rows();
 int kron_tile_cols();
 int vec_launch(int op, const RowGeom& g, double a, double b, const double* x, const double* y,
@@ -506,9 +503,9 @@ int poms_op_destroy(poms_op* o) {
 
 int poms_op_set_variant(poms_op* op, int variant) {
     // 90/91, 92-100, 101-109: diagnostic / tuning builds of v3, v4, v5
-    const bool known = variant == 0 || variant == 4 || (variant >= 7 && variant <= 11) ||
+    const bool known = variant == 0 || variant == 4 || (variant >= 7 && variant <= 10) ||
                        (variant >= 90 && variant <= 109);
-    if (!op || !known) { set_error("poms_op_set_variant: bad argument (0, 4, 7, 8, 9, 10, 11; 90-109 diagnostic)"); return 1; }
+    if (!op || !known) { set_error("poms_op_set_variant: bad argument (0, 4, 7, 8, 9, 10; 90-109 diagnostic)"); return 1; }
     if (variant > 0 && !op->v2_ok) { set_error("poms_op_set_variant: variant needs pads == pmax"); return 1; }
     op->variant = variant;
     return 0;
@@ -585,14 +582,6 @@ static bool v5_aligned(const poms_op* o, const double* x) {
     return pitch % 16 == 0 && (reinterpret_cast<uintptr_t>(x + o->L.pads[2]) & 127) == 0;
 }
 
-// v6 (variant 11, three columns per lane): the apply of 3D FORM_SUM operators at
-// p <= 3 on the line-aligned layout (x and y), arrays < 2 GiB
-static bool v6_ok(const poms_op* o, int epi, const double* x, const double* y) {
-    const int64_t bytes = (int64_t)(o->L.n[0] + 2 * o->L.pads[0]) * row_geom(&o->L).s0 * 8;
-    return epi == EPI_APPLY && o->ndim == 3 && o->form == FORM_SUM && o->v2_ok && o->pmax <= 3 &&
-           bytes < 0x7ffffff0LL && v5_aligned(o, x) && v5_aligned(o, y);
-}
-
 static int op_geom(poms_op* o, int64_t zb, int64_t ze, KronGeom& g, int v = -1, int v5_to = 0,
                    int64_t zb2 = 0, int64_t ze2 = 0, int epi = EPI_APPLY) {
     if (v < 0) v = o->variant;
@@ -604,9 +593,9 @@ static int op_geom(poms_op* o, int64_t zb, int64_t ze, KronGeom& g, int v = -1, 
     g.pd0 = r.pd0; g.pd1 = r.pd1; g.pd2 = r.pd2;
     g.g0 = (int)o->g0;
     g.tiles2 = (int)((o->L.n[2] + kron_tile_cols() - 1) / kron_tile_cols());
-    const int trows = v == 10 ? kron_v5_rows(o->pmax, epi) : v == 11 ? kron_v6_rows() : kron_tile_rows();
+    const int trows = v == 10 ? kron_v5_rows(o->pmax, epi) : kron_tile_rows();
     g.tiles1 = (int)((o->L.n[1] + trows - 1) / trows);
-    g.tout = v == 10 ? v5_to : v == 11 ? kron_v6_tile_cols() : (o->tout > 0 ? o->tout : 64 - 2 * o->pmax);
+    g.tout = v == 10 ? v5_to : (o->tout > 0 ? o->tout : 64 - 2 * o->pmax);
     if (v >= 4) g.tiles2 = (int)((o->L.n[2] + g.tout - 1) / g.tout);
     if (!is3d) {
         g.z_begin = 0; g.z_end = 1; g.chunk = 1; g.nchunks = 1; g.nch1 = 1; g.z2_begin = g.z2_end = 0;
@@ -632,7 +621,7 @@ static int op_geom(poms_op* o, int64_t zb, int64_t ze, KronGeom& g, int v = -1, 
     const int nz = (int)(ze - zb) + (int)(ze2 - zb2);
     int chunk = o->chunk;
     if (chunk <= 0)
-        chunk = auto_chunk(nz, g.tiles2 * g.tiles1, o->pmax, v >= 10 ? 256.0 : 512.0);
+        chunk = auto_chunk(nz, g.tiles2 * g.tiles1, o->pmax, v == 10 ? 256.0 : 512.0);
     chunk = std::max(1, std::min(chunk, std::max(nz, 1)));
     g.chunk = chunk;
     g.nch1 = (int)((ze - zb + chunk - 1) / chunk);
@@ -693,7 +682,6 @@ static int resolve_variant(const poms_op* o, int epi) {
         else
             v = ((epi == EPI_APPLY || epi == EPI_RESID) && o->pmax <= 3) ? 7 : 9;
     }
-    if (v == 11 && !(epi == EPI_APPLY && o->ndim == 3 && o->form == FORM_SUM && o->v2_ok && o->pmax <= 3)) v = 10;
     if (v == 10 && (!v5_ok(o) || (epi == EPI_JACOBI0 && o->pmax == 3 && !same_toeplitz12(o)))) v = 9;
     return v;
 }
@@ -727,7 +715,6 @@ static int op_run(poms_op* o, int epi, double omega, const double* x, double* y,
     int v = resolve_variant(o, epi);
     const int v5_diag = (v >= 101 && v <= 109) ? v - 100 : 0;   // v5 diagnostic / tuning builds
     if (v5_diag) v = 10;
-    if (v == 11 && !v6_ok(o, epi, x, y)) v = 10;   // (layout of these vectors: v5)
     int v5_h = 0, v5_to = 0;
     if (v == 10) kron_v5_tile(o->pmax, v5_aligned(o, x), &v5_h, &v5_to);
     KronGeom g;
@@ -751,9 +738,7 @@ static int op_run(poms_op* o, int epi, double omega, const double* x, double* y,
         tlh->ndof = (int64_t)((ze - zb) + (ze2 - zb2)) * g.n1 * g.n2;
         POMS_HIP_CHECK(hipEventRecord(tlh->e0, as_stream(stream)));
     }
-    const int rc = v == 11
-        ? kron_v6_launch(o->pmax, epi, p, g, o->tc, as_stream(stream))
-        : v == 10
+    const int rc = v == 10
         ? kron_v5_launch(o->pmax, epi, p, g, o->tc, v5_h, omega, as_stream(stream), v5_diag)
         : v == 0
         ? kron_launch(o->pmax, o->ndim == 3, o->form, epi, p, g, omega, as_stream(stream))

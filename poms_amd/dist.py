@@ -318,8 +318,9 @@ class NativeComm:
     cost the host one C call each instead of a torch.distributed round trip.
 
     :meth:`create` runs a self-test (an all-reduce and a ghost exchange checked
-    against their known results) and returns None -- the torch.distributed path
-    is used -- if anything fails."""
+    against their known results, both run on every rank before either is judged)
+    and RAISES if it fails on any rank; ``POMS_NATIVE_COMM=0`` selects the
+    torch.distributed transport explicitly."""
 
     def __init__(self, handle, device: int, callbacks=None):
         import ctypes as C
@@ -431,8 +432,9 @@ class NativeComm:
         dev = f"cuda:{self.device}"
         t = torch.full((2,), float(rank + 1), dtype=torch.float64, device=dev)
         self.allreduce(t, rt.stream_handle(), wait_back=True)
-        if not torch.allclose(t.cpu(), torch.full((2,), world * (world + 1) / 2.0, dtype=torch.float64)):
-            return False
+        # judged only after the exchange below: a rank that returned here would leave its
+        # neighbours blocked in their halo_start, and the job would hang instead of raising
+        ok = bool(torch.allclose(t.cpu(), torch.full((2,), world * (world + 1) / 2.0, dtype=torch.float64)))
         pad, width, n_loc, pe = 2, 2, 3, 8
         data = torch.zeros((n_loc + 2 * pad, pe), dtype=torch.float64, device=dev)
         for i in range(n_loc):
@@ -453,7 +455,7 @@ class NativeComm:
                 return False
             if nxt < 0 and bool(hi.any()):
                 return False
-        return True
+        return ok
 
     def halo_start(self, data: torch.Tensor, n_local: int, pad: int, width: int, prev: int, nxt: int, stream):
         from . import _lib

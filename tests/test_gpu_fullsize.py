@@ -134,3 +134,84 @@ def test_variants_agree_full_size(gpu, cfg):
         A.set_variant(v)
         y = A.dot(x)
         assert trel(y._data, ref) <= 1e-14, v
+
+
+@pytest.mark.parametrize("cfg", list(CONFIGS))
+@pytest.mark.parametrize("align", [False, True])
+def test_bench_kernels_full_size(gpu, cfg, align):
+    """Every other kernel the V-cycle bench launches, at the BASELINE sizes (a race
+    that only showed at 515^3 has happened on this path before):
+
+    * the two-sweeps-from-zero launch (JACOBI0) == diag_scale then one sweep, which are
+      themselves property-checked above; both of its norms;
+    * apply + x.Ax (APPLYDOT) == the apply, and its dot == x . (A x);
+    * the Jacobi sweep that also forms x_out . b (the JDOT build) == the plain sweep;
+    * pcg's fused vector updates (vec_flat_kernel: r -= a q with r.r; x += a p with
+      p = s + b p) against torch fp64 on the interiors, ghosts staying zero.
+    `sources/solvers.py:103-124, 207-219`."""
+    from poms_amd import solvers
+    ndim, p, N = CONFIGS[cfg]
+    V, A, M, K, n = setup(ndim, p, N, align=align)
+    g = torch.Generator(device=gpu).manual_seed(17)
+    w = 2.0 / 3.0
+
+    def rnd():
+        v = V.zeros()
+        V.interior(v._data).uniform_(-1, 1, generator=g)
+        v._mark_written()
+        return v
+
+    def ghosts_zero(v):
+        t = v._data.clone()
+        V.interior(t).zero_()
+        return not bool(t.any())
+
+    x, b = rnd(), rnd()
+    # --- APPLYDOT
+    if A.apply_dot_supported:
+        q = V.zeros()
+        pq = A.dot_inner(x, q)
+        y = A.dot(x)
+        assert trel(V.interior(q._data), V.interior(y._data)) <= 1e-15
+        want = float(torch.sum(V.interior(x._data) * V.interior(y._data)))
+        assert abs(pq - want) <= 1e-12 * abs(want)
+        assert ghosts_zero(q)
+        del q, y
+    # --- Jacobi sweep with the fused x_out . b (JDOT) vs the plain sweep
+    if A.fused_dot_supported:
+        xo1, xo2 = V.zeros(), V.zeros()
+        nrm1 = A.jacobi_sweep(b, x, xo1, w, want_norm=True)
+        nrm2, xb = A.jacobi_sweep(b, x, xo2, w, want_norm=True, want_dot=True)
+        assert trel(V.interior(xo2._data), V.interior(xo1._data)) <= 1e-15
+        assert abs(nrm2 - nrm1) <= 1e-12 * nrm1
+        want = float(torch.sum(V.interior(xo1._data) * V.interior(b._data)))
+        assert abs(xb - want) <= 1e-12 * abs(want)
+        assert ghosts_zero(xo2)
+        del xo1, xo2
+    # --- two sweeps from zero (JACOBI0) vs diag_scale + one sweep
+    if A.from_zero_supported:
+        y0 = V.zeros()
+        n1, n2 = A.jacobi_from_zero(b, y0, w, want_norm=True)
+        x1, x2 = V.zeros(), V.zeros()
+        m1 = A.diag_scale(b, x1, scale=w, want_norm=True)
+        m2 = A.jacobi_sweep(b, x1, x2, w, want_norm=True)
+        assert trel(V.interior(y0._data), V.interior(x2._data)) <= 1e-13
+        assert abs(n1 - m1) <= 1e-12 * m1 and abs(n2 - m2) <= 1e-12 * m2
+        assert ghosts_zero(y0)
+        del y0, x1, x2
+    # --- pcg vector updates
+    r, qv, xs, pv, sv = rnd(), rnd(), rnd(), rnd(), rnd()
+    r0, q0 = V.interior(r._data).clone(), V.interior(qv._data).clone()
+    alpha, beta = 0.37, -1.25
+    rr = solvers._pcg_r_update(V, alpha, r, qv)
+    want = r0 - alpha * q0
+    assert trel(V.interior(r._data), want) <= 1e-15
+    want_rr = float(torch.sum(want * want))
+    assert abs(rr - want_rr) <= 1e-12 * want_rr
+    assert ghosts_zero(r)
+    del r0, q0, want
+    x0, p0, s0 = (V.interior(v._data).clone() for v in (xs, pv, sv))
+    solvers._pcg_xp_update(V, alpha, beta, xs, pv, sv)
+    assert trel(V.interior(xs._data), x0 + alpha * p0) <= 1e-15
+    assert trel(V.interior(pv._data), s0 + beta * p0) <= 1e-15
+    assert ghosts_zero(xs) and ghosts_zero(pv)
