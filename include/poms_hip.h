@@ -325,20 +325,32 @@ int poms_dense_matvec(poms_ctx* ctx, int64_t n, const double* Minv, const double
 int poms_ksolve_create(poms_ctx* ctx, int ndim, const poms_layout* layout, int64_t n0_global,
                        const double* const* ab, const int64_t* ldab, const int* kl, const int* ku,
                        poms_ksolve** ks);
+/* As poms_ksolve_create with the global extent of EVERY axis (n_global[3]; the
+ * factor of axis d is n_global[d] x n_global[d]): the block layouts of a Cart
+ * decomposition, whose distributed axes are solved on transposed lines with
+ * poms_kron_solve_lines_dense (replaces the per-line `Allgatherv` over the axis
+ * sub-communicators of `kron_solve_par` / `kron_solve_bnd_par`,
+ * `sources/kron_product.py:119-170, 191-238`).                                  */
+int poms_ksolve_create_global(poms_ctx* ctx, int ndim, const poms_layout* layout, const int64_t* n_global,
+                              const double* const* ab, const int64_t* ldab, const int* kl, const int* ku,
+                              poms_ksolve** ks);
 int poms_ksolve_destroy(poms_ksolve* ks);
 /* dgbtrf info per axis (0 = ok, j+1 = u(j,j) is exactly zero; solves then fail). */
 int poms_ksolve_info(poms_ksolve* ks, int* info3);
 /* Absolute 0-based pivot rows of axis `axis` (n_d ints, host). */
 int poms_ksolve_pivots(poms_ksolve* ks, int axis, int* ipiv);
 /* x = solve(y) on the interior of padded device arrays (x may alias y; ghosts
- * untouched).  All axes must be local (n0 == n0_global).                      */
+ * untouched).  All axes must be local (n == n_global).                        */
 int poms_kron_solve(poms_ksolve* ks, const double* y, double* x, void* stream);
-/* One axis only (axis 0 needs n0 == n0_global). */
+/* One axis only (it must be local: n[axis] == n_global[axis]). */
 int poms_kron_solve_axis(poms_ksolve* ks, int axis, const double* in, double* out, void* stream);
 /* Axis-0 solve of a dense C-order (n0_global, m) device buffer (the all-to-all
  * transposed slab of a distributed solve; replaces the per-line `Allgatherv` +
  * `dgbtrs` of `pyccel/pyccel_functions.py:150-155`).  out may alias in.         */
 int poms_kron_solve_axis0_dense(poms_ksolve* ks, const double* in, double* out, int64_t m, void* stream);
+/* Lines of axis `axis` (any axis): a dense C-order (n_global[axis], m) device
+ * buffer, column j = one line.  out may alias in.                               */
+int poms_kron_solve_lines_dense(poms_ksolve* ks, int axis, const double* in, double* out, int64_t m, void* stream);
 /* Host-pointer drop-ins of `kron_solve_par_bnd_pyccel_2d(A_bnd, la, ua, B_bnd, lb,
  * ub, X, Y, points, pads, ...)` / `_3d` on one rank: X, Y are padded C-order
  * host arrays ((n_d + 2 pads_d) per axis); X's interior is overwritten, its

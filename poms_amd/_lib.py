@@ -126,12 +126,15 @@ _SIGS = {
     "poms_dense_matvec": [_vp, _i64, _vp, _vp, _vp, _vp],
     "poms_ksolve_create": [_vp, _i, _LP, _i64, C.POINTER(C.c_void_p), C.POINTER(_i64), C.POINTER(_i),
                            C.POINTER(_i), _pp],
+    "poms_ksolve_create_global": [_vp, _i, _LP, C.POINTER(_i64), C.POINTER(C.c_void_p), C.POINTER(_i64),
+                                  C.POINTER(_i), C.POINTER(_i), _pp],
     "poms_ksolve_destroy": [_vp],
     "poms_ksolve_info": [_vp, C.POINTER(_i)],
     "poms_ksolve_pivots": [_vp, _i, C.POINTER(_i)],
     "poms_kron_solve": [_vp, _vp, _vp, _vp],
     "poms_kron_solve_axis": [_vp, _i, _vp, _vp, _vp],
     "poms_kron_solve_axis0_dense": [_vp, _vp, _vp, _i64, _vp],
+    "poms_kron_solve_lines_dense": [_vp, _i, _vp, _vp, _i64, _vp],
     "poms_kron_solve_bnd_2d": [_vp, _vp, _i64, _i, _i, _vp, _i64, _i, _i, _vp, _vp, _vp, _vp],
     "poms_pcg_jacobi": [_vp, _vp, C.POINTER(PcgOpts), _vp, _vp, _i, C.POINTER(C.c_void_p), C.POINTER(PcgInfo), _vp],
     "poms_op_timing": [_vp, _i, _i, _i, _i],

@@ -164,6 +164,7 @@ struct poms_ksolve {
     int ndim = 3;
     poms_layout L{};
     int64_t n0g = 1;
+    int64_t ng[3]{1, 1, 1};     // global extent of every axis (the factor sizes)
     int info[3]{};
     int kl[3]{}, ku[3]{};
     std::vector<int> ipiv[3];   // absolute 0-based pivot rows (host copy, for callers)
@@ -1274,10 +1275,19 @@ int poms_ksolve_destroy(poms_ksolve* ks) {
 int poms_ksolve_create(poms_ctx* ctx, int ndim, const poms_layout* layout, int64_t n0_global,
                        const double* const* ab, const int64_t* ldab, const int* kl, const int* ku,
                        poms_ksolve** out) {
-    if (!ctx || !out || !ab || !ldab || !kl || !ku || !layout_ok(layout)) {
+    if (!layout) { set_error("poms_ksolve_create: bad argument"); return 1; }
+    const int64_t ng[3] = {n0_global, layout->n[1], layout->n[2]};
+    return poms_ksolve_create_global(ctx, ndim, layout, ng, ab, ldab, kl, ku, out);
+}
+
+int poms_ksolve_create_global(poms_ctx* ctx, int ndim, const poms_layout* layout, const int64_t* n_global,
+                              const double* const* ab, const int64_t* ldab, const int* kl, const int* ku,
+                              poms_ksolve** out) {
+    if (!ctx || !out || !ab || !ldab || !kl || !ku || !n_global || !layout_ok(layout)) {
         set_error("poms_ksolve_create: bad argument");
         return 1;
     }
+    const int64_t n0_global = n_global[0];
     if (ndim < 1 || ndim > 3) { set_error("poms_ksolve_create: ndim 1..3"); return 1; }
     const int d0 = 3 - ndim;
     for (int d = 0; d < d0; ++d)
@@ -1286,6 +1296,8 @@ int poms_ksolve_create(poms_ctx* ctx, int ndim, const poms_layout* layout, int64
             return 1;
         }
     if (ndim == 3 && n0_global < layout->n[0]) { set_error("poms_ksolve_create: n0_global < local n0"); return 1; }
+    for (int d = 1; d < 3; ++d)
+        if (d >= d0 && n_global[d] < layout->n[d]) { set_error("poms_ksolve_create: global extent < local extent"); return 1; }
     for (int d = d0; d < 3; ++d) {
         if (!ab[d] || kl[d] < 0 || ku[d] < 0 || ldab[d] < 2 * kl[d] + ku[d] + 1) {
             set_error("poms_ksolve_create: bad band of axis " + std::to_string(d));
@@ -1299,9 +1311,10 @@ int poms_ksolve_create(poms_ctx* ctx, int ndim, const poms_layout* layout, int64
     ks->ndim = ndim;
     ks->L = *layout;
     ks->n0g = ndim == 3 ? n0_global : 1;
+    for (int d = 0; d < 3; ++d) ks->ng[d] = d < d0 ? 1 : d == 0 ? ks->n0g : n_global[d];
     int rc = 0;
     for (int d = d0; d < 3 && !rc; ++d) {
-        const int64_t n = d == 0 ? ks->n0g : layout->n[d];
+        const int64_t n = ks->ng[d];
         std::vector<double> band(ab[d], ab[d] + ldab[d] * n);
         ks->ipiv[d].assign((size_t)n, 0);
         ks->info[d] = band_lu(n, kl[d], ku[d], band.data(), ldab[d], ks->ipiv[d].data());
@@ -1344,6 +1357,11 @@ static int ksolve_axis(poms_ksolve* ks, int axis, const double* in, double* out,
                   std::to_string(ks->info[axis]) + ")");
         return 1;
     }
+    if (ks->L.n[axis] != ks->ng[axis]) {
+        set_error("kron solve: axis " + std::to_string(axis) +
+                  " is distributed; solve its transposed lines with poms_kron_solve_lines_dense");
+        return 1;
+    }
     const RowGeom g = row_geom(&ks->L);
     const int64_t base = g.pd0 * g.s0 + g.pd1 * g.s1 + g.pd2;
     int rc = 0;
@@ -1382,10 +1400,20 @@ int poms_kron_solve(poms_ksolve* ks, const double* y, double* x, void* stream) {
 }
 
 int poms_kron_solve_axis0_dense(poms_ksolve* ks, const double* in, double* out, int64_t m, void* stream) {
-    if (!ks || !in || !out || ks->ndim != 3 || m < 0) { set_error("poms_kron_solve_axis0_dense: bad argument"); return 1; }
-    if (ks->info[0] != 0) { set_error("kron solve: factor of axis 0 is singular"); return 1; }
+    if (!ks || ks->ndim != 3) { set_error("poms_kron_solve_axis0_dense: bad argument"); return 1; }
+    return poms_kron_solve_lines_dense(ks, 0, in, out, m, stream);
+}
+
+int poms_kron_solve_lines_dense(poms_ksolve* ks, int axis, const double* in, double* out, int64_t m, void* stream) {
+    if (!ks || !in || !out || m < 0 || axis < 3 - ks->ndim || axis > 2) {
+        set_error("poms_kron_solve_lines_dense: bad argument");
+        return 1;
+    }
+    if (ks->info[axis] != 0) { set_error("kron solve: factor of axis " + std::to_string(axis) + " is singular"); return 1; }
+    if (m == 0) return 0;
+    // m lines of ng[axis] points, line j at column j of a dense C-order (ng, m) buffer
     LineGeom lg{0, 0, m, 1, m};
-    if (ksolve_strided_launch(lg, ks->f[0], in, out, as_stream(stream))) return 1;
+    if (ksolve_strided_launch(lg, ks->f[axis], in, out, as_stream(stream))) return 1;
     POMS_HIP_CHECK(hipGetLastError());
     return 0;
 }

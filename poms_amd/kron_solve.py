@@ -19,6 +19,16 @@ all-to-all (the slab's interior, split along axis 1, one block per rank), solved
 as dense columns and transposed back.  That replaces the per-line
 ``Allgatherv`` of `pyccel/pyccel_functions.py:150-155` (one collective per
 line) by two collectives per solve.
+
+Cart (block) decompositions, `kron_solve_par` / `kron_solve_bnd_par`
+(`sources/kron_product.py:119-170, 191-238`): every axis whose process-grid
+extent is > 1 is solved the same way inside its LINE GROUP (the ranks that share
+the block's coordinates on the other axes -- the reference's ``subcomm[d]``):
+the block, flattened over the other axes and split into one part per member, is
+exchanged so that each member holds whole axis-d lines for its part, those lines
+are solved as dense columns (``poms_kron_solve_lines_dense``) and sent back.
+Axes the grid does not split are solved in place.  Axis order 0, 1, 2 as the
+reference.
 """
 from __future__ import annotations
 
@@ -91,8 +101,8 @@ class KronSolver:
         ptrs = (C.c_void_p * 3)(*[None if b is None else b.ctypes.data for b in bands])
         self.kl, self.ku = tuple(kl), tuple(ku)
         h = C.c_void_p()
-        _lib.call("poms_ksolve_create", V.ctx, V.ndim, C.byref(V.layout), int(V.npts[0]) if V.ndim == 3 else 1,
-                  ptrs, ld, kl, ku, C.byref(h))
+        ng = (C.c_int64 * 3)(*([1] * lead + [int(n) for n in V.npts]))   # global extents (factor sizes)
+        _lib.call("poms_ksolve_create_global", V.ctx, V.ndim, C.byref(V.layout), ng, ptrs, ld, kl, ku, C.byref(h))
         self._h = h
         info = (C.c_int * 3)()
         _lib.call("poms_ksolve_info", h, info)
@@ -121,11 +131,18 @@ class KronSolver:
         if Y.space is not V and (Y.space.npts != V.npts or Y.space.pads != V.pads
                                  or Y.space.layout.pitch != V.layout.pitch):
             raise ValueError("vector is not in the solver's space")
-        if V.is_distributed and V.is_cart:
-            raise NotImplementedError("the distributed Kronecker solve transposes axis-0 slabs; "
-                                      "use a SlabDistribution")
         X = V.empty() if out is None else out
         st = rt.stream_handle()
+        if V.is_distributed and V.is_cart:
+            src = Y
+            for k in range(V.ndim):
+                if V.dist.dims[k] > 1:
+                    self._axis_cart(k, src, X)
+                else:
+                    _lib.call("poms_kron_solve_axis", self._h, 3 - V.ndim + k, rt.ptr(src._data), rt.ptr(X._data), st)
+                src = X
+            X._mark_written()
+            return X
         if not V.is_distributed:
             _lib.call("poms_kron_solve", self._h, rt.ptr(Y._data), rt.ptr(X._data), st)
         else:
@@ -163,6 +180,66 @@ class KronSolver:
             k = n0l * (b - a) * n2
             Xi[:, a:b, :].copy_(back[off:off + k].view(n0l, b - a, n2))
             off += k
+
+    def _axis_cart(self, k: int, Y: StencilVector, X: StencilVector) -> None:
+        """Axis-k line solves of a Cart block (X may be Y): transpose inside the
+        line group, dense column solves, transpose back."""
+        from .dist import slab_bounds
+        V, D = self.V, self.V.dist
+        members = []
+        for r in range(D.dims[k]):   # the line group, in axis-k order (= global order of the pieces)
+            c = list(D.coords)
+            c[k] = r
+            members.append(D.rank_of(c))
+        me = D.coords[k]
+        Yi = V.interior(Y._data).movedim(k, 0)
+        nk = Yi.shape[0]
+        R = Yi[0].numel()                                     # local points on the other axes
+        parts = [slab_bounds(R, len(members), r) for r in range(len(members))]
+        flat = Yi.reshape(nk, R)
+        nks = [slab_bounds(V.npts[k], D.dims[k], r) for r in range(D.dims[k])]
+        lo, hi = parts[me]
+        m = hi - lo
+        # forward: to member r the columns parts[r] of my nk rows; from r its rows x my columns
+        sends = [flat[:, a:b].contiguous() for a, b in parts]
+        recvs = [torch.empty((e - s, m), dtype=F64, device=flat.device) for s, e in nks]
+        self._group_exchange(members, sends, recvs)
+        lines = torch.cat(recvs, dim=0).contiguous()          # (n_global_k, m)
+        if m > 0:
+            _lib.call("poms_kron_solve_lines_dense", self._h, 3 - V.ndim + k, rt.ptr(lines), rt.ptr(lines), m,
+                      rt.stream_handle())
+        # back: to member r its rows of my columns; from r my rows of its columns
+        backs = [lines[s:e].contiguous() for s, e in nks]
+        rets = [torch.empty((nk, b - a), dtype=F64, device=flat.device) for a, b in parts]
+        self._group_exchange(members, backs, rets)
+        Xi = V.interior(X._data).movedim(k, 0)
+        Xi.copy_(torch.cat(rets, dim=1).view(Xi.shape))
+
+    def _group_exchange(self, members, sends, recvs) -> None:
+        """sends[i] to members[i], recvs[i] from members[i] (own part copied locally):
+        point-to-point inside the line group, device buffers with nccl, host-staged
+        with gloo."""
+        import torch.distributed as dist
+        D = self.V.dist
+        staged = not D.cuda_transport and sends[0].device.type != "cpu"
+        ops, land = [], []
+        for i, r in enumerate(members):
+            if r == D.rank:
+                recvs[i].copy_(sends[i])
+                continue
+            sb = sends[i].cpu() if staged else sends[i]
+            rb = torch.empty(recvs[i].shape, dtype=recvs[i].dtype) if staged else recvs[i]
+            if sb.numel():
+                ops.append(dist.P2POp(dist.isend, sb, D._peer(r), D.group))
+            if rb.numel():
+                ops.append(dist.P2POp(dist.irecv, rb, D._peer(r), D.group))
+            if staged:
+                land.append((recvs[i], rb))
+        if ops:
+            for w in dist.batch_isend_irecv(ops):
+                w.wait()
+        for dst, src in land:
+            dst.copy_(src)
 
     def _a2a(self, out: torch.Tensor, inp: torch.Tensor, out_sizes, in_sizes) -> None:
         import torch.distributed as dist

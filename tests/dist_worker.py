@@ -426,12 +426,69 @@ def run_cart_gpu():
         check(e[3] == e[4] and e[5] == e[6], f"iteration counts {errs}")
 
 
+def run_cart_ksolve():
+    """Kronecker direct solve over a Cart block decomposition (every split axis
+    solved by line-group transposes, `sources/kron_product.py:119-170, 191-238`)
+    against the single-process oracle, and pcg_glt (`sources/solvers.py:239-306`)
+    over 2D blocks against the reference's golden iterates (tests/golden/pcg_glt.npz)."""
+    from poms_amd.dist import CartDistribution
+    from poms_amd.kron_solve import KronSolver
+    from poms_amd.solvers import pcg_glt
+    from poms_amd.splines import assemble_1d, make_open_knots
+    from poms_amd.stencil import KronOperator, StencilVectorSpace
+    torch.cuda.set_device(0)
+    dims = _cart_dims()
+    nd = len(dims)
+    rng = np.random.default_rng(29)
+    n = (13, 11, 9)[3 - nd:] if nd == 3 else (13, 11)
+    F = []
+    for m, kl, ku in zip(n, (2, 1, 3), (1, 3, 2)):
+        F.append(np.triu(np.tril(rng.uniform(-1, 1, (m, m)), ku), -kl) + 0.5 * np.eye(m))
+    yg = rng.standard_normal(n)
+    xg = orc.kron_solve(F, yg)
+    for p, align in ((2, False), (3, True)):
+        d = CartDistribution.from_process_group(n, dims)
+        V = StencilVectorSpace(list(n), [p] * nd, dist=d, align=align)
+        ks = KronSolver(V, F)
+        sl = tuple(slice(s, e) for s, e in zip(d.starts, d.ends))
+        y = V.zeros().from_numpy(yg)
+        x = ks.solve(y).to_local_numpy()
+        check(rel(x, xg[sl]) <= 1e-12, f"Cart kron solve p={p} {rel(x, xg[sl])}")
+        ks.solve(y, out=y)   # in place
+        check(rel(y.to_local_numpy(), xg[sl]) <= 1e-12, f"Cart kron solve in place p={p}")
+    if nd != 2:
+        return
+    z = np.load(Path(__file__).with_name("golden") / "pcg_glt.npz", allow_pickle=False)
+    cases = {}
+    for k in z.files:
+        case, field = k.split("__", 1)
+        cases.setdefault(case, {})[field] = z[k]
+    for name in ("p2_ne8", "p3_ne12"):
+        c = cases[name]
+        p, ne = int(c["p"]), int(c["ne"])
+        M, K = assemble_1d(make_open_knots(p, ne + p), p)
+        nn = ne + p
+        d = CartDistribution.from_process_group((nn, nn), dims)
+        V = StencilVectorSpace([nn, nn], [p, p], dist=d)
+        A = KronOperator.laplace(V, [M, M], [K, K])
+        b = V.zeros().from_numpy(c["b"].reshape(nn, nn))
+        for m in (1, 3):   # fixed iteration counts: the reference's iterates at 1e-9
+            x, info = pcg_glt(A, c["M1"], c["M2"], b, tol=0.0, maxiter=m)
+            got = torch.from_numpy(x.toarray())
+            dist.all_reduce(got)
+            check(info["niter"] == int(c[f"glt_m{m}_tol0_info"][0]), f"{name} m={m} niter")
+            check(rel(got.numpy(), c[f"glt_m{m}_tol0"]) <= 1e-9, f"{name} m={m}: {rel(got.numpy(), c[f'glt_m{m}_tol0'])}")
+        x, info = pcg_glt(A, c["M1"], c["M2"], b, tol=1e-8, maxiter=100)
+        check(info["niter"] == int(c["glt_test_info"][0]) and info["success"] == bool(c["glt_test_info"][1]),
+              f"{name}: converged niter {info['niter']} vs {c['glt_test_info']}")
+
+
 def main():
     mode = sys.argv[1]
     dist.init_process_group("gloo")
     try:
         {"cpu": run_cpu, "gpu": run_gpu, "gpu_ksolve": run_gpu_ksolve, "cart_cpu": run_cart_cpu,
-         "cart_gpu": run_cart_gpu}[mode]()
+         "cart_gpu": run_cart_gpu, "cart_ksolve": run_cart_ksolve}[mode]()
         dist.barrier()
         print(f"rank {dist.get_rank()} ok", flush=True)
     finally:

@@ -151,3 +151,14 @@ def test_four_rank_cart_operator_and_vcycle_gpu(dims):
     assert torch.cuda.device_count() >= 1, "GPU test selected but no GPU visible"
     world = int(np.prod([int(v) for v in dims.split("x")]))
     _launch("cart_gpu", world=world, timeout=600, extra_env={"POMS_TEST_CART_DIMS": dims})
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("dims", ["2x2", "2x2x1", "1x2x2", "2x2x2"])
+def test_cart_kron_solve_and_pcg_glt_gpu(dims):
+    """The Kronecker direct solve on Cart blocks (line-group transposes on every split
+    axis) vs the oracle; pcg_glt on a 2x2 grid vs the reference's golden iterates."""
+    import torch
+    assert torch.cuda.device_count() >= 1, "GPU test selected but no GPU visible"
+    world = int(np.prod([int(v) for v in dims.split("x")]))
+    _launch("cart_ksolve", world=world, timeout=600, extra_env={"POMS_TEST_CART_DIMS": dims})
