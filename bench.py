@@ -52,7 +52,10 @@ def parse():
                     help="MiB written between the isolated mat-vec launches (default 512 in 2D, 0 in 3D)")
     ap.add_argument("--coarse", type=int, default=8)
     ap.add_argument("--chunk", type=int, default=0)
-    ap.add_argument("--kron-reps", type=int, default=30)
+    ap.add_argument("--kron-reps", type=int, default=50, help="timed isolated applies")
+    ap.add_argument("--kron-warm", type=int, default=30,
+                    help="untimed applies before them: the apply's launch time falls from ~700 to ~530 us over "
+                         "its first ~30 back-to-back launches at 515^3 (profiles/r03/kb_launch_series.log)")
     ap.add_argument("--cpu-cells", type=int, default=160,
                     help="cells per axis of the CPU baseline's V-cycle sample (all nproc cores)")
     ap.add_argument("--cpu-cycles", type=int, default=2)
@@ -98,11 +101,20 @@ def main():
 
     nd = args.ndim
     n = args.cells + args.p
+    comm_note = None
     if world == 1:
         dd = None
     elif nd == 3:
-        # N > 1: the library's RCCL communicator, or an exception (no silent fall-back)
-        dd = SlabDistribution.from_process_group(n)
+        # N > 1: the library's RCCL communicator.  It has never run with peers on the
+        # builder's 1-GPU boxes: if it cannot be created or fails its self-test (every
+        # rank raises together, the test ends in a MIN all-reduce) the bench runs on the
+        # torch.distributed transport instead and SAYS so in "comm" / "comm_note".
+        try:
+            dd = SlabDistribution.from_process_group(n)
+        except Exception as e:   # noqa: BLE001 -- reported in the JSON line
+            comm_note = f"native RCCL communicator unavailable ({e!r:.300}); torch.distributed transport"
+            os.environ["POMS_NATIVE_COMM"] = "0"
+            dd = SlabDistribution.from_process_group(n)
     else:
         dd = CartDistribution.from_process_group((n, n))
     transport = dd.transport if dd is not None else "none"
@@ -167,7 +179,7 @@ def main():
     xv._mark_written()
     xv.update_ghost_regions()
     yk = mg.space.empty()
-    for _ in range(3):
+    for _ in range(max(3, args.kron_warm)):
         A.dot(xv, out=yk)
     flush = torch.empty(args.flush_mall * (1 << 17), dtype=torch.float64, device="cuda") if args.flush_mall else None
     barrier()
@@ -249,6 +261,7 @@ def main():
                 "parallelism": parallelism,
             },
             "comm": transport,
+            **({"comm_note": comm_note} if comm_note else {}),
             "roofline": {
                 "kernel": f"{KERNEL_NAMES.get(jac_v, f'variant {jac_v}')}<P={args.p},{nd}D,SUM,JACOBI> (Kron apply + damped-Jacobi update)",
                 "bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBPS, "unit": "GB/s",
@@ -260,7 +273,7 @@ def main():
                           "mall_flush_mib": args.flush_mall,
                           "achieved": kron_gbps, "unit": "GB/s", "frac": kron_gbps / HBM_PEAK_GBPS,
                           "median_launch_us": kron_s * 1e6, "mean_launch_us": kron_mean_s * 1e6,
-                          "bytes_per_dof": 16, "launches": args.kron_reps},
+                          "bytes_per_dof": 16, "launches": args.kron_reps, "untimed_warmup_launches": args.kron_warm},
             "cpu_baseline": cpu,
             "solver": {"info_pre": ipre, "info_pos": ipos},
         }

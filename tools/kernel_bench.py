@@ -32,6 +32,7 @@ def main():
     ap.add_argument("--variants", type=str, default="")
     ap.add_argument("--kinds", type=str, default="apply,jacobi")
     ap.add_argument("--json", type=str, default="")
+    ap.add_argument("--dump", action="store_true", help="print every launch time (us) of each row")
     ap.add_argument("--flush", action="store_true",
                     help="write a 512 MiB buffer before every timed launch (evicts L2 and the 256 MiB MALL)")
     a = ap.parse_args()
@@ -93,6 +94,7 @@ def main():
         med = statistics.median(ts)
         bpd = 16 if kind in ("apply", "dot", "from_zero") else 24
         row = {"chunk": ch, "tile_cols": tcols, "aligned": not a.no_align, "variant": var, "kind": kind, "median_us": med, "min_us": min(ts),
+               **({"launch_us": [round(t, 1) for t in ts]} if a.dump else {}),
                "GBps": bpd * dof / med / 1e3, "GDOFps": dof / med / 1e3}
         out.append(row)
         print(json.dumps(row), flush=True)
