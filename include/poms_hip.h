@@ -397,10 +397,15 @@ int poms_halo_finish(poms_comm* comm, void* stream);
  * wait_back: `stream` waits for the result, else it is ready on the
  * communication stream only.                                                  */
 int poms_allreduce_sum(poms_comm* comm, double* buf, int64_t count, void* stream, int wait_back);
-/* Lazily read global sums: a ring of device slots (2 doubles each).  A launch
- * reduces into poms_comm_slot's slot, poms_allreduce_to_host all-reduces it and
- * copies it to pinned host memory on the communication stream, poms_comm_wait
- * returns when the host copy is there.                                        */
+/* Lazily read global sums (values only the host reads: stop tests).  A ring of
+ * slots of 2 doubles in pinned, device-mapped host memory: a launch reduces the
+ * rank's local sum into poms_comm_slot's slot; poms_allreduce_to_host records the
+ * launch (queued on `stream`) and where the result goes; poms_comm_wait spins
+ * until the slot is written, sums it over the ranks ON THE HOST (node-local
+ * shared memory; the host transport's callback; RCCL synchronously when the
+ * ranks span nodes) and leaves the sums in host_dst.  Nothing is queued on the
+ * communication stream.  Every rank must wait on the same tickets in the same
+ * order (the sums are collective).                                            */
 int poms_comm_slot(poms_comm* comm, double** dev_slot, int* ticket);
 int poms_allreduce_to_host(poms_comm* comm, int ticket, int count, double* host_dst, void* stream);
 int poms_comm_wait(poms_comm* comm, int ticket);

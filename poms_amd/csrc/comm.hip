@@ -16,6 +16,14 @@
 
 #include <rccl/rccl.h>
 
+#include <fcntl.h>
+#include <sys/mman.h>
+#include <unistd.h>
+
+#include <atomic>
+#include <chrono>
+#include <cmath>
+#include <cstdlib>
 #include <cstring>
 #include <vector>
 
@@ -28,13 +36,33 @@ struct poms_comm {
     hipEvent_t ev_in = nullptr;     // caller's stream -> cs
     hipEvent_t ev_halo = nullptr;   // exchange done (cs -> caller)
     hipEvent_t ev_red = nullptr;    // all-reduce done (cs -> caller)
-    // ring of device scalar slots for lazily read global sums (damped-Jacobi
-    // norms): a launch reduces its partials into a slot, the slot is all-reduced
-    // and copied to pinned host memory on cs, and the host waits on the slot's event
+    // Ring of slots for global sums only the host reads (the damped-Jacobi norms,
+    // pcg's r.r): a launch's reduction kernel writes the rank's local sum straight
+    // into the slot -- pinned, coherent host memory mapped into the device -- and
+    // poms_comm_wait sums the ranks' values ON THE HOST (shared memory between the
+    // ranks of the node, or the host transport's callback).  No RCCL kernel, no copy
+    // and nothing on the communication stream, which then carries the ghost exchange
+    // alone: each such kernel used to wait for CUs behind the interior launch and
+    // hold up the next exchange (profiles/r03/proxy/).
     static constexpr int kRing = 16;
-    double* ring = nullptr;         // kRing x 2 doubles
-    hipEvent_t ring_ev[kRing] = {};
+    double* ring = nullptr;         // kRing x 2 doubles, host-coherent, device-mapped
+    hipEvent_t ring_ev[kRing] = {}; // after the launch that writes the slot
+    double* ring_dst[kRing] = {};   // where poms_comm_wait leaves the global sums
+    int ring_cnt[kRing] = {};
+    bool ring_done[kRing] = {};
     int ring_next = 0;
+    // node-local shared memory for the host-side sums (nullptr: not all ranks on this
+    // node -- the sums then go through RCCL synchronously)
+    struct ShmSlot {
+        std::atomic<uint64_t> seq;
+        double v[2];
+        char pad[64 - sizeof(std::atomic<uint64_t>) - 2 * sizeof(double)];
+    };
+    ShmSlot* shm = nullptr;         // [2][nranks]: round s uses half s & 1
+    size_t shm_bytes = 0;
+    uint64_t shm_seq = 0;
+    char shm_name[64] = {};
+    double* dev_tmp = nullptr;      // 2 doubles: the RCCL fall-back of the host sums
     // host transport (poms_comm_create_host): the same schedule with the data moved
     // by caller-supplied host callbacks (e.g. torch.distributed / gloo) instead of
     // RCCL -- every call synchronises the caller's stream, stages the planes or
@@ -56,6 +84,50 @@ struct poms_comm {
     } while (0)
 
 static hipStream_t cstream(void* s) { return reinterpret_cast<hipStream_t>(s); }
+
+namespace poms {
+int op_run_split(poms_op* op, int epilogue, double omega, const double* x, double* y, const double* b,
+                 int64_t ib, int64_t ie, int64_t b1s, int64_t b1e, int64_t b2s, int64_t b2e, double* norm_out,
+                 double* dot_out, int (*between)(void*), void* arg, void* stream);
+}
+
+static bool getenv_off(const char* name) {
+    const char* e = getenv(name);
+    return e && e[0] == '0';
+}
+
+// a NaN payload no reduction produces: "this slot has not been written yet"
+static constexpr uint64_t kUnset = 0x7ff8dead0000beefull;
+static void slot_arm(double* v) {
+    std::memcpy(v, &kUnset, sizeof(double));
+}
+static bool slot_unset(const double* v) {
+    uint64_t u;
+    std::memcpy(&u, const_cast<const double*>(reinterpret_cast<const volatile double*>(v)), sizeof(u));
+    return u == kUnset;
+}
+
+// Map the node-local shared-memory block of the communicator named by `id` and mark
+// this rank present.  Every rank calls this before ncclCommInitRank (a collective):
+// after it, all ranks of THIS node have marked themselves, and poms_comm_create
+// agrees over the ranks whether every rank found all the others.
+static void shm_open_block(poms_comm* c, const ncclUniqueId& id) {
+    uint64_t h = 1469598103934665603ull;   // FNV-1a of the unique id
+    for (size_t i = 0; i < sizeof(id); ++i) h = (h ^ (uint8_t)id.internal[i]) * 1099511628211ull;
+    char name[64];
+    snprintf(name, sizeof(name), "/poms_comm_%016llx", (unsigned long long)h);
+    c->shm_bytes = (size_t)(2 * c->nranks + 1) * sizeof(poms_comm::ShmSlot);
+    int fd = shm_open(name, O_CREAT | O_RDWR, 0600);
+    if (fd < 0) return;
+    if (ftruncate(fd, (off_t)c->shm_bytes) != 0) { close(fd); return; }
+    void* p = mmap(nullptr, c->shm_bytes, PROT_READ | PROT_WRITE, MAP_SHARED, fd, 0);
+    close(fd);
+    if (p == MAP_FAILED) return;
+    c->shm = static_cast<poms_comm::ShmSlot*>(p);
+    // the last slot's seq counts the ranks present (zero-filled by the first ftruncate)
+    reinterpret_cast<std::atomic<uint64_t>*>(&c->shm[2 * c->nranks].seq)->fetch_add(1);
+    snprintf(c->shm_name, sizeof(c->shm_name), "%s", name);
+}
 
 extern "C" {
 
@@ -81,11 +153,49 @@ int poms_comm_create(int device, const char* id, int rank, int nranks, poms_comm
     c->device = device;
     ncclUniqueId uid;
     std::memcpy(&uid, id, sizeof(uid));
-    ncclResult_t r = ncclCommInitRank(&c->comm, nranks, uid, rank);
+    if (nranks > 1 && !getenv_off("POMS_COMM_SHM")) shm_open_block(c, uid);
+    // POMS_COMM_CTAS caps the workgroups of every RCCL kernel of this communicator
+    // (ncclConfig_t::maxCTAs): an exchange overlapped with the interior launch takes
+    // CUs from it, and the p-plane message needs few of them (tuning knob; unset =
+    // RCCL's choice)
+    ncclConfig_t cfg = NCCL_CONFIG_INITIALIZER;
+    if (const char* e = getenv("POMS_COMM_CTAS")) {
+        const int n = atoi(e);
+        if (n > 0) cfg.minCTAs = cfg.maxCTAs = n;
+    }
+    ncclResult_t r = ncclCommInitRankConfig(&c->comm, nranks, uid, rank, &cfg);
+    if (c->shm && c->shm_name[0]) shm_unlink(c->shm_name);   // every rank of the node has it mapped now
     if (r != ncclSuccess) {
         set_error(std::string("ncclCommInitRank: ") + ncclGetErrorString(r));
+        if (c->shm) munmap(c->shm, c->shm_bytes);
         delete c;
         return 1;
+    }
+    if (nranks > 1 && !getenv_off("POMS_COMM_SHM")) {
+        // use the block only if EVERY rank found all nranks in it (one node) -- the
+        // same answer on every rank, so the host sums take one path everywhere; every
+        // rank added itself before entering the collective init above
+        const uint64_t present =
+            c->shm ? reinterpret_cast<std::atomic<uint64_t>*>(&c->shm[2 * nranks].seq)->load(std::memory_order_acquire)
+                   : 0;
+        int local_all = present == (uint64_t)nranks ? 1 : 0;
+        int* dflag = nullptr;
+        bool ok = hipMalloc(reinterpret_cast<void**>(&dflag), sizeof(int)) == hipSuccess &&
+                  hipMemcpy(dflag, &local_all, sizeof(int), hipMemcpyHostToDevice) == hipSuccess &&
+                  ncclAllReduce(dflag, dflag, 1, ncclInt32, ncclMin, c->comm, nullptr) == ncclSuccess &&
+                  hipMemcpy(&local_all, dflag, sizeof(int), hipMemcpyDeviceToHost) == hipSuccess;
+        if (dflag) (void)hipFree(dflag);
+        if (!ok) {
+            set_error("poms_comm_create: the shared-memory agreement all-reduce failed");
+            if (c->shm) munmap(c->shm, c->shm_bytes);
+            c->shm = nullptr;
+            poms_comm_destroy(c);
+            return 1;
+        }
+        if (!local_all && c->shm) {
+            munmap(c->shm, c->shm_bytes);
+            c->shm = nullptr;
+        }
     }
     if (comm_common_init(c)) {
         poms_comm_destroy(c);
@@ -96,14 +206,24 @@ int poms_comm_create(int device, const char* id, int rank, int nranks, poms_comm
 }
 
 static int comm_common_init(poms_comm* c) {
-    if (hipStreamCreateWithFlags(&c->cs, hipStreamNonBlocking) != hipSuccess ||
+    // The communication stream gets the highest priority: HIP then gives it a hardware
+    // queue of its own.  A normal-priority stream may share the compute stream's
+    // queue (GPU_MAX_HW_QUEUES = 4), and a shared queue runs the exchange between
+    // the compute launches instead of beside them -- rocprofv3 showed every RCCL
+    // kernel serialised with the interior launch it was meant to overlap
+    // (profiles/r03/proxy/).
+    int least = 0, greatest = 0;
+    if (hipDeviceGetStreamPriorityRange(&least, &greatest) != hipSuccess ||
+        hipStreamCreateWithPriority(&c->cs, hipStreamNonBlocking, greatest) != hipSuccess ||
         hipEventCreateWithFlags(&c->ev_in, hipEventDisableTiming) != hipSuccess ||
         hipEventCreateWithFlags(&c->ev_halo, hipEventDisableTiming) != hipSuccess ||
         hipEventCreateWithFlags(&c->ev_red, hipEventDisableTiming) != hipSuccess) {
         set_error("poms_comm_create: stream / event creation failed");
         return 1;
     }
-    bool ok = hipMalloc(reinterpret_cast<void**>(&c->ring), poms_comm::kRing * 2 * sizeof(double)) == hipSuccess;
+    bool ok = hipHostMalloc(reinterpret_cast<void**>(&c->ring), poms_comm::kRing * 2 * sizeof(double),
+                            hipHostMallocMapped | hipHostMallocCoherent) == hipSuccess &&
+              hipMalloc(reinterpret_cast<void**>(&c->dev_tmp), 2 * sizeof(double)) == hipSuccess;
     for (int i = 0; ok && i < poms_comm::kRing; ++i)
         ok = hipEventCreateWithFlags(&c->ring_ev[i], hipEventDisableTiming) == hipSuccess;
     if (!ok) {
@@ -160,7 +280,9 @@ int poms_comm_destroy(poms_comm* c) {
         if (e) (void)hipEventDestroy(e);
     for (hipEvent_t e : c->ring_ev)
         if (e) (void)hipEventDestroy(e);
-    if (c->ring) (void)hipFree(c->ring);
+    if (c->ring) (void)hipHostFree(c->ring);
+    if (c->dev_tmp) (void)hipFree(c->dev_tmp);
+    if (c->shm) munmap(c->shm, c->shm_bytes);
     if (c->cs) (void)hipStreamDestroy(c->cs);
     delete c;
     return 0;
@@ -254,43 +376,96 @@ int poms_allreduce_sum(poms_comm* c, double* buf, int64_t count, void* stream, i
     return 0;
 }
 
-// Next ring slot (2 device doubles) for a lazily read global sum; waits for the
-// slot's previous use to finish first.
+// Next ring slot (2 doubles of pinned, device-mapped host memory, armed unset) for
+// a global sum only the host reads.  A slot is re-armed only after the launch that
+// last wrote it is complete (its event): an abandoned launch may still write it.
 int poms_comm_slot(poms_comm* c, double** dev_slot, int* ticket) {
     if (!c || !dev_slot || !ticket) { set_error("poms_comm_slot: null argument"); return 1; }
     const int t = c->ring_next;
     c->ring_next = (t + 1) % poms_comm::kRing;
     POMS_HIP_CHECK(hipEventSynchronize(c->ring_ev[t]));
+    slot_arm(c->ring + 2 * t);
+    slot_arm(c->ring + 2 * t + 1);
+    c->ring_dst[t] = nullptr;
+    c->ring_cnt[t] = 0;
+    c->ring_done[t] = false;
     *dev_slot = c->ring + 2 * t;
     *ticket = t;
     return 0;
 }
 
-// All-reduce `count` (<= 2) doubles of ring slot `ticket` in place and copy them
-// to `host_dst` (pinned), both on the communication stream after the work queued
-// on `stream`; poms_comm_wait(ticket) returns when host_dst holds the sums.
+// The launch writing ring slot `ticket` (`count` <= 2 local sums) is queued on
+// `stream`; poms_comm_wait(ticket) leaves the global sums in host_dst.
 int poms_allreduce_to_host(poms_comm* c, int ticket, int count, double* host_dst, void* stream) {
     if (!c || !host_dst || ticket < 0 || ticket >= poms_comm::kRing || count < 1 || count > 2) {
         set_error("poms_allreduce_to_host: bad argument");
         return 1;
     }
-    double* slot = c->ring + 2 * ticket;
-    if (c->host) {   // synchronous: host_dst holds the sums on return
-        if (host_allreduce(c, slot, count, cstream(stream))) return 1;
-        POMS_HIP_CHECK(hipMemcpy(host_dst, slot, count * sizeof(double), hipMemcpyDeviceToHost));
-        // the ticket's event on the communication stream, ordered after the caller's
-        // stream, as on the RCCL path (work queued on poms_comm_stream after this call
-        // is then ordered after the result)
-        POMS_HIP_CHECK(hipEventRecord(c->ev_in, cstream(stream)));
-        POMS_HIP_CHECK(hipStreamWaitEvent(c->cs, c->ev_in, 0));
-        POMS_HIP_CHECK(hipEventRecord(c->ring_ev[ticket], c->cs));
-        return 0;
+    c->ring_dst[ticket] = host_dst;
+    c->ring_cnt[ticket] = count;
+    POMS_HIP_CHECK(hipEventRecord(c->ring_ev[ticket], cstream(stream)));
+    return 0;
+}
+
+// Sum `cnt` doubles over the ranks, on the host: every rank publishes its values in
+// the half of the block this round uses and adds all ranks' values in rank order
+// (the same sum, bit for bit, on every rank).  Two halves suffice: a rank starts
+// round s + 2 only after every rank published round s + 1, i.e. finished reading s.
+static int shm_allsum(poms_comm* c, double* v, int cnt) {
+    const uint64_t s = ++c->shm_seq;
+    poms_comm::ShmSlot* half = c->shm + (s & 1) * c->nranks;
+    poms_comm::ShmSlot& mine = half[c->rank];
+    for (int i = 0; i < cnt; ++i) mine.v[i] = v[i];
+    mine.seq.store(s, std::memory_order_release);
+    double acc[2] = {0.0, 0.0};
+    auto t0 = std::chrono::steady_clock::now();
+    for (int r = 0; r < c->nranks; ++r) {
+        for (long n = 1; half[r].seq.load(std::memory_order_acquire) < s; ++n) {
+            __builtin_ia32_pause();
+            if ((n & 65535) == 0 && std::chrono::steady_clock::now() - t0 > std::chrono::seconds(120)) {
+                set_error("poms_comm_wait: a rank did not publish its sum within 120 s");
+                return 1;
+            }
+        }
+        for (int i = 0; i < cnt; ++i) acc[i] += half[r].v[i];
     }
-    POMS_HIP_CHECK(hipEventRecord(c->ev_in, cstream(stream)));
-    POMS_HIP_CHECK(hipStreamWaitEvent(c->cs, c->ev_in, 0));
-    POMS_NCCL_CHECK(ncclAllReduce(slot, slot, (size_t)count, ncclDouble, ncclSum, c->comm, c->cs));
-    POMS_HIP_CHECK(hipMemcpyAsync(host_dst, slot, count * sizeof(double), hipMemcpyDeviceToHost, c->cs));
-    POMS_HIP_CHECK(hipEventRecord(c->ring_ev[ticket], c->cs));
+    for (int i = 0; i < cnt; ++i) v[i] = acc[i];
+    return 0;
+}
+
+int poms_comm_wait(poms_comm* c, int ticket) {
+    if (!c || ticket < 0 || ticket >= poms_comm::kRing) { set_error("poms_comm_wait: bad argument"); return 1; }
+    if (c->ring_done[ticket]) return 0;
+    const int cnt = c->ring_cnt[ticket];
+    if (cnt < 1 || !c->ring_dst[ticket]) { set_error("poms_comm_wait: ticket has no pending sum"); return 1; }
+    double* slot = c->ring + 2 * ticket;
+    // spin on the slot (the reduction kernel's store lands ~1 us after it ends; an
+    // event wake-up costs ~15 us), checking now and then that the launch is alive
+    for (int i = 0; i < cnt; ++i) {
+        for (long n = 1; slot_unset(slot + i); ++n) {
+            __builtin_ia32_pause();
+            if ((n & 4095) == 0 && hipEventQuery(c->ring_ev[ticket]) != hipErrorNotReady) {
+                std::atomic_thread_fence(std::memory_order_seq_cst);
+                if (slot_unset(slot + i)) { set_error("poms_comm_wait: the launch did not write its sum"); return 1; }
+            }
+        }
+    }
+    std::atomic_thread_fence(std::memory_order_acquire);
+    double v[2] = {slot[0], cnt > 1 ? slot[1] : 0.0};
+    if (c->nranks > 1) {
+        if (c->host) {
+            if (c->ar(c->user, v, cnt)) { set_error("host transport: all-reduce callback failed"); return 1; }
+        } else if (c->shm) {
+            if (shm_allsum(c, v, cnt)) return 1;
+        } else {   // ranks on several nodes: through RCCL, synchronously
+            POMS_HIP_CHECK(hipMemcpyAsync(c->dev_tmp, v, cnt * sizeof(double), hipMemcpyHostToDevice, c->cs));
+            POMS_NCCL_CHECK(ncclAllReduce(c->dev_tmp, c->dev_tmp, (size_t)cnt, ncclDouble, ncclSum, c->comm, c->cs));
+            POMS_HIP_CHECK(hipMemcpyAsync(v, c->dev_tmp, cnt * sizeof(double), hipMemcpyDeviceToHost, c->cs));
+            POMS_HIP_CHECK(hipStreamSynchronize(c->cs));
+        }
+    }
+    for (int i = 0; i < cnt; ++i) c->ring_dst[ticket][i] = v[i];
+    c->ring_done[ticket] = true;
     return 0;
 }
 
@@ -320,11 +495,16 @@ int poms_op_run_dist(poms_op* op, poms_comm* c, int epilogue, double omega, cons
     }
     if (exchange && n_local > 2 * pmax) {
         if (poms_halo_start(c, xplanes, plane_elems, n_local, pad, pmax, prev, next, stream)) return 1;
-        if (poms_op_run_reduce2(op, epilogue, omega, x, y, b, pmax, n_local - pmax, 0, 0, nout, dout, 0, stream))
-            return 1;
-        if (poms_halo_finish(c, stream)) return 1;
-        if (poms_op_run_reduce2(op, epilogue, omega, x, y, b, 0, pmax, n_local - pmax, n_local, nout, dout, 1,
-                                stream))
+        struct Finish {
+            poms_comm* c;
+            void* stream;
+            static int run(void* a) {
+                auto* f = static_cast<Finish*>(a);
+                return poms_halo_finish(f->c, f->stream);
+            }
+        } fin{c, stream};
+        if (op_run_split(op, epilogue, omega, x, y, b, pmax, n_local - pmax, 0, pmax, n_local - pmax, n_local, nout,
+                         dout, &Finish::run, &fin, stream))
             return 1;
     } else {
         if (exchange) {
@@ -340,10 +520,5 @@ int poms_op_run_dist(poms_op* op, poms_comm* c, int epilogue, double omega, cons
     return 0;
 }
 
-int poms_comm_wait(poms_comm* c, int ticket) {
-    if (!c || ticket < 0 || ticket >= poms_comm::kRing) { set_error("poms_comm_wait: bad argument"); return 1; }
-    POMS_HIP_CHECK(hipEventSynchronize(c->ring_ev[ticket]));
-    return 0;
-}
 
 }  // extern "C"

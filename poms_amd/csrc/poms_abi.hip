@@ -71,6 +71,10 @@ struct poms_ctx {
 
 struct poms_op {
     poms_ctx* ctx = nullptr;
+    // where a launch writes its per-block partials: norms at scratch + part_off, dots
+    // at scratch + (dot_base < 0 ? nblk : dot_base) + part_off (op_run_split puts two
+    // launches' partials side by side and reduces them once)
+    int64_t part_off = 0, dot_base = -1;
     int ndim = 3, form = FORM_SUM, pmax = 1, chunk = 0, tout = 0;
     poms_layout L{};
     int64_t g0 = 0, n0g = 1;
@@ -84,10 +88,9 @@ struct poms_op {
     ToepConst tc{};
     double* coef = nullptr;   // FORM_STENCIL: (2p+1)^d coefficient planes of the owned rows
     int sp[3]{};              // FORM_STENCIL: stencil half-widths per axis
-    // native pcg loop (poms_pcg_jacobi): device scalars, their pinned host copies, events
+    // native pcg loop (poms_pcg_jacobi): device scalars and the pinned host slots
     double* sv_dev = nullptr;
     double* sv_host = nullptr;
-    hipEvent_t sv_ev[8]{};
     // poms_pcg_jacobi, one rank: ring of pinned host slots the reduction kernels
     // write the host-read norms into.  sv_seq[i] = launch sequence number that armed
     // slot i (-1: never); every launch numbered below sv_done is known complete (a
@@ -492,8 +495,6 @@ int poms_op_destroy(poms_op* o) {
     for (double* p : {o->a0t, o->b0t, o->a1, o->b1, o->a2, o->b2, o->dg2a, o->dg2b, o->rdiag0, o->coef, o->sv_dev})
         if (p) (void)hipFree(p);
     if (o->sv_host) (void)hipHostFree(o->sv_host);
-    for (hipEvent_t e : o->sv_ev)
-        if (e) (void)hipEventDestroy(e);
     for (auto& t : o->tl) {
         (void)hipEventDestroy(t.e0);
         (void)hipEventDestroy(t.e1);
@@ -722,9 +723,15 @@ static int op_run(poms_op* o, int epi, double omega, const double* x, double* y,
     if (op_geom(o, zb, ze, g, v, v5_to, zb2, ze2, epi)) return 1;
     const int64_t nblk = (int64_t)g.tiles2 * g.tiles1 * g.nchunks;
     if (nblk == 0) { o->last_partials = 0; return 0; }
-    if ((want_norm || want_dot) && 2 * nblk > kScratch) { set_error("too many blocks for the partial-sum scratch"); return 1; }
+    const int64_t dbase = o->dot_base < 0 ? nblk : o->dot_base;
+    if ((want_norm || want_dot) &&
+        (o->part_off + nblk > dbase || dbase + o->part_off + nblk > kScratch)) {
+        set_error("too many blocks for the partial-sum scratch");
+        return 1;
+    }
     KronPtrs p{x, y, b, o->a0t, o->b0t, o->a1, o->b1, o->a2, o->b2,
-               want_norm ? o->ctx->scratch : nullptr, want_dot ? o->ctx->scratch + nblk : nullptr, o->rdiag0};
+               want_norm ? o->ctx->scratch + o->part_off : nullptr,
+               want_dot ? o->ctx->scratch + dbase + o->part_off : nullptr, o->rdiag0};
     poms_op::TimedLaunch* tlh = nullptr;
     if (o->timing && (o->t_epi < 0 || o->t_epi == epi) && (o->t_seen++ % o->t_every) == 0) {
         // events on the launch stream around this launch (a sample: every t_every-th)
@@ -832,11 +839,12 @@ int poms_op_set_ghost_corners(poms_op* op, int yes) {
 
 // One launch plus its reductions (one host call instead of three); the launch
 // may cover a second plane range [zb2, ze2) (the slab's other boundary).
-int poms_op_run_reduce2(poms_op* op, int epilogue, double omega, const double* x, double* y,
-                        const double* b, int64_t zb, int64_t ze, int64_t zb2, int64_t ze2,
-                        double* norm_out, double* dot_out, int accumulate, void* stream) {
-    if (!op) { set_error("poms_op_run_reduce: null operator"); return 1; }
-    const bool wn = norm_out != nullptr, wd = dot_out != nullptr;
+}  // extern "C"
+
+// One launch of `epilogue` over planes [zb, ze) + [zb2, ze2), its partials written
+// where op->part_off / dot_base say; the argument checks of poms_op_run_reduce2.
+static int op_run_epi(poms_op* op, int epilogue, double omega, const double* x, double* y, const double* b,
+                      int64_t zb, int64_t ze, int64_t zb2, int64_t ze2, bool wn, bool wd, void* stream) {
     switch (epilogue) {
         case EPI_APPLY:
             if (wn || wd) { set_error("poms_op_run_reduce: apply has no reductions"); return 1; }
@@ -865,6 +873,53 @@ int poms_op_run_reduce2(poms_op* op, int epilogue, double omega, const double* x
             set_error("poms_op_run_reduce: bad epilogue");
             return 1;
     }
+    return 0;
+}
+
+namespace poms {
+// The distributed operator call's two launches -- planes [ib, ie) first, then
+// `between` (the wait for the ghost exchange), then the boundary ranges [b1s, b1e) +
+// [b2s, b2e) -- with both launches' partials side by side in the scratch and ONE
+// reduction per requested sum after the second launch (one launch fewer per sum
+// than reducing each launch; poms_op_run_dist).
+int op_run_split(poms_op* op, int epilogue, double omega, const double* x, double* y, const double* b,
+                 int64_t ib, int64_t ie, int64_t b1s, int64_t b1e, int64_t b2s, int64_t b2e, double* norm_out,
+                 double* dot_out, int (*between)(void*), void* arg, void* stream) {
+    if (!op) { set_error("op_run_split: null operator"); return 1; }
+    if (op->form == FORM_STENCIL) {   // its own partials layout: reduce each launch
+        if (poms_op_run_reduce2(op, epilogue, omega, x, y, b, ib, ie, 0, 0, norm_out, dot_out, 0, stream)) return 1;
+        if (between && between(arg)) return 1;
+        return poms_op_run_reduce2(op, epilogue, omega, x, y, b, b1s, b1e, b2s, b2e, norm_out, dot_out, 1, stream);
+    }
+    const bool wn = norm_out != nullptr, wd = dot_out != nullptr;
+    struct Reset {
+        poms_op* o;
+        ~Reset() { o->part_off = 0; o->dot_base = -1; }
+    } reset{op};
+    op->part_off = 0;
+    op->dot_base = kScratch / 2;
+    if (op_run_epi(op, epilogue, omega, x, y, b, ib, ie, 0, 0, wn, wd, stream)) return 1;
+    const int64_t n1 = op->last_partials;
+    if (between && between(arg)) return 1;
+    op->part_off = n1;
+    if (op_run_epi(op, epilogue, omega, x, y, b, b1s, b1e, b2s, b2e, wn, wd, stream)) return 1;
+    const int64_t n = n1 + op->last_partials;
+    op->last_partials = 0;   // not in the layout poms_op_last_partials describes
+    if (wn) reduce_launch(op->ctx->scratch, (int)n, norm_out, as_stream(stream));
+    if (wd) reduce_launch(op->ctx->scratch + kScratch / 2, (int)n, dot_out, as_stream(stream));
+    POMS_HIP_CHECK(hipGetLastError());
+    return 0;
+}
+}  // namespace poms
+
+extern "C" {
+
+int poms_op_run_reduce2(poms_op* op, int epilogue, double omega, const double* x, double* y,
+                        const double* b, int64_t zb, int64_t ze, int64_t zb2, int64_t ze2,
+                        double* norm_out, double* dot_out, int accumulate, void* stream) {
+    if (!op) { set_error("poms_op_run_reduce: null operator"); return 1; }
+    const bool wn = norm_out != nullptr, wd = dot_out != nullptr;
+    if (op_run_epi(op, epilogue, omega, x, y, b, zb, ze, zb2, ze2, wn, wd, stream)) return 1;
     const int64_t n = op->last_partials;
     if (wn) reduce_launch(op->ctx->scratch, (int)n, norm_out, as_stream(stream), accumulate);
     if (wd) reduce_launch(op->ctx->scratch + n, (int)n, dot_out, as_stream(stream), accumulate);
@@ -1486,9 +1541,8 @@ int poms_kron_solve_bnd_3d(poms_ctx* ctx, const double* A_bnd, int64_t lda, int 
 // (the GPU never waits for the host while the host waits for that norm).
 namespace {
 
-enum { SC_SR = 0, SC_PQ = 1, SC_ONE = 2, SC_ALPHA = 3, SC_ALPHA2 = 4, SC_BETA = 5, SC_SRN = 6, SC_RR = 7,
-       SC_RR0 = 8, SC_J0 = 9 /* 9, 10: ||x1||^2, ||dr2||^2 */, SC_JN = 11 /* 11, 12: sweep norm ring */,
-       SC_N = 16 };
+// device scalars (the sums only the host reads live in host slots / comm ring slots)
+enum { SC_SR = 0, SC_PQ = 1, SC_ONE = 2, SC_ALPHA = 3, SC_ALPHA2 = 4, SC_BETA = 5, SC_SRN = 6, SC_N = 16 };
 enum { H_RR0 = 0, H_RR = 1, H_J0 = 2 /* 2 slots */, H_JN = 4 /* 2 slots */ };
 
 __global__ void pcg_scalars_kernel(double* sc, int mode) {
@@ -1524,14 +1578,32 @@ struct PcgRun {
         }
         return poms_op_run_reduce2(op, epi, o->omega, x, y, b, 0, n0, 0, 0, nrm, dot, 0, stv);
     }
+    int tk[poms_op::kSvRing] = {};   // with a communicator: the ring ticket of host slot h
+    // a sum the device needs (alpha, beta): all-reduced, the compute stream waits
     int allsum(double* d, int cnt) { return comm ? poms_allreduce_sum(comm, d, cnt, stv, 1) : 0; }
-    // A value the host reads: one rank -- the reduction kernel writes it straight
+    // A value only the host reads: one rank -- the reduction kernel writes it straight
     // into the pinned (coherent, device-mapped) host slot, armed with a sentinel the
     // host spins on (~1-2 us after the kernel instead of an event wake-up, ~15 us:
-    // profiles/r02/sync_probe.log); with a communicator -- device scalar,
-    // all-reduce, copy and event (fixed slots h: stream order covers those).
+    // profiles/r02/sync_probe.log); with a communicator -- a ring slot of the
+    // communicator, all-reduced and copied to the host slot on the communication
+    // stream while the compute stream goes on (lazy_post; the compute stream used to
+    // wait for that all-reduce and copy, ~40 us per sweep in profiles/r03/proxy/).
     bool direct() const { return comm == nullptr; }
-    double* hdst(int sc_idx, int h) { return direct() ? host + h : sc + sc_idx; }
+    double* hslot(int h) {
+        if (direct()) return host + h;
+        double* d = nullptr;
+        if (poms_comm_slot(comm, &d, &tk[h])) return nullptr;
+        return d;
+    }
+    int lazy_post(int h, int cnt) { return direct() ? 0 : poms_allreduce_to_host(comm, tk[h], cnt, host + h, stv); }
+    // an operator launch whose sums only the host reads: [dot, norm] from host slot h
+    int jrun(int epi, const double* x, double* y, const double* b, bool wn, bool wd, int h) {
+        if (direct()) return run(epi, x, y, b, wn ? host + h + (wd ? 1 : 0) : nullptr, wd ? host + h : nullptr);
+        const RowGeom g = row_geom(&op->L);
+        return poms_op_run_dist(op, comm, epi, o->omega, x, y, b, const_cast<double*>(x), g.s0, op->L.n[0],
+                                (int)op->L.pads[0], op->pmax, o->prev, o->next, 1, wn ? 1 : 0, wd ? 1 : 0, nullptr,
+                                nullptr, (wn ? 1 : 0) + (wd ? 1 : 0), host + h, &tk[h], stv);
+    }
     // Arm `cnt` consecutive host slots for the next launch and return the first.
     // Direct mode takes fresh slots from a ring: a launch the loop abandoned (an
     // early damped-Jacobi stop leaves the next sweep queued) still writes ITS slot
@@ -1556,15 +1628,9 @@ struct PcgRun {
         ++op->sv_seq_next;
         return h;
     }
-    int post(int sc_idx, int cnt, int h) {   // device scalars -> pinned host slot, event after the copy
-        if (direct()) return 0;
-        POMS_HIP_CHECK(hipMemcpyAsync(host + h, sc + sc_idx, cnt * sizeof(double), hipMemcpyDeviceToHost, st));
-        POMS_HIP_CHECK(hipEventRecord(op->sv_ev[h], st));
-        return 0;
-    }
     double get(int h, int i = 0) {
         if (!direct()) {
-            (void)hipEventSynchronize(op->sv_ev[h]);
+            if (poms_comm_wait(comm, tk[h])) return std::nan("");
             return host[h + i];
         }
         const volatile double* v = reinterpret_cast<const volatile double*>(host) + h + i;
@@ -1583,10 +1649,12 @@ struct PcgRun {
         if (poms_vec_dot(op->ctx, &op->L, a, b, dst, stv)) return 1;
         return allsum(dst, 1);
     }
-    int diag_scale_norm(const double* b, double* x, double* dst) {   // x = omega b / diag, ||x||^2
+    int diag_scale_norm(const double* b, double* x, int h) {   // x = omega b / diag, ||x||^2 -> host slot h
         if (poms_op_diag_scale(op, o->omega, b, x, 1, stv)) return 1;
-        reduce_launch(op->ctx->scratch, (int)op->last_partials, dst, st);
-        return allsum(dst, 1);
+        double* d = hslot(h);
+        if (!d) return 1;
+        reduce_launch(op->ctx->scratch, (int)op->last_partials, d, st);
+        return lazy_post(h, 1);
     }
 
     // damped_jacobi(A, rhs) with x0 = None into buffers {A, B}; the last sweep also
@@ -1602,14 +1670,13 @@ struct PcgRun {
         if (op->ndim == 3 && maxit >= 2 && maxit != 2 && op->form != FORM_STENCIL) (void)poms_op_from_zero_supported(op, &fz);
         if (fz) {   // sweeps 1, 2 from x = 0 in one pass over rhs
             h0 = arm(H_J0, 2);
-            if (run(EPI_JACOBI0, rhs, A, rhs, hdst(SC_J0 + 1, h0 + 1), hdst(SC_J0, h0))) return 1;
-            if (allsum(hdst(SC_J0, h0), 2) || post(SC_J0, 2, h0)) return 1;
+            if (jrun(EPI_JACOBI0, rhs, A, rhs, true, true, h0)) return 1;   // [||x1||^2, ||dr2||^2]
             pend = 2;
             k0 = 3;
         } else {
             if (maxit < 1) { set_error("pcg: jacobi maxiter < 1"); return 1; }
             pend_h = arm(H_JN, 1);
-            if (diag_scale_norm(rhs, A, hdst(SC_JN, pend_h)) || post(SC_JN, 1, pend_h)) return 1;
+            if (diag_scale_norm(rhs, A, pend_h)) return 1;
             pend = 1;
             ring = 1;
             k0 = 2;
@@ -1639,9 +1706,7 @@ struct PcgRun {
                 if (run(EPI_JACOBI, x, xn, rhs, nullptr, sc + dot_idx) || allsum(sc + dot_idx, 1)) return 1;
             } else {
                 h = arm(H_JN + ring, 1);
-                if (run(EPI_JACOBI, x, xn, rhs, hdst(SC_JN + ring, h), nullptr) || allsum(hdst(SC_JN + ring, h), 1) ||
-                    post(SC_JN + ring, 1, h))
-                    return 1;
+                if (jrun(EPI_JACOBI, x, xn, rhs, true, false, h)) return 1;
                 ring ^= 1;
             }
             if (pend) {   // stop test of the previous sweep, read after this one is queued
@@ -1683,7 +1748,6 @@ int poms_pcg_jacobi(poms_op* op, poms_comm* comm, const poms_pcg_opts* o, const 
         POMS_HIP_CHECK(hipHostMalloc(reinterpret_cast<void**>(&op->sv_host), poms_op::kSvRing * sizeof(double),
                                      hipHostMallocMapped | hipHostMallocCoherent));
         for (int64_t& q : op->sv_seq) q = -1;
-        for (hipEvent_t& e : op->sv_ev) POMS_HIP_CHECK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
     }
     PcgRun R{op, comm, o, as_stream(stream), stream, op->sv_dev, op->sv_host};
     R.n0 = op->ndim == 3 ? op->L.n[0] : 1;
@@ -1698,7 +1762,10 @@ int poms_pcg_jacobi(poms_op* op, poms_comm* comm, const poms_pcg_opts* o, const 
         return 1;
     }
     const int hrr0 = R.arm(H_RR0, 1);
-    if (R.dot(r, r, R.hdst(SC_RR0, hrr0)) || R.post(SC_RR0, 1, hrr0)) return 1;
+    {
+        double* d = R.hslot(hrr0);
+        if (!d || poms_vec_dot(ctx, L, r, r, d, stream) || R.lazy_post(hrr0, 1)) return 1;
+    }
     const double nrmr0 = std::sqrt(R.get(hrr0));
     double* s = nullptr;
     int dd = 0;
@@ -1715,8 +1782,8 @@ int poms_pcg_jacobi(poms_op* op, poms_comm* comm, const poms_pcg_opts* o, const 
         if (R.run(EPI_APPLYDOT, p, q, p, nullptr, R.sc + SC_PQ) || R.allsum(R.sc + SC_PQ, 1)) return 1;
         hipLaunchKernelGGL(pcg_scalars_kernel, dim3(1), dim3(64), 0, R.st, R.sc, 0);
         const int hrr = R.arm(H_RR, 1);
-        if (poms_pcg_r_update_dev(ctx, L, R.sc + SC_ALPHA, r, q, R.hdst(SC_RR, hrr), stream) ||
-            R.allsum(R.hdst(SC_RR, hrr), 1) || R.post(SC_RR, 1, hrr))
+        double* drr = R.hslot(hrr);
+        if (!drr || poms_pcg_r_update_dev(ctx, L, R.sc + SC_ALPHA, r, q, drr, stream) || R.lazy_post(hrr, 1))
             return 1;
         double* sn = nullptr;
         if (R.damped_jacobi(r, fa, fb, SC_SRN, &sn, &dd)) return 1;   // queued before the read

@@ -81,14 +81,33 @@ class SlabDistribution:
             d.native = NativeComm.create(group)
         return d
 
+    @classmethod
+    def loopback(cls, n0_global: int, rank: int, world: int) -> "SlabDistribution":
+        """Rank ``rank``'s slab of a ``world``-rank split, run ALONE on this GPU, its
+        halo exchanges and sums going through a one-rank RCCL communicator: every
+        exchange sends the slab's boundary planes to itself (the ghosts then hold the
+        slab's own planes, not a neighbour's) and every all-reduce is a one-rank RCCL
+        call.  A timing proxy for one rank of the N-GPU run (``tools/slab_proxy.py``):
+        that rank's kernels, exchanges and sums on the production schedule, with
+        RCCL's on-device copy in place of the xGMI transfer.  Its results are not
+        the global problem's."""
+        d = cls(n0_global, rank, world, None, cuda_transport=True, device_reductions=True)
+        d.native = NativeComm.create_loopback()
+        d.prev = 0 if d.prev is not None else None   # the communicator's only rank
+        d.next = 0 if d.next is not None else None
+        return d
+
     @property
     def transport(self) -> str:
         """Which path moves ghosts and sums: "native" (RCCL from C), "native-host"
-        (the C schedule over host callbacks), "torch" (torch.distributed) or "none"."""
+        (the C schedule over host callbacks), "native-loopback" (:meth:`loopback`),
+        "torch" (torch.distributed) or "none"."""
         if self.world == 1:
             return "none"
         if self.native is None:
             return "torch"
+        if self.native.is_loopback:
+            return "native-loopback"
         return "native-host" if self.native.is_host else "native"
 
     # ------------------------------------------------------------------
@@ -328,6 +347,7 @@ class NativeComm:
         self.h = handle
         self.device = device
         self._callbacks = callbacks   # host transport: keep the ctypes thunks alive
+        self.is_loopback = False
         s = C.c_void_p()
         _lib.call("poms_comm_stream", self.h, C.byref(s))
         self.stream = torch.cuda.ExternalStream(s.value, device=torch.device("cuda", device))
@@ -355,6 +375,22 @@ class NativeComm:
                   dist.get_world_size(group), C.byref(h))
         comm = cls(h, dev)
         comm._check_self_test(group)
+        return comm
+
+    @classmethod
+    def create_loopback(cls):
+        """A one-rank RCCL communicator on the current GPU (no process group); see
+        :meth:`SlabDistribution.loopback`."""
+        import ctypes as C
+        from . import _lib
+        dev = torch.cuda.current_device()
+        nb = _lib.lib.poms_comm_id_bytes()
+        buf = C.create_string_buffer(nb)
+        _lib.call("poms_comm_unique_id", buf, nb)
+        h = C.c_void_p()
+        _lib.call("poms_comm_create", dev, buf, 0, 1, C.byref(h))
+        comm = cls(h, dev)
+        comm.is_loopback = True
         return comm
 
     @classmethod
@@ -477,8 +513,9 @@ class NativeComm:
         return p.value, t.value
 
     def to_host(self, ticket: int, count: int, host_slot: torch.Tensor, stream) -> "LazyNative":
-        """All-reduce ring slot ``ticket`` and copy it to ``host_slot`` (pinned) on the
-        communication stream; the returned object's ``value(i)`` waits for it."""
+        """Ring slot ``ticket`` is written by the launch just queued on ``stream``; the
+        returned object's ``value(i)`` waits for it, sums it over the ranks on the host
+        (``poms_comm_wait``) and reads the global sum from ``host_slot``."""
         from . import _lib
         import ctypes as C
         _lib.call("poms_allreduce_to_host", self.h, int(ticket), int(count), C.c_void_p(host_slot.data_ptr()),
@@ -493,8 +530,9 @@ class NativeComm:
 
 
 class LazyNative:
-    """A global sum being all-reduced and copied to pinned memory on the native
-    communicator's stream (the LazyScalar interface)."""
+    """A global sum of the native communicator's host-side ring (the LazyScalar
+    interface): ``value`` waits for the launch's local sum and adds the ranks' sums
+    on the host."""
 
     def __init__(self, comm: NativeComm, ticket: int, host_slot: torch.Tensor):
         self._comm, self._ticket, self._host = comm, ticket, host_slot

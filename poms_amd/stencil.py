@@ -842,7 +842,8 @@ class KronOperator:
         V = self.space
         nb = V.scalar_buffer()
         if lazy and want_norm and not want_dot and V.is_distributed and V.dist.native is not None:
-            # native RCCL: reduce into a ring slot, all-reduce + copy on the comm stream
+            # native communicator: reduce into a host-mapped ring slot, summed over the
+            # ranks on the host when read
             from .dist import LazyNative
             host = V.pinned_slots(1)
             ticket = self._run_native("jacobi", x_in, x_out, b, omega, lazy_count=1, host_dst=host)

@@ -380,7 +380,8 @@ def test_two_range_launch(gpu, variant):
 @pytest.mark.gpu
 def test_native_comm_lazy_slot(gpu):
     """The native ring slot path of a lazily read norm (one rank): the sweep reduces
-    into the slot, poms_allreduce_to_host copies it, value() waits for it."""
+    into the host-mapped slot, poms_allreduce_to_host registers it, value() waits for
+    it (and leaves the sum in the pinned destination)."""
     import ctypes as C
     from poms_amd import _lib, runtime as rt
     from poms_amd.dist import NativeComm

@@ -10,6 +10,13 @@ kernel durations (rocprofv3 --kernel-trace --stats on this script) gives the
 host-issue floor: the time the GPU waits for the Python host.
 
     python tools/slab_proxy.py --planes 67 --steps 3
+
+``--loopback-rank R --world W`` runs rank R's slab of the W-rank split of the real
+global problem instead (``SlabDistribution.loopback``): the production distributed
+schedule -- interior planes, the p-plane exchange on the communication stream, the
+boundary launch, the native pcg loop's all-reduces and lazy norms -- with every
+exchange and sum going through a one-rank RCCL communicator (the slab sends its
+boundary planes to itself).  RCCL's on-device copy stands in for the xGMI link.
 """
 from __future__ import annotations
 
@@ -65,10 +72,24 @@ def main():
     ap.add_argument("--coarse", type=int, default=8)
     ap.add_argument("--steps", type=int, default=3)
     ap.add_argument("--warmup", type=int, default=1)
+    ap.add_argument("--loopback-rank", type=int, default=None)
+    ap.add_argument("--world", type=int, default=8)
     a = ap.parse_args()
     import torch
     torch.cuda.set_device(0)
-    mg, npts = build(a.planes - a.p, a.cells, a.p, a.coarse)
+    if a.loopback_rank is not None:
+        from poms_amd.dist import SlabDistribution
+        from poms_amd.mg import TwoLevelVCycle
+        n = a.cells + a.p
+        d = SlabDistribution.loopback(n, a.loopback_rank, a.world)
+        mg = TwoLevelVCycle(a.p, a.cells, a.coarse, ndim=3, dist=d)
+        npts = [d.n_local, n, n]
+        label = (f"rank {a.loopback_rank} of {a.world}: {npts[0]}x{n}x{n} owned DOF of the {n}^3 problem, "
+                 f"exchanges with {(d.prev is not None) + (d.next is not None)} neighbour side(s) "
+                 f"looped back through a one-rank RCCL communicator ({d.transport})")
+    else:
+        mg, npts = build(a.planes - a.p, a.cells, a.p, a.coarse)
+        label = f"{npts[0]}x{npts[1]}x{npts[2]} DOF (one slab of the 8-GPU bench, no halo)"
     bf = mg.rhs_ones()
     for _ in range(a.warmup):
         mg.cycle(bf)
@@ -89,7 +110,7 @@ def main():
     for kind in ("apply", "residual", "jacobi", "jacobi_from_zero", "apply_dot"):
         t, n, _ = mg.A.timing_read(kind)
         per[kind] = {"gpu_ms_per_cycle": t * 1e3 / a.steps, "launches_per_cycle": n / a.steps}
-    print(json.dumps({"proxy": f"{npts[0]}x{npts[1]}x{npts[2]} DOF (one slab of the 8-GPU bench, no halo)",
+    print(json.dumps({"proxy": label,
                       "ms_per_cycle": dt * 1e3,
                       "operator_gpu_ms_per_cycle": sum(v["gpu_ms_per_cycle"] for v in per.values()),
                       "operator": per, "info_pre": ipre, "info_pos": ipos}), flush=True)
