@@ -100,6 +100,20 @@ struct poms_op {
     int sv_next = 0;
     int64_t sv_seq_next = 0, sv_done = 0;
     int64_t sv_seq[kSvRing];
+    // ... and per slot a region of kSvPart doubles the operator launch writes its
+    // per-block partial sums into (no reduction launch: the host adds them in the
+    // reduction kernel's order when it reads the slot).  sv_npart[i] = blocks of the
+    // launch that last used region i (0: none pending), sv_pkind[i] bit 0 norm
+    // partials at [0, n), bit 1 dot partials after them.
+    static constexpr int kSvPart = 4096;
+    double* sv_part = nullptr;   // kSvRing x kSvPart, pinned, device-mapped, armed unset
+    int sv_npart[kSvRing] = {};
+    int sv_pkind[kSvRing] = {};
+    // op_run: write the partials to part_dst instead of the scratch when they fit
+    // in part_cap doubles (last_part_host says whether they went there)
+    double* part_dst = nullptr;
+    int64_t part_cap = 0;
+    bool last_part_host = false;
     // launch timing (poms_op_timing): HIP events around every operator launch
     struct TimedLaunch { int epi; int64_t ndof; hipEvent_t e0, e1; };
     bool timing = false;
@@ -495,6 +509,7 @@ int poms_op_destroy(poms_op* o) {
     for (double* p : {o->a0t, o->b0t, o->a1, o->b1, o->a2, o->b2, o->dg2a, o->dg2b, o->rdiag0, o->coef, o->sv_dev})
         if (p) (void)hipFree(p);
     if (o->sv_host) (void)hipHostFree(o->sv_host);
+    if (o->sv_part) (void)hipHostFree(o->sv_part);
     for (auto& t : o->tl) {
         (void)hipEventDestroy(t.e0);
         (void)hipEventDestroy(t.e1);
@@ -729,9 +744,16 @@ static int op_run(poms_op* o, int epi, double omega, const double* x, double* y,
         set_error("too many blocks for the partial-sum scratch");
         return 1;
     }
-    KronPtrs p{x, y, b, o->a0t, o->b0t, o->a1, o->b1, o->a2, o->b2,
-               want_norm ? o->ctx->scratch + o->part_off : nullptr,
-               want_dot ? o->ctx->scratch + dbase + o->part_off : nullptr, o->rdiag0};
+    double* pn = o->ctx->scratch + o->part_off;
+    double* pd = o->ctx->scratch + dbase + o->part_off;
+    o->last_part_host = false;
+    if (o->part_dst && ((want_norm ? 1 : 0) + (want_dot ? 1 : 0)) * nblk <= o->part_cap) {
+        pn = o->part_dst;
+        pd = o->part_dst + (want_norm ? nblk : 0);
+        o->last_part_host = true;
+    }
+    KronPtrs p{x, y, b, o->a0t, o->b0t, o->a1, o->b1, o->a2, o->b2, want_norm ? pn : nullptr,
+               want_dot ? pd : nullptr, o->rdiag0};
     poms_op::TimedLaunch* tlh = nullptr;
     if (o->timing && (o->t_epi < 0 || o->t_epi == epi) && (o->t_seen++ % o->t_every) == 0) {
         // events on the launch stream around this launch (a sample: every t_every-th)
@@ -1544,6 +1566,8 @@ namespace {
 // device scalars (the sums only the host reads live in host slots / comm ring slots)
 enum { SC_SR = 0, SC_PQ = 1, SC_ONE = 2, SC_ALPHA = 3, SC_ALPHA2 = 4, SC_BETA = 5, SC_SRN = 6, SC_N = 16 };
 enum { H_RR0 = 0, H_RR = 1, H_J0 = 2 /* 2 slots */, H_JN = 4 /* 2 slots */ };
+// an unwritten partial in a host region: a NaN payload no reduction produces
+constexpr uint64_t kPartUnset = 0x7ff8dead0000beefull;
 
 __global__ void pcg_scalars_kernel(double* sc, int mode) {
     if (threadIdx.x != 0) return;
@@ -1598,7 +1622,28 @@ struct PcgRun {
     int lazy_post(int h, int cnt) { return direct() ? 0 : poms_allreduce_to_host(comm, tk[h], cnt, host + h, stv); }
     // an operator launch whose sums only the host reads: [dot, norm] from host slot h
     int jrun(int epi, const double* x, double* y, const double* b, bool wn, bool wd, int h) {
-        if (direct()) return run(epi, x, y, b, wn ? host + h + (wd ? 1 : 0) : nullptr, wd ? host + h : nullptr);
+        if (direct()) {   // the launch writes its partials into slot h's host region
+            // (up to host_partials_max() blocks).  A/B on one box
+            // (profiles/r03/host_partials/): 2D 1027^2 cycle 4.5-5.2 -> 3.6-3.7 ms,
+            // 3D 515^3 195.0-195.5 -> 194.9-195.3 ms
+            op->part_dst = op->sv_part + (size_t)h * poms_op::kSvPart;
+            op->part_cap = ((wn ? 1 : 0) + (wd ? 1 : 0)) * host_partials_max();
+            const int rc = op_run_epi(op, epi, o->omega, x, y, b, 0, n0, 0, 0, wn, wd, stv);
+            op->part_dst = nullptr;
+            if (rc) return 1;
+            const int64_t n = op->last_partials;
+            if (op->last_part_host) {
+                op->sv_npart[h] = (int)n;
+                op->sv_pkind[h] = (wn ? 1 : 0) | (wd ? 2 : 0);
+                return 0;
+            }
+            // too many blocks for the region: reduce on the device into the slots
+            double* pdot = op->ctx->scratch + (op->dot_base < 0 ? n : op->dot_base);
+            if (wn) reduce_launch(op->ctx->scratch, (int)n, host + h + (wd ? 1 : 0), st);
+            if (wd) reduce_launch(pdot, (int)n, host + h, st);
+            POMS_HIP_CHECK(hipGetLastError());
+            return 0;
+        }
         const RowGeom g = row_geom(&op->L);
         return poms_op_run_dist(op, comm, epi, o->omega, x, y, b, const_cast<double*>(x), g.s0, op->L.n[0],
                                 (int)op->L.pads[0], op->pmax, o->prev, o->next, 1, wn ? 1 : 0, wd ? 1 : 0, nullptr,
@@ -1624,13 +1669,87 @@ struct PcgRun {
         for (int i = 0; i < cnt; ++i) {
             reinterpret_cast<volatile double*>(host)[h + i] = -1.0;   // norms are >= 0
             op->sv_seq[h + i] = op->sv_seq_next;
+            if (op->sv_npart[h + i] > 0) {   // an abandoned launch's partials (complete by now): re-arm
+                const int nsum = ((op->sv_pkind[h + i] & 1) ? 1 : 0) + ((op->sv_pkind[h + i] & 2) ? 1 : 0);
+                part_arm(op->sv_part + (size_t)(h + i) * poms_op::kSvPart, nsum * op->sv_npart[h + i]);
+                op->sv_npart[h + i] = 0;
+                op->sv_pkind[h + i] = 0;
+            }
         }
         ++op->sv_seq_next;
         return h;
     }
+    static int64_t host_partials_max() {   // tuning: POMS_HOST_PARTIALS (0: always reduce on the device)
+        static int64_t m = -1;
+        if (m < 0) {
+            const char* e = getenv("POMS_HOST_PARTIALS");
+            m = e ? std::max<int64_t>(0, atoll(e)) : poms_op::kSvPart / 2;
+            m = std::min<int64_t>(m, poms_op::kSvPart / 2);
+        }
+        return m;
+    }
+    // Wait for every partial of slot h's region and add them on the host in the
+    // order of reduce_partials_kernel (256 strided running sums, the 64-lane xor
+    // butterfly, then (w0 + w1) + (w2 + w3)): the same bits as the device reduction.
+    static double host_reduce(const double* p, int n) {
+        double sv[256];
+        for (int t = 0; t < 256; ++t) {
+            double a = 0.0;
+            for (int i = t; i < n; i += 256) a += p[i];
+            sv[t] = a;
+        }
+        double red[4];
+        for (int w = 0; w < 4; ++w) {
+            double v[64], nv[64];
+            for (int l = 0; l < 64; ++l) v[l] = sv[64 * w + l];
+            for (int off = 32; off > 0; off >>= 1) {
+                for (int l = 0; l < 64; ++l) nv[l] = v[l] + v[l ^ off];
+                for (int l = 0; l < 64; ++l) v[l] = nv[l];
+            }
+            red[w] = v[0];
+        }
+        return (red[0] + red[1]) + (red[2] + red[3]);
+    }
+    int settle_partials(int h) {
+        const int n = op->sv_npart[h];
+        double* reg = op->sv_part + (size_t)h * poms_op::kSvPart;
+        const int nsum = ((op->sv_pkind[h] & 1) ? 1 : 0) + ((op->sv_pkind[h] & 2) ? 1 : 0);
+        for (int i = 0; i < nsum * n; ++i) {
+            for (long k = 1; part_unset(reg + i); ++k) {
+                __builtin_ia32_pause();
+                if ((k & 4095) == 0 && hipStreamQuery(st) != hipErrorNotReady) {
+                    std::atomic_thread_fence(std::memory_order_seq_cst);
+                    if (part_unset(reg + i)) return 1;   // never written: the launch failed
+                }
+            }
+        }
+        std::atomic_thread_fence(std::memory_order_acquire);
+        const bool wn = op->sv_pkind[h] & 1, wd = op->sv_pkind[h] & 2;
+        if (wn) host[h + (wd ? 1 : 0)] = host_reduce(reg, n);
+        if (wd) host[h] = host_reduce(reg + (wn ? n : 0), n);
+        part_arm(reg, nsum * n);
+        op->sv_npart[h] = 0;
+        op->sv_pkind[h] = 0;
+        return 0;
+    }
+    static bool part_unset(const double* v) {
+        uint64_t u;
+        const volatile uint64_t* q = reinterpret_cast<const volatile uint64_t*>(v);
+        u = *q;
+        return u == kPartUnset;
+    }
+    static void part_arm(double* v, int n) {
+        volatile uint64_t* q = reinterpret_cast<volatile uint64_t*>(v);
+        for (int i = 0; i < n; ++i) q[i] = kPartUnset;
+    }
     double get(int h, int i = 0) {
         if (!direct()) {
             if (poms_comm_wait(comm, tk[h])) return std::nan("");
+            return host[h + i];
+        }
+        if (op->sv_npart[h] > 0) {
+            if (settle_partials(h)) return std::nan("");
+            op->sv_done = std::max(op->sv_done, op->sv_seq[h] + 1);
             return host[h + i];
         }
         const volatile double* v = reinterpret_cast<const volatile double*>(host) + h + i;
@@ -1747,6 +1866,10 @@ int poms_pcg_jacobi(poms_op* op, poms_comm* comm, const poms_pcg_opts* o, const 
         // host-read norms straight into it
         POMS_HIP_CHECK(hipHostMalloc(reinterpret_cast<void**>(&op->sv_host), poms_op::kSvRing * sizeof(double),
                                      hipHostMallocMapped | hipHostMallocCoherent));
+        POMS_HIP_CHECK(hipHostMalloc(reinterpret_cast<void**>(&op->sv_part),
+                                     (size_t)poms_op::kSvRing * poms_op::kSvPart * sizeof(double),
+                                     hipHostMallocMapped | hipHostMallocCoherent));
+        PcgRun::part_arm(op->sv_part, poms_op::kSvRing * poms_op::kSvPart);
         for (int64_t& q : op->sv_seq) q = -1;
     }
     PcgRun R{op, comm, o, as_stream(stream), stream, op->sv_dev, op->sv_host};
