@@ -35,7 +35,12 @@ def _flags() -> list[str]:
 def _needs(obj: Path, src: Path) -> bool:
     if not obj.exists():
         return True
-    deps = [src, CSRC / "common.hpp", HERE.parent / "include" / "poms_hip.h"]
+    # the source and the headers it includes by quoted name (csrc/ or include/)
+    deps = [src]
+    for line in src.read_text().splitlines():
+        if line.startswith('#include "'):
+            name = Path(line.split('"')[1]).name
+            deps += [CSRC / name, HERE.parent / "include" / name]
     return any(d.stat().st_mtime > obj.stat().st_mtime for d in deps if d.exists())
 
 

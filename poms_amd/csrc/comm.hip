@@ -12,6 +12,7 @@
 // per direction, `pyccel/kron_product.py:21-41`) and `comm.allreduce` of the
 // solver scalars (`sources/solvers.py:87-124`, `sources/mg_jac.py:95`).
 #include "common.hpp"
+#include "split_hooks.hpp"
 #include "../../include/poms_hip.h"
 
 #include <rccl/rccl.h>
@@ -36,6 +37,7 @@ struct poms_comm {
     hipEvent_t ev_in = nullptr;     // caller's stream -> cs
     hipEvent_t ev_halo = nullptr;   // exchange done (cs -> caller)
     hipEvent_t ev_red = nullptr;    // all-reduce done (cs -> caller)
+    hipEvent_t ev_bnd = nullptr;    // boundary launch on cs done (cs -> caller)
     // Ring of slots for global sums only the host reads (the damped-Jacobi norms,
     // pcg's r.r): a launch's reduction kernel writes the rank's local sum straight
     // into the slot -- pinned, coherent host memory mapped into the device -- and
@@ -88,7 +90,7 @@ static hipStream_t cstream(void* s) { return reinterpret_cast<hipStream_t>(s); }
 namespace poms {
 int op_run_split(poms_op* op, int epilogue, double omega, const double* x, double* y, const double* b,
                  int64_t ib, int64_t ie, int64_t b1s, int64_t b1e, int64_t b2s, int64_t b2e, double* norm_out,
-                 double* dot_out, int (*between)(void*), void* arg, void* stream);
+                 double* dot_out, const SplitHooks& h, void* stream);
 }
 
 static bool getenv_off(const char* name) {
@@ -217,7 +219,8 @@ static int comm_common_init(poms_comm* c) {
         hipStreamCreateWithPriority(&c->cs, hipStreamNonBlocking, greatest) != hipSuccess ||
         hipEventCreateWithFlags(&c->ev_in, hipEventDisableTiming) != hipSuccess ||
         hipEventCreateWithFlags(&c->ev_halo, hipEventDisableTiming) != hipSuccess ||
-        hipEventCreateWithFlags(&c->ev_red, hipEventDisableTiming) != hipSuccess) {
+        hipEventCreateWithFlags(&c->ev_red, hipEventDisableTiming) != hipSuccess ||
+        hipEventCreateWithFlags(&c->ev_bnd, hipEventDisableTiming) != hipSuccess) {
         set_error("poms_comm_create: stream / event creation failed");
         return 1;
     }
@@ -276,7 +279,7 @@ int poms_comm_destroy(poms_comm* c) {
     if (!c) return 0;
     if (c->cs) (void)hipStreamSynchronize(c->cs);
     if (c->comm) ncclCommDestroy(c->comm);
-    for (hipEvent_t e : {c->ev_in, c->ev_halo, c->ev_red})
+    for (hipEvent_t e : {c->ev_in, c->ev_halo, c->ev_red, c->ev_bnd})
         if (e) (void)hipEventDestroy(e);
     for (hipEvent_t e : c->ring_ev)
         if (e) (void)hipEventDestroy(e);
@@ -495,16 +498,25 @@ int poms_op_run_dist(poms_op* op, poms_comm* c, int epilogue, double omega, cons
     }
     if (exchange && n_local > 2 * pmax) {
         if (poms_halo_start(c, xplanes, plane_elems, n_local, pad, pmax, prev, next, stream)) return 1;
-        struct Finish {
-            poms_comm* c;
-            void* stream;
-            static int run(void* a) {
-                auto* f = static_cast<Finish*>(a);
-                return poms_halo_finish(f->c, f->stream);
+        // the boundary launch runs on the communication stream behind the exchange
+        // (POMS_BOUNDARY_ON_CS=0: on the caller's stream after it, as before)
+        struct Hooks {
+            static int ghosts_on(void* a, void* s) {   // `s` waits for the exchange
+                auto* c = static_cast<poms_comm*>(a);
+                POMS_HIP_CHECK(hipStreamWaitEvent(cstream(s), c->ev_halo, 0));
+                return 0;
             }
-        } fin{c, stream};
+            static int join(void* a, void* from, void* to) {
+                auto* c = static_cast<poms_comm*>(a);
+                POMS_HIP_CHECK(hipEventRecord(c->ev_bnd, cstream(from)));
+                POMS_HIP_CHECK(hipStreamWaitEvent(cstream(to), c->ev_bnd, 0));
+                return 0;
+            }
+        };
+        static const bool on_cs = !getenv_off("POMS_BOUNDARY_ON_CS");
+        const SplitHooks h{on_cs ? static_cast<void*>(c->cs) : nullptr, &Hooks::ghosts_on, &Hooks::join, c};
         if (op_run_split(op, epilogue, omega, x, y, b, pmax, n_local - pmax, 0, pmax, n_local - pmax, n_local, nout,
-                         dout, &Finish::run, &fin, stream))
+                         dout, h, stream))
             return 1;
     } else {
         if (exchange) {

@@ -94,10 +94,11 @@ __device__ __forceinline__ void v5_barrier() {
 // Waves per workgroup (= output rows per tile): 16 at p <= 3 (4 waves per SIMD,
 // 128 VGPRs).  p >= 4 needs more registers for its 2p+1 wide windows: 8 waves (2
 // per SIMD, up to 256 VGPRs); the x tile is then 8 + 2p rows, up to 3 DMAs per
-// wave.  The two-sweeps-from-zero build fits 16 waves at p = 3 once its x1
-// scaling happens in place in the ring and its two sums live in LDS (930 vs 945 us
-// for v3 at 515^3); at p <= 2 it keeps 8 waves (256^3 p = 2: 16 waves 154 us, 8
-// waves 136, v3 135-146; profiles/r02/j0_16wave/).
+// wave.  The two-sweeps-from-zero build fits 16 waves at p = 3 with its two sums in
+// LDS and x1 = s b scaled as the rows are read (round 3: on the row-Toeplitz tiles
+// after the axis-1 pass; round 2 scaled the ring in place before each plane's
+// barrier, 917 us at 515^3); at p <= 2 it keeps 8 waves (256^3 p = 2: 16 waves
+// 154 us, 8 waves 136, v3 135-146; profiles/r02/j0_16wave/).
 // (12 waves at 168 VGPRs fit the p = 5 apply but ran 254 us against 185 at 256^3,
 // profiles/r02/configs/kb_p5_waves12.log vs kb_p5_waves8.log.)
 constexpr int v5_waves(int P, int EPI) { return (P == 3 || (P < 3 && EPI != EPI_JACOBI0)) ? 16 : 8; }
@@ -210,6 +211,13 @@ kron_v5_kernel(const double* __restrict__ x, double* __restrict__ y, const doubl
     }
     const bool fast1 = orow >= tc.lo1 && orow < tc.hi1;                          // per wave
     const bool fast2 = (c0 >= tc.lo2) && (min(c0 + TO, g.n2) <= tc.hi2);         // per workgroup
+    // J0 row-Toeplitz tile (per workgroup): every x-tile row has the Toeplitz axis-1
+    // band, so omega/diag depends on the plane and the column only.  Such a tile (31
+    // of 33 tile rows at 515^3) scales x1 = s b AFTER the axis-1 pass -- 4 multiplies
+    // of u, v per lane and plane -- instead of scaling its x rows in the LDS ring in
+    // place before the plane's barrier (a read-modify-write of the ring on the
+    // critical path of every plane).
+    const bool jrf = J0 && r0 - P >= tc.lo1 && r0 + T1 + P <= tc.hi1;
 
     // axis-2 band rows of the tile's columns (only outside the Toeplitz interior)
     if (!fast2) {
@@ -275,8 +283,7 @@ kron_v5_kernel(const double* __restrict__ x, double* __restrict__ y, const doubl
     // the output columns H .. H+TO-1: on the aligned layout that drops the two
     // half-lines of halo each b row fetched (8 of 64 lanes) and a quarter-line at
     // each end of every x row.
-    // (J0 keeps every lane: the trim's extra VGPR makes its p = 3 build spill)
-    const uint32_t colbx = (uint32_t)colb + ((J0 || (2 * lane + 1 >= H - P && 2 * lane < H + TO + P)) ? 0u : 0x80000000u);
+    const uint32_t colbx = (uint32_t)colb + ((2 * lane + 1 >= H - P && 2 * lane < H + TO + P) ? 0u : 0x80000000u);
     const uint32_t colbb = (uint32_t)colb + ((2 * lane + 1 >= H && 2 * lane < H + TO) ? 0u : 0x80000000u);
 
     // ---- LDS-DMA issue (per wave per plane: x NXM - 1 or NXM rows, b 1 row) ----
@@ -372,37 +379,6 @@ kron_v5_kernel(const double* __restrict__ x, double* __restrict__ y, const doubl
                     else if (xtra) v5_wait_vm<(PFX - 1) * NXM>();
                     else v5_wait_vm<(PFX - 1) * (NXM - 1)>();
                 }
-                if constexpr (J0) {
-                    // x1 = omega b / diag: each wave scales the rows it DMA'd itself, once, in
-                    // place, before the barrier publishes them (instead of every reading wave
-                    // scaling all 2P+1 rows it reads: 2P+1 LDS reads and 4P+2 multiplies less
-                    // per lane and plane, and the VGPRs p = 3 lacked)
-                    const int m = g.g0 + z0 - P + t;   // global plane of x(t)
-                    const bool tp = m >= tc.lo0 && m < tc.hi0;
-                    double d0a = 0.0, d0b = 0.0;
-                    if (!tp) {
-                        const int i0 = (m + P) * W + P;
-                        d0a = a0t[i0];
-                        d0b = b0t[i0];
-                    }
-                    double* xs0 = lds + XS_OFF + (t % D) * XR * TC + 2 * lane;
-#pragma unroll
-                    for (int r = 0; r < NXM; ++r) {
-                        if (r == NXM - 1 && !xtra) break;
-                        const int qr = wv + r * NW;
-                        d2 v = *(const d2*)(xs0 + qr * TC);
-                        if (tp) {
-                            const d2 sc = *(const d2*)(lds + RS_OFF + qr * TC + 2 * lane);
-                            v[0] *= sc[0];
-                            v[1] *= sc[1];
-                        } else {   // the p planes next to each global end (and ghost planes)
-                            v[0] *= j0_scale(qr, 2 * lane, d0a, d0b);
-                            v[1] *= j0_scale(qr, 2 * lane + 1, d0a, d0b);
-                        }
-                        *(d2*)(xs0 + qr * TC) = v;
-                    }
-                    __builtin_amdgcn_s_waitcnt(0xc07f);   // lgkmcnt(0): the scaled rows written
-                }
                 v5_barrier();
                 if constexpr (B3) {
                     dma_x(t + PFX < nplanes ? z0 - P + t + PFX : -(1 << 20), (t + PFX) % D);
@@ -417,6 +393,36 @@ kron_v5_kernel(const double* __restrict__ x, double* __restrict__ y, const doubl
                 d2 xv[W];
 #pragma unroll
                 for (int k = 0; k < W; ++k) xv[k] = *(const d2*)(xs + (wv + k) * TC);
+                // J0: the ring holds b; x1 = s b with s = omega / diag.  On a row-Toeplitz tile
+                // (jrf) and a plane of the axis-0 Toeplitz interior s depends on the column only
+                // and is applied after the axis-1 pass (below); elsewhere each of the 2P+1 rows
+                // is scaled as it is read (s from the LDS table, or -- the P planes next to each
+                // global end -- formed from the plane's axis-0 diagonal entries).  Nothing is
+                // written back into the ring: no read-modify-write before the plane's barrier.
+                bool jsc = false;
+                if constexpr (J0) {
+                    const int m = g.g0 + z0 - P + t;   // global plane of x(t)
+                    const bool tp = m >= tc.lo0 && m < tc.hi0;
+                    jsc = jrf && tp;
+                    if (!jsc) {
+                        if (tp) {
+#pragma unroll
+                            for (int k = 0; k < W; ++k) {
+                                const d2 sc = *(const d2*)(lds + RS_OFF + (wv + k) * TC + 2 * lane);
+                                xv[k][0] *= sc[0];
+                                xv[k][1] *= sc[1];
+                            }
+                        } else {
+                            const int i0 = (m + P) * W + P;
+                            const double d0a = a0t[i0], d0b = b0t[i0];
+#pragma unroll
+                            for (int k = 0; k < W; ++k) {
+                                xv[k][0] *= j0_scale(wv + k, 2 * lane, d0a, d0b);
+                                xv[k][1] *= j0_scale(wv + k, 2 * lane + 1, d0a, d0b);
+                            }
+                        }
+                    }
+                }
                 if constexpr (MODE == 1) {
                     const bool ok0 = t >= 2 * P && row_ok && (cok & 1);
                     bstore2_s(ry, ok0 ? (orow + P) * s1 * 8 + colb + (zo_of(t) + g.pd0) * (int)plane8 : 0x7ffffff0,
@@ -451,6 +457,18 @@ kron_v5_kernel(const double* __restrict__ x, double* __restrict__ y, const doubl
                         }
                         u[e] = su;
                         v[e] = sv;
+                    }
+                }
+                if constexpr (J0) {
+                    if (jsc) {   // x1 = s(column) b: the scaling commutes with the axis-1 pass
+                        __asm__ volatile("" ::: "memory");   // (load sc here, not beside the 2P+1 rows)
+                        const d2 sc = *(const d2*)(lds + RS_OFF + 2 * lane);   // (every table row is equal here)
+#pragma unroll
+                        for (int e = 0; e < 2; ++e) {
+                            u[e] *= sc[e];
+                            v[e] *= sc[e];
+                            xv[P][e] *= sc[e];   // the centre tap the x1 history keeps
+                        }
                     }
                 }
 
@@ -719,11 +737,10 @@ static int v5_launch_t1(const KronPtrs& p, const KronGeom& g, const ToepConst& t
 template <int P, int EPI, int D, int MODE = 0, int CP = 0, bool XH = false>
 static int v5_launch_t(const KronPtrs& p, const KronGeom& g, const ToepConst& tc, int H, double omega,
                        hipStream_t st) {
-    // (the p = 3 two-sweeps-from-zero build always stores 8-B halves: with the 16-B
-    // store's aligned register quad it spills at 16 waves; so does its build with
-    // distinct axis-1 / axis-2 Toeplitz rows, which resolve_variant leaves to v3)
+    // (the p = 3 two-sweeps-from-zero build with distinct axis-1 / axis-2 Toeplitz
+    // rows spills at 16 waves; resolve_variant leaves that case to v3)
     const bool st16 = ((reinterpret_cast<uintptr_t>(p.y) + 8 * (int64_t)(g.pd2 - H)) & 15) == 0 &&
-                      g.s1 % 2 == 0 && g.s0 % 2 == 0 && !(EPI == EPI_JACOBI0 && P == 3);
+                      g.s1 % 2 == 0 && g.s0 % 2 == 0;
     // the Jacobi x_in history does not fit the VGPRs beside the split stores: the
     // unaligned build DMAs x_in next to b instead
     constexpr bool XHU = (EPI == EPI_JACOBI) ? false : XH;
@@ -776,8 +793,8 @@ static int v5_launch_p(int epi, const KronPtrs& p, const KronGeom& g, const Toep
             if (store_policy() == 2) return v5_launch_t<P, EPI_JACOBI, 3, 0, 2 | 32, true>(p, g, tc, H, omega, st);
             return v5_launch_t<P, EPI_JACOBI, 4, 0, 6 | 64, true>(p, g, tc, H, omega, st);
         case EPI_APPLYDOT: return v5_launch_t<P, EPI_APPLYDOT, 4, 0, 6>(p, g, tc, H, omega, st);
-        // x ring = b (read once, apply's policy), scaled in place to x1 after it lands;
-        // y = x2 streamed
+        // x ring = b (read once, apply's policy), scaled to x1 as it is read; y = x2
+        // streamed
         case EPI_JACOBI0: return v5_launch_t<P, EPI_JACOBI0, 4, 0, 14>(p, g, tc, H, omega, st);
     }
     set_error("v5: epilogue not built");

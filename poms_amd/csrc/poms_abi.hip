@@ -1,5 +1,6 @@
 // extern "C" boundary of libpoms_hip.so (declared in include/poms_hip.h).
 #include "common.hpp"
+#include "split_hooks.hpp"
 #include "../../include/poms_hip.h"
 
 #include <algorithm>
@@ -899,18 +900,22 @@ static int op_run_epi(poms_op* op, int epilogue, double omega, const double* x, 
 }
 
 namespace poms {
-// The distributed operator call's two launches -- planes [ib, ie) first, then
-// `between` (the wait for the ghost exchange), then the boundary ranges [b1s, b1e) +
-// [b2s, b2e) -- with both launches' partials side by side in the scratch and ONE
-// reduction per requested sum after the second launch (one launch fewer per sum
-// than reducing each launch; poms_op_run_dist).
+// The distributed operator call's two launches -- planes [ib, ie) on `stream`, then
+// the boundary ranges [b1s, b1e) + [b2s, b2e) once the ghost exchange is done --
+// with both launches' partials side by side in the scratch and ONE reduction per
+// requested sum after both (one launch fewer per sum than reducing each launch;
+// poms_op_run_dist).  The boundary launch goes to h.bstream when given (the
+// communication stream, right behind the exchange): it depends on the exchange
+// only, not on the interior launch, so its workgroups fill the CUs the interior
+// launch's last round leaves idle instead of running as a separate, mostly empty
+// round of its own; `stream` then waits for it (h.join) before the reductions.
 int op_run_split(poms_op* op, int epilogue, double omega, const double* x, double* y, const double* b,
                  int64_t ib, int64_t ie, int64_t b1s, int64_t b1e, int64_t b2s, int64_t b2e, double* norm_out,
-                 double* dot_out, int (*between)(void*), void* arg, void* stream) {
+                 double* dot_out, const SplitHooks& h, void* stream) {
     if (!op) { set_error("op_run_split: null operator"); return 1; }
-    if (op->form == FORM_STENCIL) {   // its own partials layout: reduce each launch
+    if (op->form == FORM_STENCIL) {   // its own partials layout: reduce each launch, both on `stream`
         if (poms_op_run_reduce2(op, epilogue, omega, x, y, b, ib, ie, 0, 0, norm_out, dot_out, 0, stream)) return 1;
-        if (between && between(arg)) return 1;
+        if (h.ghosts_on(h.arg, stream)) return 1;
         return poms_op_run_reduce2(op, epilogue, omega, x, y, b, b1s, b1e, b2s, b2e, norm_out, dot_out, 1, stream);
     }
     const bool wn = norm_out != nullptr, wd = dot_out != nullptr;
@@ -922,9 +927,11 @@ int op_run_split(poms_op* op, int epilogue, double omega, const double* x, doubl
     op->dot_base = kScratch / 2;
     if (op_run_epi(op, epilogue, omega, x, y, b, ib, ie, 0, 0, wn, wd, stream)) return 1;
     const int64_t n1 = op->last_partials;
-    if (between && between(arg)) return 1;
+    void* bs = h.bstream ? h.bstream : stream;
+    if (h.ghosts_on(h.arg, bs)) return 1;
     op->part_off = n1;
-    if (op_run_epi(op, epilogue, omega, x, y, b, b1s, b1e, b2s, b2e, wn, wd, stream)) return 1;
+    if (op_run_epi(op, epilogue, omega, x, y, b, b1s, b1e, b2s, b2e, wn, wd, bs)) return 1;
+    if (bs != stream && h.join(h.arg, bs, stream)) return 1;
     const int64_t n = n1 + op->last_partials;
     op->last_partials = 0;   // not in the layout poms_op_last_partials describes
     if (wn) reduce_launch(op->ctx->scratch, (int)n, norm_out, as_stream(stream));

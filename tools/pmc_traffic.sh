@@ -16,4 +16,4 @@ for grp in FETCH_SIZE WRITE_SIZE; do
   rc=$?; echo "$tag group $gi rc=$rc"
   [[ $rc -eq 0 ]] || { echo "STOP"; exit $rc; }
 done
-python3 "$ROOT/tools/pmc_traffic.py" "$OUT" "$sub" 136590875 "$OUT/traffic.json" > /dev/null && cat "$OUT/traffic.json"
+python3 "$ROOT/tools/pmc_traffic.py" "$OUT" "$sub" ${POMS_PMC_DOF:-136590875} "$OUT/traffic.json" > /dev/null && cat "$OUT/traffic.json"
