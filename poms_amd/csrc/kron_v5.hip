@@ -160,6 +160,10 @@ kron_v5_kernel(const double* __restrict__ x, double* __restrict__ y, const doubl
     // VGPRs they would pin for the whole march are what p = 3 lacks at 16 waves
     // (p = 3 only: the 8-wave builds of p <= 2 keep them in VGPRs, which they have)
     constexpr bool JSL = J0 && P == 3;
+    // J0 diagnostic builds (MODE 3: no sums, 4: no x1 scaling of the rows, 5: both;
+    // results wrong by design -- timing only)
+    constexpr bool J0NS = J0 && (MODE == 3 || MODE == 5);
+    constexpr bool J0NX = J0 && (MODE == 4 || MODE == 5);
     constexpr int JS_OFF = (D1_OFF + (J0 ? 2 * XR : 0) + 1) & ~1;
     constexpr int LDS_N = JS_OFF + (JSL ? 2 * NW * 64 : 0);
     __shared__ __attribute__((aligned(16))) double lds[LDS_N];
@@ -400,7 +404,7 @@ kron_v5_kernel(const double* __restrict__ x, double* __restrict__ y, const doubl
                 // global end -- formed from the plane's axis-0 diagonal entries).  Nothing is
                 // written back into the ring: no read-modify-write before the plane's barrier.
                 bool jsc = false;
-                if constexpr (J0) {
+                if constexpr (J0 && !J0NX) {
                     const int m = g.g0 + z0 - P + t;   // global plane of x(t)
                     const bool tp = m >= tc.lo0 && m < tc.hi0;
                     jsc = jrf && tp;
@@ -583,16 +587,19 @@ kron_v5_kernel(const double* __restrict__ x, double* __restrict__ y, const doubl
                         sc[1] = j0_scale(wv + P, 2 * lane + 1, d0a, d0b);
                     }
                     d2 js = {nrm, dotp};
-                    if constexpr (JSL) js = *(const d2*)(lds + JS_OFF + 2 * tid);   // this lane's own slot
+                    if constexpr (JSL && !J0NS) js = *(const d2*)(lds + JS_OFF + 2 * tid);   // this lane's own slot
 #pragma unroll
                     for (int e = 0; e < 2; ++e) {
                         const double x1 = xin[e];
                         const double dr = fma(-vo[e], sc[e], x1);
                         outv[e] = x1 + dr;
-                        js[0] = ok[e] ? fma(dr, dr, js[0]) : js[0];   // ||dr_2||^2
-                        js[1] = ok[e] ? fma(x1, x1, js[1]) : js[1];   // ||x1||^2 = ||dr_1||^2
+                        if constexpr (!J0NS) {
+                            js[0] = ok[e] ? fma(dr, dr, js[0]) : js[0];   // ||dr_2||^2
+                            js[1] = ok[e] ? fma(x1, x1, js[1]) : js[1];   // ||x1||^2 = ||dr_1||^2
+                        }
                     }
-                    if constexpr (JSL) {
+                    if constexpr (J0NS) {
+                    } else if constexpr (JSL) {
                         *(d2*)(lds + JS_OFF + 2 * tid) = js;
                     } else {
                         nrm = js[0];
@@ -824,6 +831,12 @@ int kron_v5_launch(int pmax, int epi, const KronPtrs& p, const KronGeom& g, cons
 #ifndef POMS_V5_QUICK   // (POMS_V5_QUICK: p = 3 production builds only, for quick tuning builds)
     if (diag_mode) {   // DIAGNOSTIC / tuning builds (p = 3)
         if (pmax != 3) { set_error("v5 diag mode: p = 3 only"); return 1; }
+        if (diag_mode >= 10 && diag_mode <= 12) {   // two sweeps from zero: 10 no sums, 11 no x1 scaling, 12 both
+            if (epi != EPI_JACOBI0) { set_error("v5 diag mode 10-12: two sweeps from zero only"); return 1; }
+            return diag_mode == 10 ? v5_launch_t<3, EPI_JACOBI0, 4, 3, 14>(p, g, tc, H, omega, st)
+                 : diag_mode == 11 ? v5_launch_t<3, EPI_JACOBI0, 4, 4, 14>(p, g, tc, H, omega, st)
+                                   : v5_launch_t<3, EPI_JACOBI0, 4, 5, 14>(p, g, tc, H, omega, st);
+        }
         if (diag_mode <= 2) {   // 1 = memory only, 2 = arithmetic only (apply)
             if (epi != EPI_APPLY) { set_error("v5 diag mode 1/2: apply only"); return 1; }
             return diag_mode == 1 ? v5_launch_t<3, EPI_APPLY, 4, 1>(p, g, tc, H, omega, st)

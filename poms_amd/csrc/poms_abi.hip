@@ -520,10 +520,11 @@ int poms_op_destroy(poms_op* o) {
 }
 
 int poms_op_set_variant(poms_op* op, int variant) {
-    // 90/91, 92-100, 101-109: diagnostic / tuning builds of v3, v4, v5
+    // 90/91, 92-100, 101-112: diagnostic / tuning builds of v3, v4, v5 (110-112: v5
+    // two sweeps from zero without sums / x1 scaling, timing only)
     const bool known = variant == 0 || variant == 4 || (variant >= 7 && variant <= 10) ||
-                       (variant >= 90 && variant <= 109);
-    if (!op || !known) { set_error("poms_op_set_variant: bad argument (0, 4, 7, 8, 9, 10; 90-109 diagnostic)"); return 1; }
+                       (variant >= 90 && variant <= 112);
+    if (!op || !known) { set_error("poms_op_set_variant: bad argument (0, 4, 7, 8, 9, 10; 90-112 diagnostic)"); return 1; }
     if (variant > 0 && !op->v2_ok) { set_error("poms_op_set_variant: variant needs pads == pmax"); return 1; }
     op->variant = variant;
     return 0;
@@ -719,7 +720,8 @@ static int op_run(poms_op* o, int epi, double omega, const double* x, double* y,
         set_error("fused x_out.b needs a Jacobi sweep on kernel variants 4-10");
         return 1;
     }
-    if (epi == EPI_JACOBI0 && !(o->variant == 8 || o->variant == 9 || o->variant == 10)) {
+    if (epi == EPI_JACOBI0 && !(o->variant == 8 || o->variant == 9 || o->variant == 10 ||
+                                (o->variant >= 110 && o->variant <= 112))) {
         set_error("two sweeps from zero: kernel variant 8, 9 or 10 only");
         return 1;
     }
@@ -731,7 +733,7 @@ static int op_run(poms_op* o, int epi, double omega, const double* x, double* y,
     // Variant 10 (v5) runs apply / residual / Jacobi / apply+dot of 3D p <= 3
     // operators, and is what 8 picks for them; 9 otherwise.
     int v = resolve_variant(o, epi);
-    const int v5_diag = (v >= 101 && v <= 109) ? v - 100 : 0;   // v5 diagnostic / tuning builds
+    const int v5_diag = (v >= 101 && v <= 112) ? v - 100 : 0;   // v5 diagnostic / tuning builds
     if (v5_diag) v = 10;
     int v5_h = 0, v5_to = 0;
     if (v == 10) kron_v5_tile(o->pmax, v5_aligned(o, x), &v5_h, &v5_to);
@@ -828,7 +830,8 @@ int poms_op_jacobi_from_zero(poms_op* op, double omega, const double* b, double*
 int poms_op_from_zero_supported(poms_op* op, int* yes) {
     if (!op || !yes) { set_error("poms_op_from_zero_supported: null argument"); return 1; }
     const int64_t bytes = (int64_t)(op->L.n[0] + 2 * op->L.pads[0]) * row_geom(&op->L).s0 * 8;
-    *yes = (op->ndim == 3 && op->form != FORM_STENCIL && (op->variant == 8 || op->variant == 9 || op->variant == 10) &&
+    *yes = (op->ndim == 3 && op->form != FORM_STENCIL &&
+            (op->variant == 8 || op->variant == 9 || op->variant == 10 || (op->variant >= 110 && op->variant <= 112)) &&
             bytes < 0x7ffffff0LL) ? 1 : 0;
     return 0;
 }

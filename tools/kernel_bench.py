@@ -66,6 +66,7 @@ def main():
                 for kind in kinds:
                     fn = {"dot": lambda: x.dot(b),
                           "apply": lambda: A.dot(x, out=y),
+                          "apply_dot": lambda: A.dot_inner(x, y, device=True),
                           "residual": lambda: A.residual(b, x, out=y),
                           "jacobi": lambda: A.jacobi_sweep(b, x, y, 2.0 / 3.0, want_norm=False),
                           "from_zero": lambda: A.jacobi_from_zero(b, y, 2.0 / 3.0, want_norm=False)}[kind]
@@ -92,7 +93,7 @@ def main():
     out = []
     for (ch, tcols, var, kind), ts in res.items():
         med = statistics.median(ts)
-        bpd = 16 if kind in ("apply", "dot", "from_zero") else 24
+        bpd = 16 if kind in ("apply", "apply_dot", "dot", "from_zero") else 24
         row = {"chunk": ch, "tile_cols": tcols, "aligned": not a.no_align, "variant": var, "kind": kind, "median_us": med, "min_us": min(ts),
                **({"launch_us": [round(t, 1) for t in ts]} if a.dump else {}),
                "GBps": bpd * dof / med / 1e3, "GDOFps": dof / med / 1e3}
