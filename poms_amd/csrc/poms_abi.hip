@@ -31,6 +31,7 @@ int vec_launch(int op, const RowGeom& g, double a, double b, const double* x, co
                double* z, double* w, const double* q, double* partial, hipStream_t st,
                int* nblk_out, const double* ab = nullptr);
 int reduce_launch(const double* partial, int count, double* out, hipStream_t st, int accumulate = 0);
+int reduce_wide_launch(const double* partial, int count, double* out, hipStream_t st, int accumulate = 0);
 int vec_flat_launch(int op, int64_t count, double a, double b, const double* x, const double* y,
                     double* z, double* w, const double* q, double* partial, hipStream_t st,
                     int* nblk_out, const double* ab = nullptr);
@@ -1052,7 +1053,7 @@ static int vec_common(poms_ctx* ctx, const poms_layout* L, int op, double a, dou
     if (!flat && vec_launch(op, g, a, b, x, y, z, w, q, red ? ctx->scratch : nullptr, as_stream(stream), &nb,
                             ab_dev))
         return 1;
-    if (red) reduce_launch(ctx->scratch, nb, out_dev, as_stream(stream));
+    if (red) reduce_wide_launch(ctx->scratch, nb, out_dev, as_stream(stream));
     POMS_HIP_CHECK(hipGetLastError());
     return 0;
 }

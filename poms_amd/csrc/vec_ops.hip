@@ -7,11 +7,18 @@
 // HBM-bound: 16-32 B per DOF, no reuse.
 #include "common.hpp"
 
+#include <cstdlib>
+
 namespace poms {
 
 enum VecOp : int { V_AXPBY = 0, V_SCALE = 1, V_FILL = 2, V_DOT = 3, V_PCGUPD = 4, V_RUPD = 5, V_XPUPD = 6 };
 
-constexpr int kMaxPartials = 4096;
+// grid caps (= partial sums per launch): the flat vector kernels run one pass per
+// thread up to 65536 blocks of 256 (grid-stride beyond): at 515^3 the r update
+// took 720 us with 4096 grid-stride blocks and 640 with 65536 (x/p update 1221 ->
+// 1042 us; profiles/r03/s3/vec_blocks_16k_64k.log); the per-row kernels keep 4096
+constexpr int kMaxPartials = 65536;
+constexpr int kMaxRowPartials = 4096;
 
 template <int OP>
 __global__ void __launch_bounds__(256)
@@ -183,6 +190,35 @@ reduce_partials_kernel(const double* __restrict__ partial, int count, double* __
     if (threadIdx.x == 0) out[0] = accumulate ? out[0] + t : t;
 }
 
+// Deterministic single-block reduction of many partials (the flat vector kernels'
+// up to kMaxPartials blocks): 1024 threads, each a strided running sum with four
+// independent accumulators, then the wave butterflies and the 16 wave sums in order.
+// (reduce_partials_kernel keeps its 256-thread order: the native loop's host-side
+// sums of the operator launches' partials reproduce it bit for bit.)
+__global__ void __launch_bounds__(1024)
+reduce_partials_wide_kernel(const double* __restrict__ partial, int count, double* __restrict__ out, int accumulate) {
+    __shared__ double red[16];
+    double s0 = 0.0, s1 = 0.0, s2 = 0.0, s3 = 0.0;
+    int i = threadIdx.x;
+    for (; i + 3 * 1024 < count; i += 4 * 1024) {
+        s0 += partial[i];
+        s1 += partial[i + 1024];
+        s2 += partial[i + 2 * 1024];
+        s3 += partial[i + 3 * 1024];
+    }
+    for (; i < count; i += 1024) s0 += partial[i];
+    double s = (s0 + s1) + (s2 + s3);
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) s += __shfl_xor(s, off, 64);
+    if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = s;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        double t = 0.0;
+        for (int w = 0; w < 16; ++w) t += red[w];
+        out[0] = accumulate ? out[0] + t : t;
+    }
+}
+
 // x = scale * b / diag(A), optional ||x||^2 partials.  diag(A) from the 1D
 // band diagonals exactly as in the fused kernels' JACOBI epilogue; the
 // axis-2 diagonals come as contiguous arrays (dg2a, dg2b) so the loads are
@@ -256,7 +292,7 @@ dense_matvec_kernel(const int n, const double* __restrict__ M, const double* __r
 static int row_blocks(const RowGeom& g) {
     const int64_t nrows = (int64_t)g.n0 * g.n1;
     int64_t nb = (nrows + 3) / 4;
-    if (nb > kMaxPartials) nb = kMaxPartials;
+    if (nb > kMaxRowPartials) nb = kMaxRowPartials;
     if (nb < 1) nb = 1;
     return (int)nb;
 }
@@ -333,7 +369,12 @@ int vec_flat_launch(int op, int64_t count, double a, double b, const double* x, 
     const int64_t nd2 = (count - head) / 2;
     const int tail = (int)((count - head) - 2 * nd2);
     int64_t nb = (nd2 + 256 * 4 - 1) / (256 * 4);
-    if (nb > kMaxPartials) nb = kMaxPartials;
+    static const int cap = [] {   // grid cap (tuning: POMS_VEC_BLOCKS, at most kMaxPartials)
+        const char* e = getenv("POMS_VEC_BLOCKS");
+        const int v = e ? atoi(e) : kMaxPartials;
+        return v < 64 ? 64 : v > kMaxPartials ? kMaxPartials : v;
+    }();
+    if (nb > cap) nb = cap;
     if (nb < 1) nb = 1;
     if (nblk_out) *nblk_out = (int)nb;
     switch (op) {
@@ -355,6 +396,12 @@ int vec_flat_launch(int op, int64_t count, double a, double b, const double* x, 
 
 int reduce_launch(const double* partial, int count, double* out, hipStream_t st, int accumulate) {
     hipLaunchKernelGGL(reduce_partials_kernel, dim3(1), dim3(256), 0, st, partial, count, out, accumulate);
+    return 0;
+}
+
+int reduce_wide_launch(const double* partial, int count, double* out, hipStream_t st, int accumulate) {
+    if (count <= 4096) return reduce_launch(partial, count, out, st, accumulate);
+    hipLaunchKernelGGL(reduce_partials_wide_kernel, dim3(1), dim3(1024), 0, st, partial, count, out, accumulate);
     return 0;
 }
 
