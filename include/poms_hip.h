@@ -141,7 +141,7 @@ int poms_op_set_tile_cols(poms_op* op, int cols);
  *       (3D FORM_SUM, arrays < 2 GiB, not at odd p with ghost corners; other
  *       operators, and two-sweeps-from-zero at p = 3 with distinct axis-1 /
  *       axis-2 Toeplitz rows, run variant 9);
- *  90-112 = diagnostic / tuning builds (memory-only, compute-only, cache policies;
+ *  90-113 = diagnostic / tuning builds (memory-only, compute-only, cache policies;
  *  110-112: two sweeps from zero without sums / x1 scaling, timing only).
  * Variants 4-10 need storage pads == pmax on every used axis.                  */
 int poms_op_set_variant(poms_op* op, int variant);

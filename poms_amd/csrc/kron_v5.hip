@@ -831,6 +831,10 @@ int kron_v5_launch(int pmax, int epi, const KronPtrs& p, const KronGeom& g, cons
 #ifndef POMS_V5_QUICK   // (POMS_V5_QUICK: p = 3 production builds only, for quick tuning builds)
     if (diag_mode) {   // DIAGNOSTIC / tuning builds (p = 3)
         if (pmax != 3) { set_error("v5 diag mode: p = 3 only"); return 1; }
+        if (diag_mode == 13) {   // Jacobi sweep (production ring depths) + nt on the x rows no other tile reads
+            if (epi != EPI_JACOBI) { set_error("v5 diag mode 13: Jacobi only"); return 1; }
+            return v5_launch_t<3, EPI_JACOBI, 4, 0, 14 | 64, true>(p, g, tc, H, omega, st);
+        }
         if (diag_mode >= 10 && diag_mode <= 12) {   // two sweeps from zero: 10 no sums, 11 no x1 scaling, 12 both
             if (epi != EPI_JACOBI0) { set_error("v5 diag mode 10-12: two sweeps from zero only"); return 1; }
             return diag_mode == 10 ? v5_launch_t<3, EPI_JACOBI0, 4, 3, 14>(p, g, tc, H, omega, st)

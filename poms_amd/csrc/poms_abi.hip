@@ -521,11 +521,12 @@ int poms_op_destroy(poms_op* o) {
 }
 
 int poms_op_set_variant(poms_op* op, int variant) {
-    // 90/91, 92-100, 101-112: diagnostic / tuning builds of v3, v4, v5 (110-112: v5
-    // two sweeps from zero without sums / x1 scaling, timing only)
+    // 90/91, 92-100, 101-113: diagnostic / tuning builds of v3, v4, v5 (110-112: v5
+    // two sweeps from zero without sums / x1 scaling, timing only; 113: the Jacobi
+    // sweep streaming the x rows no other tile reads)
     const bool known = variant == 0 || variant == 4 || (variant >= 7 && variant <= 10) ||
-                       (variant >= 90 && variant <= 112);
-    if (!op || !known) { set_error("poms_op_set_variant: bad argument (0, 4, 7, 8, 9, 10; 90-112 diagnostic)"); return 1; }
+                       (variant >= 90 && variant <= 113);
+    if (!op || !known) { set_error("poms_op_set_variant: bad argument (0, 4, 7, 8, 9, 10; 90-113 diagnostic)"); return 1; }
     if (variant > 0 && !op->v2_ok) { set_error("poms_op_set_variant: variant needs pads == pmax"); return 1; }
     op->variant = variant;
     return 0;
@@ -734,7 +735,7 @@ static int op_run(poms_op* o, int epi, double omega, const double* x, double* y,
     // Variant 10 (v5) runs apply / residual / Jacobi / apply+dot of 3D p <= 3
     // operators, and is what 8 picks for them; 9 otherwise.
     int v = resolve_variant(o, epi);
-    const int v5_diag = (v >= 101 && v <= 112) ? v - 100 : 0;   // v5 diagnostic / tuning builds
+    const int v5_diag = (v >= 101 && v <= 113) ? v - 100 : 0;   // v5 diagnostic / tuning builds
     if (v5_diag) v = 10;
     int v5_h = 0, v5_to = 0;
     if (v == 10) kron_v5_tile(o->pmax, v5_aligned(o, x), &v5_h, &v5_to);
