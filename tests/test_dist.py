@@ -83,16 +83,18 @@ def test_two_rank_distributed_operator_and_vcycle_gpu(device_reductions):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("world", [2, 3])
-def test_two_rank_native_schedule_with_peers_gpu(world):
+@pytest.mark.parametrize("world,boundary_on_cs", [(2, "1"), (3, "1"), (2, "0")])
+def test_two_rank_native_schedule_with_peers_gpu(world, boundary_on_cs):
     """The production slab schedule (poms_op_run_dist: exchange, interior planes,
-    both boundaries in one launch; lazy ring-slot norms; device-scalar pcg;
-    restriction all-reduce through the library communicator) with REAL
-    neighbours: the communicator's host transport moves the planes and sums over
-    gloo, since RCCL cannot pair ranks that share one GPU."""
+    both boundaries in one launch -- on the communication stream behind the
+    exchange, or with POMS_BOUNDARY_ON_CS=0 on the compute stream; lazy ring-slot
+    norms; device-scalar pcg; restriction all-reduce through the library
+    communicator) with REAL neighbours: the communicator's host transport moves the
+    planes and sums over gloo, since RCCL cannot pair ranks that share one GPU."""
     import torch
     assert torch.cuda.device_count() >= 1, "GPU test selected but no GPU visible"
-    _launch("gpu", world=world, extra_env={"POMS_TEST_DEVRED": "1", "POMS_TEST_HOST_TRANSPORT": "1"})
+    _launch("gpu", world=world, extra_env={"POMS_TEST_DEVRED": "1", "POMS_TEST_HOST_TRANSPORT": "1",
+                                           "POMS_BOUNDARY_ON_CS": boundary_on_cs})
 
 
 @pytest.mark.gpu
