@@ -686,6 +686,17 @@ static bool same_toeplitz12(const poms_op* o) {
     return true;
 }
 
+// 2D Jacobi sweeps at p <= 3: v3 (9) by default; POMS_JAC2D_VARIANT=7 selects v4
+// (tuning knob)
+static int jacobi2d_variant() {
+    static int v = -1;
+    if (v < 0) {
+        const char* e = getenv("POMS_JAC2D_VARIANT");
+        v = (e && atoi(e) == 7) ? 7 : 9;
+    }
+    return v;
+}
+
 // The kernel variant one launch of epilogue `epi` runs (see op_run).
 static int resolve_variant(const poms_op* o, int epi) {
     int v = o->variant;
@@ -700,6 +711,8 @@ static int resolve_variant(const poms_op* o, int epi) {
                       // axes 1 and 2 share their rows (the other build spills)
         else if (o->ndim == 3)
             v = ((epi == EPI_APPLY && o->pmax >= 3) || (plain && o->pmax >= 4)) ? 7 : 9;
+        else if (epi == EPI_JACOBI && o->pmax <= 3)
+            v = jacobi2d_variant();
         else
             v = ((epi == EPI_APPLY || epi == EPI_RESID) && o->pmax <= 3) ? 7 : 9;
     }
