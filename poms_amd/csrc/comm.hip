@@ -503,6 +503,7 @@ int poms_op_run_dist(poms_op* op, poms_comm* c, int epilogue, double omega, cons
         struct Hooks {
             static int ghosts_on(void* a, void* s) {   // `s` waits for the exchange
                 auto* c = static_cast<poms_comm*>(a);
+                if (!c->host && cstream(s) == c->cs) return 0;   // queued behind it already
                 POMS_HIP_CHECK(hipStreamWaitEvent(cstream(s), c->ev_halo, 0));
                 return 0;
             }

@@ -952,6 +952,9 @@ int op_run_split(poms_op* op, int epilogue, double omega, const double* x, doubl
     if (bs != stream && h.join(h.arg, bs, stream)) return 1;
     const int64_t n = n1 + op->last_partials;
     op->last_partials = 0;   // not in the layout poms_op_last_partials describes
+    // (the reductions stay on `stream`: queued on the boundary stream behind the
+    // boundary launch they added a second cross-queue wait per call -- loopback proxy
+    // 41.7 -> 43.5 ms, profiles/r03/proxy/reductions_on_cs_REVERTED/)
     if (wn) reduce_launch(op->ctx->scratch, (int)n, norm_out, as_stream(stream));
     if (wd) reduce_launch(op->ctx->scratch + kScratch / 2, (int)n, dot_out, as_stream(stream));
     POMS_HIP_CHECK(hipGetLastError());
