@@ -99,7 +99,7 @@ __device__ __forceinline__ void vec_elem(double a, double b, const double* x, co
     }
 }
 
-template <int OP>
+template <int OP, bool NTL = true>   // NTL: non-temporal loads (tuning: POMS_VEC_LOADS=plain)
 __global__ void __launch_bounds__(256)
 vec_flat_kernel(const int head, const int64_t nd2, const int tail, double a, double b,
                 const double* __restrict__ x, const double* __restrict__ yv, double* __restrict__ z,
@@ -125,11 +125,12 @@ vec_flat_kernel(const int head, const int64_t nd2, const int tail, double a, dou
                 // non-temporal loads as well as stores: each operand is streamed once
                 // (tools/ubench_copy.hip: 1 KiB per wave and load, nt loads + nt stores
                 // 6.1-6.2 TB/s against 5.7 with plain loads)
-                if constexpr (OP == V_AXPBY || OP == V_SCALE || OP == V_DOT || OP == V_XPUPD) xa[u] = __builtin_nontemporal_load(X + i);
-                if constexpr (OP == V_AXPBY || OP == V_DOT || OP == V_PCGUPD) ya[u] = __builtin_nontemporal_load(Y + i);
-                if constexpr (OP == V_PCGUPD || OP == V_XPUPD) za[u] = __builtin_nontemporal_load(Z + i);
-                if constexpr (OP == V_PCGUPD || OP == V_RUPD || OP == V_XPUPD) wa[u] = __builtin_nontemporal_load(Wv + i);
-                if constexpr (OP == V_PCGUPD || OP == V_RUPD) qa[u] = __builtin_nontemporal_load(Q + i);
+                auto ld = [](const d2* ptr) { if constexpr (NTL) return __builtin_nontemporal_load(ptr); else return *ptr; };
+                if constexpr (OP == V_AXPBY || OP == V_SCALE || OP == V_DOT || OP == V_XPUPD) xa[u] = ld(X + i);
+                if constexpr (OP == V_AXPBY || OP == V_DOT || OP == V_PCGUPD) ya[u] = ld(Y + i);
+                if constexpr (OP == V_PCGUPD || OP == V_XPUPD) za[u] = ld(Z + i);
+                if constexpr (OP == V_PCGUPD || OP == V_RUPD || OP == V_XPUPD) wa[u] = ld(Wv + i);
+                if constexpr (OP == V_PCGUPD || OP == V_RUPD) qa[u] = ld(Q + i);
             }
         }
 #pragma unroll
@@ -377,11 +378,19 @@ int vec_flat_launch(int op, int64_t count, double a, double b, const double* x, 
     if (nb > cap) nb = cap;
     if (nb < 1) nb = 1;
     if (nblk_out) *nblk_out = (int)nb;
+    static const bool plain = [] {
+        const char* e = getenv("POMS_VEC_LOADS");
+        return e && e[0] == 'p';
+    }();
     switch (op) {
 #define POMS_VF(OPV)                                                                                  \
     case OPV:                                                                                         \
-        hipLaunchKernelGGL(vec_flat_kernel<OPV>, dim3((int)nb), dim3(256), 0, st, head, nd2, tail, a, b, x, y, \
-                           z, w, q, partial, ab);                                                     \
+        if (plain)                                                                                    \
+            hipLaunchKernelGGL((vec_flat_kernel<OPV, false>), dim3((int)nb), dim3(256), 0, st, head, nd2, tail, a, b, \
+                               x, y, z, w, q, partial, ab);                                           \
+        else                                                                                          \
+            hipLaunchKernelGGL((vec_flat_kernel<OPV, true>), dim3((int)nb), dim3(256), 0, st, head, nd2, tail, a, b, \
+                               x, y, z, w, q, partial, ab);                                           \
         return 0;
         POMS_VF(V_AXPBY)
         POMS_VF(V_SCALE)
