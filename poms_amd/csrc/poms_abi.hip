@@ -641,8 +641,15 @@ static int op_geom(poms_op* o, int64_t zb, int64_t ze, KronGeom& g, int v = -1, 
     g.z2_end = (int)ze2;
     const int nz = (int)(ze - zb) + (int)(ze2 - zb2);
     int chunk = o->chunk;
-    if (chunk <= 0)
+    if (chunk <= 0) {
         chunk = auto_chunk(nz, g.tiles2 * g.tiles1, o->pmax, v == 10 ? 256.0 : 512.0);
+        // the v5 two-sweeps-from-zero launch (VALU-bound) balances better over twice
+        // as many chunks: 515^3 p = 3, 86 instead of 172 planes, 836-838 against
+        // 865-882 us in two interleaved sweeps, equal medians (833 us) in a third
+        // (profiles/r03/chunks/); the other epilogues keep the model's pick (Jacobi
+        // 715 us at 172 against 729 at 86)
+        if (v == 10 && epi == EPI_JACOBI0 && o->pmax == 3 && chunk / 2 >= 8 * o->pmax) chunk = (chunk + 1) / 2;
+    }
     chunk = std::max(1, std::min(chunk, std::max(nz, 1)));
     g.chunk = chunk;
     g.nch1 = (int)((ze - zb + chunk - 1) / chunk);
