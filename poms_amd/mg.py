@@ -143,7 +143,8 @@ class TwoLevelVCycle:
             from .solvers import pcg_kron
             xf2, info_pos = pcg_kron(A, self.glt, bf, x0=xf, tol=self.tol, maxiter=self.p + 1)
         else:
-            xf2, info_pos = pcg(A, damped_jacobi, bf, x0=xf, tol=self.tol, maxiter=self.maxiter)
+            # (xf is this cycle's own temporary: iterate in its buffer, no copy)
+            xf2, info_pos = pcg(A, damped_jacobi, bf, x0=xf, tol=self.tol, maxiter=self.maxiter, _x0_owned=True)
         return xf2, info_pre, info_pos
 
 

@@ -59,14 +59,18 @@ def _print_header(title):
     print("+---------+---------------------+")
 
 
-def pcg(A, psolve, b, x0=None, tol=1e-6, maxiter=100, verbose=False):
-    """Preconditioned conjugate gradient (`sources/solvers.py:69-135`)."""
+def pcg(A, psolve, b, x0=None, tol=1e-6, maxiter=100, verbose=False, *, _x0_owned=False):
+    """Preconditioned conjugate gradient (`sources/solvers.py:69-135`).
+
+    ``_x0_owned`` (internal: the V-cycle's own temporaries) lets the native loop
+    iterate in x0's buffer instead of a copy of it -- the reference copies x0
+    (`sources/solvers.py:82`); a caller that never reads x0 again loses nothing."""
     _check(A, b)
     V = b.space
     if (psolve is damped_jacobi and not verbose and V.lazy_reductions and A.apply_dot_supported
             and A.fused_dot_supported):
         if _native_ok(A, V):
-            return _pcg_native(A, b, x0, tol, maxiter)
+            return _pcg_native(A, b, x0, tol, maxiter, _x0_owned)
         return _pcg_device(A, b, x0, tol, maxiter)
     ctx, lay = V.ctx, V.layout
     if x0 is None:
@@ -173,7 +177,7 @@ def _native_ok(A, V) -> bool:
     return not V.is_distributed or V.dist.native is not None
 
 
-def _pcg_native(A, b, x0, tol, maxiter):
+def _pcg_native(A, b, x0, tol, maxiter, x0_owned=False):
     """pcg(A, damped_jacobi, b, x0, tol, maxiter) as one C call (``poms_pcg_jacobi``):
     the launches, device scalars and stop tests of :func:`_pcg_device`, bitwise the
     same iterates, without a Python round trip per launch."""
@@ -183,7 +187,7 @@ def _pcg_native(A, b, x0, tol, maxiter):
     work = getattr(A, "_pcg_work", None)
     if work is None or work[0].space is not V:
         work = A._pcg_work = [V.empty() for _ in range(5)]
-    x = V.zeros() if x0 is None else x0.copy()
+    x = V.zeros() if x0 is None else (x0 if x0_owned else x0.copy())
     if x0 is not None:
         assert x0.shape == (A.shape[0],)
     d = V.dist if V.is_distributed else None
