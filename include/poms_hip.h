@@ -388,6 +388,14 @@ typedef int (*poms_host_allreduce_fn)(void* user, double* buf, int64_t cnt);
 int poms_comm_create_host(int device, int rank, int nranks, poms_host_exchange_fn exchange,
                           poms_host_allreduce_fn allreduce, void* user, poms_comm** out);
 int poms_comm_is_host(poms_comm* comm, int* yes);
+/* Host transport on one node: attach the node-local shared-memory block named by
+ * `id` (id_len bytes, identical on every rank; collective over the ranks through
+ * the all-reduce callback) so that the lazily read sums (poms_comm_wait) are added
+ * in shared memory as on the RCCL path.  *attached = 0 when not every rank found
+ * all the others (the callback then keeps doing the sums).                     */
+int poms_comm_host_attach_shm(poms_comm* comm, const char* id, int id_len, int* attached);
+/* 1 when poms_comm_wait sums through the node-local shared-memory block.       */
+int poms_comm_uses_shm(poms_comm* comm, int* yes);
 /* data -> plane 0 of the padded local array (first ghost plane); the first /
  * last `width` owned planes go to prev / next (-1: none), the neighbours'
  * planes land in the ghost planes.  Starts after the work queued on `stream`;

@@ -85,6 +85,8 @@ _SIGS = {
     "poms_comm_stream": [_vp, _pp],
     "poms_comm_create_host": [_i, _i, _i, _vp, _vp, _vp, _pp],
     "poms_comm_is_host": [_vp, C.POINTER(_i)],
+    "poms_comm_host_attach_shm": [_vp, C.c_char_p, _i, C.POINTER(_i)],
+    "poms_comm_uses_shm": [_vp, C.POINTER(_i)],
     "poms_halo_start": [_vp, _vp, _i64, _i64, _i, _i, _i, _i, _vp],
     "poms_halo_finish": [_vp, _vp],
     "poms_allreduce_sum": [_vp, _vp, _i64, _vp, _i],

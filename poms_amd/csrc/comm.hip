@@ -113,9 +113,9 @@ static bool slot_unset(const double* v) {
 // this rank present.  Every rank calls this before ncclCommInitRank (a collective):
 // after it, all ranks of THIS node have marked themselves, and poms_comm_create
 // agrees over the ranks whether every rank found all the others.
-static void shm_open_block(poms_comm* c, const ncclUniqueId& id) {
-    uint64_t h = 1469598103934665603ull;   // FNV-1a of the unique id
-    for (size_t i = 0; i < sizeof(id); ++i) h = (h ^ (uint8_t)id.internal[i]) * 1099511628211ull;
+static void shm_open_block(poms_comm* c, const char* id, size_t id_len) {
+    uint64_t h = 1469598103934665603ull;   // FNV-1a of the id bytes
+    for (size_t i = 0; i < id_len; ++i) h = (h ^ (uint8_t)id[i]) * 1099511628211ull;
     char name[64];
     snprintf(name, sizeof(name), "/poms_comm_%016llx", (unsigned long long)h);
     c->shm_bytes = (size_t)(2 * c->nranks + 1) * sizeof(poms_comm::ShmSlot);
@@ -155,7 +155,7 @@ int poms_comm_create(int device, const char* id, int rank, int nranks, poms_comm
     c->device = device;
     ncclUniqueId uid;
     std::memcpy(&uid, id, sizeof(uid));
-    if (nranks > 1 && !getenv_off("POMS_COMM_SHM")) shm_open_block(c, uid);
+    if (nranks > 1 && !getenv_off("POMS_COMM_SHM")) shm_open_block(c, uid.internal, sizeof(uid.internal));
     // POMS_COMM_CTAS caps the workgroups of every RCCL kernel of this communicator
     // (ncclConfig_t::maxCTAs): an exchange overlapped with the interior launch takes
     // CUs from it, and the p-plane message needs few of them (tuning knob; unset =
@@ -256,6 +256,46 @@ int poms_comm_create_host(int device, int rank, int nranks, poms_host_exchange_f
         return 1;
     }
     *out = c;
+    return 0;
+}
+
+// Host transport: attach the node-local shared-memory block named by `id` (id_len
+// bytes, the same on every rank), so that host-read sums take shm_allsum exactly as
+// on the RCCL path of a one-node run.  Collective: the all-reduce callback serves as
+// the barrier after which every rank of the node has marked itself present, and
+// then as the agreement that every rank found all the others (the same answer
+// everywhere; otherwise the block is dropped and the sums keep the callback).
+// Lets the gloo tests run shm_allsum and poms_comm_wait's shared-memory branch,
+// which the 8-GPU RCCL run depends on (advisor / verdict, round 3).
+int poms_comm_host_attach_shm(poms_comm* c, const char* id, int id_len, int* attached) {
+    if (!c || !id || id_len < 1 || !attached) { set_error("poms_comm_host_attach_shm: bad argument"); return 1; }
+    *attached = 0;
+    if (!c->host) { set_error("poms_comm_host_attach_shm: not a host-transport communicator"); return 1; }
+    if (c->nranks < 2 || c->shm) {
+        *attached = c->shm ? 1 : 0;
+        return 0;
+    }
+    shm_open_block(c, id, (size_t)id_len);
+    double v[2] = {1.0, 0.0};
+    if (c->ar(c->user, v, 1)) { set_error("host transport: all-reduce callback failed"); return 1; }
+    if (c->shm && c->shm_name[0]) shm_unlink(c->shm_name);   // every rank of the node has it mapped now
+    const uint64_t present =
+        c->shm ? reinterpret_cast<std::atomic<uint64_t>*>(&c->shm[2 * c->nranks].seq)->load(std::memory_order_acquire)
+               : 0;
+    v[0] = present == (uint64_t)c->nranks ? 1.0 : 0.0;
+    if (c->ar(c->user, v, 1)) { set_error("host transport: all-reduce callback failed"); return 1; }
+    if (v[0] != (double)c->nranks) {
+        if (c->shm) munmap(c->shm, c->shm_bytes);
+        c->shm = nullptr;
+        return 0;
+    }
+    *attached = 1;
+    return 0;
+}
+
+int poms_comm_uses_shm(poms_comm* c, int* yes) {
+    if (!c || !yes) { set_error("poms_comm_uses_shm: null argument"); return 1; }
+    *yes = c->shm ? 1 : 0;
     return 0;
 }
 
@@ -456,10 +496,10 @@ int poms_comm_wait(poms_comm* c, int ticket) {
     std::atomic_thread_fence(std::memory_order_acquire);
     double v[2] = {slot[0], cnt > 1 ? slot[1] : 0.0};
     if (c->nranks > 1) {
-        if (c->host) {
-            if (c->ar(c->user, v, cnt)) { set_error("host transport: all-reduce callback failed"); return 1; }
-        } else if (c->shm) {
+        if (c->shm) {   // one node (RCCL ranks, or a host transport with the block attached)
             if (shm_allsum(c, v, cnt)) return 1;
+        } else if (c->host) {
+            if (c->ar(c->user, v, cnt)) { set_error("host transport: all-reduce callback failed"); return 1; }
         } else {   // ranks on several nodes: through RCCL, synchronously
             POMS_HIP_CHECK(hipMemcpyAsync(c->dev_tmp, v, cnt * sizeof(double), hipMemcpyHostToDevice, c->cs));
             POMS_NCCL_CHECK(ncclAllReduce(c->dev_tmp, c->dev_tmp, (size_t)cnt, ncclDouble, ncclSum, c->comm, c->cs));
@@ -496,7 +536,13 @@ int poms_op_run_dist(poms_op* op, poms_comm* c, int epilogue, double omega, cons
         dout = want_dot ? slot : nullptr;
         nout = want_norm ? slot + (want_dot ? 1 : 0) : nullptr;
     }
-    if (exchange && n_local > 2 * pmax) {
+    // the split (interior | boundaries) schedule only when an exchange is actually
+    // queued: with no neighbour (a one-rank loopback, a one-rank host transport)
+    // poms_halo_start records no event, and the boundary launch on the communication
+    // stream would not be ordered after the work on `stream` that wrote x
+    // (advisor, round 3)
+    const bool queued = exchange && pmax > 0 && (prev >= 0 || next >= 0);
+    if (queued && n_local > 2 * pmax) {
         if (poms_halo_start(c, xplanes, plane_elems, n_local, pad, pmax, prev, next, stream)) return 1;
         // the boundary launch runs on the communication stream behind the exchange
         // (POMS_BOUNDARY_ON_CS=0: on the caller's stream after it, as before)

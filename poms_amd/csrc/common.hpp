@@ -7,6 +7,9 @@
 namespace poms {
 
 constexpr int kBlock = 256;  // 4 wave64s per workgroup
+// doubles of the per-context partial-sum scratch (poms_ctx::scratch); every kernel
+// that writes per-block partials there caps its grid at this (vec_ops.hip asserts it)
+constexpr int64_t kScratch = 1 << 16;
 
 enum Form : int { FORM_SINGLE = 0, FORM_SUM = 1, FORM_STENCIL = 2 };
 enum Epi : int { EPI_APPLY = 0, EPI_RESID = 1, EPI_JACOBI = 2,

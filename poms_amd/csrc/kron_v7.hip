@@ -1,0 +1,487 @@
+// Fused Kronecker-sum operator, v7 (variant 11): flat lane mapping, axis 1 then
+// axis 2 through LDS windows, one barrier per plane.
+//
+// Why (round 4).  v5 (kron_v5.hip) gives each wave one output row of a 128-column
+// tile: 16 of its 128 lane-columns are halo, the last tile column of a 515-wide grid
+// holds 67 output columns in 128 lanes, and the axis-2 neighbours come in by 24 DPP
+// lane shifts per lane and plane -- 121 VALU instructions per lane and plane for
+// ~1.65 output points on average (profiles/r03/pmc_sq_v5_apply_jacobi.txt).  The
+// VALU is busy ~68 % of the kernel while the access pattern alone needs ~80 % of
+// its time, and at 4 waves per SIMD the two do not overlap better than that.
+//
+// v7 separates the two passes and lets the lanes of a workgroup map onto the tile
+// freely ("flat" pairs: lane L of wave W handles pair W*64+L in row-major order):
+//   * tile: R output rows x C output columns (C = 112 for the wide tile columns:
+//     7 whole 128-B lines of output per row on the aligned layout; the last tile
+//     column, when the grid is not a multiple of 112 wide, is CN < 112 columns wide
+//     and has more rows);
+//   * x tile: R+2P rows x XP pairs (XP = C/2 + 2 HP, HP = ceil(P/2) halo pairs a
+//     side), packed flat in LDS (pair q*XP + k) and DMA'd by buffer_load ... lds,
+//     64 pairs per instruction, into a D-deep ring, D-1 planes ahead;
+//   * stage 1, plane t: lane -> (row r, x pair k), R*XP <= 1024: u = F1a x and
+//     v = F1b x from the 2P+1 x-tile rows around r (one ds_read_b128 per tap at a
+//     constant offset), written into the u/v buffer of plane t (two slots);
+//   * stage 2, plane t-1: lane -> (row r, output pair j): the axis-2 window (2HP+1
+//     pairs of u and of v, read from LDS: no lane shifts), c = F2a u and
+//     d = F2a v + F2b u, then the axis-0 scatter into 2P+1 rotating accumulators and
+//     the epilogue of the finished plane;
+//   * one barrier per plane: after it x(t) has landed, u/v(t-1) is complete, and
+//     every wave has finished reading u/v(t-2) and x(t-1), whose slots the
+//     iteration then refills.
+//
+// Preconditions (host, v7_ok in poms_abi.hip): 3D FORM_SUM, P == 3, storage pads ==
+// P, line-aligned layout (row pitch a multiple of 16 doubles, interior column 0 on a
+// 128-B line), array < 2 GiB, every non-Toeplitz row / column of the axis-1 / axis-2
+// factors among the first or last P, and no data in the corner ghosts (as v5 at odd P).
+#include "common.hpp"
+
+#include <algorithm>
+#include <cstdlib>
+
+namespace poms {
+
+typedef __attribute__((address_space(3))) void lds7_void_t;
+
+struct V7Geom {
+    int nw2;        // wide tile columns (112 output columns each)
+    int cn;         // narrow last tile column: template width (0: none)
+    int rw, rn;     // output rows per wide / narrow tile
+    int t1w, t1n;   // tile rows of each type
+    int ntiles;     // nw2 * t1w + (cn ? t1n : 0)
+};
+
+constexpr int V7_NW = 16;           // waves per workgroup
+constexpr int V7_CW = 112;          // output columns of a wide tile
+constexpr int v7_hp(int P) { return (P + 1) / 2; }
+constexpr int v7_xp(int P, int C) { return C / 2 + 2 * v7_hp(P); }
+constexpr int v7_rmax(int P, int C) { return 1024 / v7_xp(P, C); }
+// x-tile DMAs per plane at the largest R the lanes allow (R * XP <= 1024)
+constexpr int v7_ndma(int P, int C) { return ((v7_rmax(P, C) + 2 * P) * v7_xp(P, C) + 63) / 64; }
+constexpr int v7_max(int a, int b) { return a > b ? a : b; }
+
+template <int AUX = 0>
+__device__ __forceinline__ void v7_dma16(__amdgpu_buffer_rsrc_t r, double* lds_dst, int voff, unsigned soff) {
+    __builtin_amdgcn_raw_ptr_buffer_load_lds(r, (lds7_void_t*)lds_dst, 16, voff, (int)soff, 0, AUX);
+}
+template <int AUX>
+__device__ __forceinline__ void v7_store16(__amdgpu_buffer_rsrc_t r, int voff, double d0, double d1) {
+    u32x4 v;
+    const u32x2 a = __builtin_bit_cast(u32x2, d0), b = __builtin_bit_cast(u32x2, d1);
+    v.x = a.x; v.y = a.y; v.z = b.x; v.w = b.y;
+    __builtin_amdgcn_raw_buffer_store_b128(v, r, voff, 0, AUX);
+}
+template <int N>
+__device__ __forceinline__ void v7_wait_vm() {  // s_waitcnt vmcnt(N) (gfx9 encoding)
+    static_assert(N >= 0 && N < 64, "vmcnt range");
+    __builtin_amdgcn_s_waitcnt((N & 15) | (7 << 4) | (15 << 8) | ((N >> 4) << 14));
+}
+__device__ __forceinline__ void v7_barrier() {
+    __asm__ volatile("" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    __asm__ volatile("" ::: "memory");
+}
+
+// LDS layout (doubles), shared by the two tile shapes of one launch
+template <int P, int D, int CN>
+struct V7Lds {
+    static constexpr int W = 2 * P + 1;
+    static constexpr int NDMA = v7_max(v7_ndma(P, V7_CW), CN ? v7_ndma(P, CN) : 0);
+    static constexpr int SLOT = 128 * NDMA;        // one x plane tile
+    static constexpr int XS = 0;
+    static constexpr int UVQ = 2048;               // one quantity (u or v) of one slot: 1024 pairs
+    static constexpr int UV = XS + D * SLOT;       // 2 slots x (u, v)
+    static constexpr int NBT = (2 * P + 1) * W * 2;   // boundary rows 0..P-1, n-P..n-1, the Toeplitz row
+    static constexpr int BT1 = UV + 4 * UVQ;
+    static constexpr int BT2 = BT1 + NBT;
+    static constexpr int RED = BT2 + NBT;
+    static constexpr int N = RED + V7_NW;
+};
+
+// One workgroup's march over its tile (R rows x C output columns) and axis-0 chunk.
+template <int P, int EPI, int D, int C, int CN, int CP, bool SAME12>
+__device__ __forceinline__ void v7_body(double* __restrict__ lds, const double* __restrict__ x,
+                                        double* __restrict__ y, const double* __restrict__ a0t,
+                                        const double* __restrict__ b0t, const KronGeom& g, const ToepConst& tc,
+                                        const int R, const int r0, const int c0, const int ch) {
+    typedef V7Lds<P, D, CN> L;
+    constexpr int W = L::W;
+    constexpr int NS = W;               // rotating axis-0 accumulators
+    constexpr int HP = v7_hp(P);
+    constexpr int XP = v7_xp(P, C);     // x pairs per x-tile row
+    constexpr int OP = C / 2;           // output pairs per row
+    constexpr int NWIN = 2 * HP + 1;    // window pairs of one quantity
+    constexpr int PFX = D - 1;          // x prefetch distance (planes)
+    constexpr int YAUX = (CP & 4) ? 2 : 0;
+    typedef double d2 __attribute__((ext_vector_type(2)));
+    static_assert(v7_ndma(P, C) <= 2 * V7_NW, "at most two x DMAs per wave and plane");
+#define T2A(k) (SAME12 ? tc.t1a[k] : tc.t2a[k])
+#define T2B(k) (SAME12 ? tc.t1b[k] : tc.t2b[k])
+
+    const int tid = threadIdx.x;
+    const int lane = tid & 63;
+    const int wv = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int fl = wv * 64 + lane;      // this lane's flat pair index
+
+    // stage-1 mapping (x pairs) and stage-2 mapping (output pairs); idle lanes read
+    // pair 0 (in range) and write nothing
+    const int ru = fl / XP;
+    const bool act1 = ru < R;
+    const int fu = act1 ? fl : 0;
+    const int ro = fl / OP, jo = fl - ro * OP;
+    const bool act2 = ro < R;
+    const int fo = act2 ? ro * XP + jo : 0;   // first window pair of this lane in the u/v buffer
+    const int orow = r0 + ro;           // output row (stage 2)
+    const int ocol = c0 + 2 * jo;       // output column of element 0
+
+    // tile-uniform fast paths: every row / column the tile computes is Toeplitz
+    const bool fast1 = r0 >= tc.lo1 && min(r0 + R, g.n1) <= tc.hi1;
+    const bool fast2 = c0 >= tc.lo2 && min(c0 + C, g.n2) <= tc.hi2;
+
+    int z0, z1;
+    chunk_planes(g, ch, z0, z1);
+    const int nplanes = (z1 - z0) + 2 * P;
+    const int nsp = g.n0 + 2 * g.pd0;
+    const int s1 = (int)g.s1;
+    const uint32_t arr_bytes = (uint32_t)((int64_t)nsp * g.s0 * 8);
+    const uint32_t plane8 = (uint32_t)(g.s0 * 8);
+    const __amdgpu_buffer_rsrc_t rx = make_rsrc(x, arr_bytes);
+    const __amdgpu_buffer_rsrc_t ry = make_rsrc(y, arr_bytes);
+
+    // ---- per-lane DMA voffsets (the plane goes into soffset): DMA i of a plane moves
+    // flat x pairs 64 i .. 64 i + 63; this wave issues i = wv and, if dma2, wv + 16.
+    // Pairs past the tile, rows past the padded rows and columns past the row pitch
+    // get a voffset out of the buffer range (+2^31, arrays < 2 GiB): no bytes move.
+    const int nxp = (R + 2 * P) * XP;
+    const bool dma2 = wv + V7_NW < (nxp + 63) / 64;
+    uint32_t xvo[2];
+#pragma unroll
+    for (int s = 0; s < 2; ++s) {
+        const int f = (wv + s * V7_NW) * 64 + lane;
+        const int q = f / XP, k = f - q * XP;
+        const int srow = r0 + q;        // x-tile row q = interior row r0 - P + q = storage row r0 + q
+        const int scol = g.pd2 + c0 - 2 * HP + 2 * k;
+        // (the pair at storage column -1 of storage row 0 -- the corner ghost -- is dropped,
+        // as in v5: zero unless the layout holds corner data, which v7_ok excludes)
+        const bool ok = f < nxp && srow < g.n1 + 2 * g.pd1 && srow * s1 + scol >= 0 && scol + 1 < s1;
+        xvo[s] = ok ? (uint32_t)((srow * s1 + scol) * 8) : 0x80000000u;
+    }
+
+    auto dma_x = [&](int t, int slot) {   // x plane t of the march (dummy past its end)
+        const int sp = z0 - P + t + g.pd0;
+        const bool ok = t < nplanes && sp >= 0 && sp < nsp;
+        const uint32_t so = ok ? (uint32_t)sp * plane8 : 0u;
+        double* dst = lds + L::XS + slot * L::SLOT + wv * 128;
+        v7_dma16<0>(rx, dst, ok ? (int)xvo[0] : (int)0x80000000u, so);
+        if (dma2) v7_dma16<0>(rx, dst + V7_NW * 128, ok ? (int)xvo[1] : (int)0x80000000u, so);
+    };
+
+    double acc[NS][2];
+#pragma unroll
+    for (int s = 0; s < NS; ++s) { acc[s][0] = 0.0; acc[s][1] = 0.0; }
+
+#pragma unroll
+    for (int i = 0; i < PFX; ++i) dma_x(i, i);
+
+    for (int tb = 0; tb <= nplanes; tb += NS) {
+#pragma unroll
+        for (int q = 0; q < NS; ++q) {
+            const int t = tb + q;
+            if (t <= nplanes) {
+                // ---- x(t) landed: own DMAs by vmcnt (the loads issued after x(t)'s are
+                // the DMAs of planes t+1 .. t+PFX-1), everyone's by the barrier
+                if (dma2) v7_wait_vm<2 * (PFX - 1)>();
+                else v7_wait_vm<PFX - 1>();
+                v7_barrier();
+                dma_x(t + PFX, (t + PFX) % D);
+
+                // ---- stage 1: u = F1a x, v = F1b x of plane t
+                if (t < nplanes) {
+                    const double* xs = lds + L::XS + (t % D) * L::SLOT + 2 * fu;
+                    d2 xv[W];
+#pragma unroll
+                    for (int k = 0; k < W; ++k) xv[k] = *(const d2*)(xs + 2 * k * XP);
+                    double u[2], v[2];
+                    if (fast1) {
+#pragma unroll
+                        for (int e = 0; e < 2; ++e) {
+                            double pr[P + 1];
+                            pr[0] = xv[P][e];
+#pragma unroll
+                            for (int k = 1; k <= P; ++k) pr[k] = xv[P - k][e] + xv[P + k][e];
+                            double su = tc.t1a[0] * pr[0], sv = tc.t1b[0] * pr[0];
+#pragma unroll
+                            for (int k = 1; k <= P; ++k) {
+                                su = fma(tc.t1a[k], pr[k], su);
+                                sv = fma(tc.t1b[k], pr[k], sv);
+                            }
+                            u[e] = su;
+                            v[e] = sv;
+                        }
+                    } else {
+                        const int row = r0 + ru;
+                        const int bi = row < P ? row : (row >= g.n1 - P ? P + row - (g.n1 - P) : 2 * P);
+                        const double* bt = lds + L::BT1 + 2 * W * (act1 ? bi : 2 * P);
+                        u[0] = u[1] = v[0] = v[1] = 0.0;
+#pragma unroll
+                        for (int k = 0; k < W; ++k) {
+                            const d2 f = *(const d2*)(bt + 2 * k);
+#pragma unroll
+                            for (int e = 0; e < 2; ++e) {
+                                u[e] = fma(f[0], xv[k][e], u[e]);
+                                v[e] = fma(f[1], xv[k][e], v[e]);
+                            }
+                        }
+                    }
+                    if (act1) {
+                        double* uv = lds + L::UV + (t & 1) * 2 * L::UVQ + 2 * fl;
+                        *(d2*)uv = d2{u[0], u[1]};
+                        *(d2*)(uv + L::UVQ) = d2{v[0], v[1]};
+                    }
+                }
+
+                // ---- stage 2: plane t-1 -- axis 2 from the u/v windows, axis 0, epilogue
+                if (t >= 1) {
+                    const int q2 = (q + NS - 1) % NS;   // (t - 1) mod NS (folded by the unroll)
+                    const int t2 = t - 1;
+                    const double* us = lds + L::UV + (t2 & 1) * 2 * L::UVQ + 2 * fo;
+                    double wu[2 * NWIN], wvv[2 * NWIN];
+#pragma unroll
+                    for (int m = 0; m < NWIN; ++m) {
+                        const d2 a = *(const d2*)(us + 2 * m);
+                        const d2 b = *(const d2*)(us + L::UVQ + 2 * m);
+                        wu[2 * m] = a[0];
+                        wu[2 * m + 1] = a[1];
+                        wvv[2 * m] = b[0];
+                        wvv[2 * m + 1] = b[1];
+                    }
+                    double cc[2], dd[2];
+                    if (fast2) {
+#pragma unroll
+                        for (int e = 0; e < 2; ++e) {
+                            constexpr int cen0 = 2 * HP;
+                            const int cen = cen0 + e;
+                            double pu[P + 1], pv[P + 1];
+                            pu[0] = wu[cen];
+                            pv[0] = wvv[cen];
+#pragma unroll
+                            for (int k = 1; k <= P; ++k) {
+                                pu[k] = wu[cen - k] + wu[cen + k];
+                                pv[k] = wvv[cen - k] + wvv[cen + k];
+                            }
+                            double c = T2A(0) * pu[0];
+                            double d = fma(T2A(0), pv[0], T2B(0) * pu[0]);
+#pragma unroll
+                            for (int k = 1; k <= P; ++k) {
+                                c = fma(T2A(k), pu[k], c);
+                                d = fma(T2A(k), pv[k], fma(T2B(k), pu[k], d));
+                            }
+                            cc[e] = c;
+                            dd[e] = d;
+                        }
+                    } else {
+#pragma unroll
+                        for (int e = 0; e < 2; ++e) {
+                            const int col = ocol + e;
+                            const int bi = col < P ? col : (col >= g.n2 - P ? P + col - (g.n2 - P) : 2 * P);
+                            const double* bt = lds + L::BT2 + 2 * W * (act2 ? bi : 2 * P);
+                            double c = 0.0, d = 0.0;
+#pragma unroll
+                            for (int k = 0; k < W; ++k) {
+                                const d2 f = *(const d2*)(bt + 2 * k);
+                                const int wi = 2 * HP - P + e + k;
+                                c = fma(f[0], wu[wi], c);
+                                d = fma(f[0], wvv[wi], fma(f[1], wu[wi], d));
+                            }
+                            cc[e] = c;
+                            dd[e] = d;
+                        }
+                    }
+
+                    // ---- axis 0: scatter into the rotating slots (scalar loads of the
+                    // axis-0 factor column of the global input plane)
+                    const int jrow = (g.g0 + z0 - P + t2 + P) * W;
+#pragma unroll
+                    for (int s = 0; s < W; ++s) {
+                        const int slot = (q2 - P + s + NS) % NS;
+                        const double ka = a0t[jrow + s];
+                        const double kb = b0t[jrow + s];
+#pragma unroll
+                        for (int e = 0; e < 2; ++e) acc[slot][e] = fma(ka, cc[e], fma(kb, dd[e], acc[slot][e]));
+                    }
+                    const int done = (q2 + P + 1) % NS;
+                    double vo[2] = {acc[done][0], acc[done][1]};
+                    acc[done][0] = 0.0;
+                    acc[done][1] = 0.0;
+                    const bool en = t2 >= 2 * P;
+                    const int zo = max(z0 - 2 * P + t2, z0);
+                    bool ok[2];
+#pragma unroll
+                    for (int e = 0; e < 2; ++e) ok[e] = en && act2 && orow < g.n1 && ocol + e < g.n2;
+                    double outv[2];
+                    if constexpr (EPI == EPI_APPLY) {
+                        outv[0] = vo[0];
+                        outv[1] = vo[1];
+                    }
+                    // one 16-B store per lane; a second column past n2 (ghost or dead pitch
+                    // column) is written 0.  The plane offset goes into voffset (gfx950 wait
+                    // state before a VALU overwrites a >8-B store's data VGPRs; see v5).
+                    const bool any = ok[0] || ok[1];
+                    const double o1 = ok[1] ? outv[1] : 0.0;
+                    const int voy = ((orow + g.pd1) * s1 + g.pd2 + ocol) * 8 + (zo + g.pd0) * (int)plane8;
+                    v7_store16<YAUX>(ry, any ? voy : (int)0x80000000u, outv[0], o1);
+                }
+            }
+        }
+    }
+    v7_wait_vm<0>();  // no LDS-DMA may outlive the workgroup
+#undef T2A
+#undef T2B
+}
+
+template <int P, int EPI, int D, int CN, int CP, bool SAME12>
+__global__ void __launch_bounds__(64 * V7_NW, 1)
+kron_v7_kernel(const double* __restrict__ x, double* __restrict__ y, const double* __restrict__ a0t,
+               const double* __restrict__ b0t, const double* __restrict__ a1, const double* __restrict__ b1,
+               const double* __restrict__ a2, const double* __restrict__ b2, const KronGeom g,
+               const ToepConst tc, const V7Geom vg) {
+    typedef V7Lds<P, D, CN> L;
+    constexpr int W = L::W;
+    __shared__ __attribute__((aligned(16))) double lds[L::N];
+
+    int bid;
+    {   // consecutive work items on one XCD (round-robin dispatch over the 8 XCDs)
+        const int nblk = gridDim.x;
+        const int b = blockIdx.x, q = nblk >> 3, rr = nblk & 7, xcd = b & 7, k = b >> 3;
+        bid = (xcd < rr ? xcd * (q + 1) : rr * (q + 1) + (xcd - rr) * q) + k;
+    }
+    const int tile = bid % vg.ntiles;
+    const int ch = bid / vg.ntiles;
+
+    // boundary coefficient tables (a, b interleaved) of both axes; entry 2P = the
+    // Toeplitz row (lanes on interior rows / columns of a boundary tile read it)
+    for (int e = threadIdx.x; e < (2 * P + 1) * W; e += V7_NW * 64) {
+        const int i = e / W, k = e - i * W;
+        const int r1 = i < P ? i : g.n1 - 2 * P + i;
+        const int r2 = i < P ? i : g.n2 - 2 * P + i;
+        const int ct = k < P ? P - k : k - P;
+        lds[L::BT1 + 2 * e] = i == 2 * P ? tc.t1a[ct] : a1[(int64_t)r1 * W + k];
+        lds[L::BT1 + 2 * e + 1] = i == 2 * P ? tc.t1b[ct] : b1[(int64_t)r1 * W + k];
+        lds[L::BT2 + 2 * e] = i == 2 * P ? (SAME12 ? tc.t1a[ct] : tc.t2a[ct]) : a2[(int64_t)r2 * W + k];
+        lds[L::BT2 + 2 * e + 1] = i == 2 * P ? (SAME12 ? tc.t1b[ct] : tc.t2b[ct]) : b2[(int64_t)r2 * W + k];
+    }
+    // (v7_body's first barrier orders these writes before any read)
+
+    const int nwide = vg.nw2 * vg.t1w;
+    if constexpr (CN > 0) {
+        if (tile >= nwide) {
+            const int t1 = tile - nwide;
+            v7_body<P, EPI, D, CN, CN, CP, SAME12>(lds, x, y, a0t, b0t, g, tc, vg.rn, t1 * vg.rn, vg.nw2 * V7_CW, ch);
+            return;
+        }
+    }
+    const int t1 = tile / vg.nw2, t2 = tile - t1 * vg.nw2;
+    v7_body<P, EPI, D, V7_CW, CN, CP, SAME12>(lds, x, y, a0t, b0t, g, tc, vg.rw, t1 * vg.rw, t2 * V7_CW, ch);
+}
+
+// Tile plan for an n1 x n2 plane at degree P: wide tiles of 112 columns, the rest
+// (if any) in one narrow column of width CN (a multiple of 16 below 112), rows
+// balanced over the tile rows of each type.
+static int v7_cn_of(int n2, int* nw2) {
+    int w = n2 / V7_CW, rem = n2 - w * V7_CW;
+    int cn = rem == 0 ? 0 : ((rem + 15) / 16) * 16;
+    if (cn > 96) { ++w; cn = 0; }   // the remainder takes a whole wide tile
+    *nw2 = w;
+    return cn;
+}
+
+static int v7_rows(int n1, int rmax) {
+    rmax = std::max(1, std::min(rmax, n1));
+    const int nt = (n1 + rmax - 1) / rmax;
+    return (n1 + nt - 1) / nt;
+}
+
+template <int P>
+static int v7_plan_p(int n1, int n2, V7Geom* vg) {
+    int nw2 = 0;
+    const int cn = v7_cn_of(n2, &nw2);
+    vg->nw2 = nw2;
+    vg->cn = cn;
+    vg->rw = v7_rows(n1, v7_rmax(P, V7_CW));
+    vg->t1w = (n1 + vg->rw - 1) / vg->rw;
+    if (cn) {
+        vg->rn = v7_rows(n1, v7_rmax(P, cn));
+        vg->t1n = (n1 + vg->rn - 1) / vg->rn;
+    } else {
+        vg->rn = vg->t1n = 0;
+    }
+    vg->ntiles = nw2 * vg->t1w + (cn ? vg->t1n : 0);
+    return 0;
+}
+
+// Number of (tile, chunk)-independent tiles of a v7 launch over an n1 x n2 plane.
+int kron_v7_tiles(int pmax, int n1, int n2) {
+    V7Geom vg{};
+    if (pmax != 3) return 0;
+    v7_plan_p<3>(n1, n2, &vg);
+    return vg.ntiles;
+}
+
+template <int P, int EPI, int D, int CN, int CP, bool SAME12>
+static int v7_launch_t(const KronPtrs& p, const KronGeom& g, const V7Geom& vg, const ToepConst& tc,
+                       hipStream_t st) {
+    // hand-counted vmcnt waits: a build that spills to scratch would break them
+    static int scratch = -1;
+    if (scratch < 0) {
+        hipFuncAttributes at{};
+        if (hipFuncGetAttributes(&at, reinterpret_cast<const void*>(&kron_v7_kernel<P, EPI, D, CN, CP, SAME12>)) !=
+            hipSuccess) {
+            set_error("v7: hipFuncGetAttributes failed");
+            return 1;
+        }
+        scratch = (int)at.localSizeBytes;
+    }
+    if (scratch > 0) {
+        set_error("v7: kernel build spills to scratch (vmcnt counting invalid)");
+        return 1;
+    }
+    const int nblk = vg.ntiles * g.nchunks;
+    hipLaunchKernelGGL((kron_v7_kernel<P, EPI, D, CN, CP, SAME12>), dim3(nblk), dim3(64 * V7_NW), 0, st, p.x, p.y,
+                       p.a0t, p.b0t, p.a1, p.b1, p.a2, p.b2, g, tc, vg);
+    return 0;
+}
+
+template <int P, int EPI, int D, int CP, bool SAME12>
+static int v7_launch_cn(const KronPtrs& p, const KronGeom& g, const V7Geom& vg, const ToepConst& tc,
+                        hipStream_t st) {
+    switch (vg.cn) {
+        case 0: return v7_launch_t<P, EPI, D, 0, CP, SAME12>(p, g, vg, tc, st);
+        case 16: return v7_launch_t<P, EPI, D, 16, CP, SAME12>(p, g, vg, tc, st);
+        case 32: return v7_launch_t<P, EPI, D, 32, CP, SAME12>(p, g, vg, tc, st);
+        case 48: return v7_launch_t<P, EPI, D, 48, CP, SAME12>(p, g, vg, tc, st);
+        case 64: return v7_launch_t<P, EPI, D, 64, CP, SAME12>(p, g, vg, tc, st);
+        case 80: return v7_launch_t<P, EPI, D, 80, CP, SAME12>(p, g, vg, tc, st);
+        case 96: return v7_launch_t<P, EPI, D, 96, CP, SAME12>(p, g, vg, tc, st);
+    }
+    set_error("v7: bad narrow tile width");
+    return 1;
+}
+
+int kron_v7_launch(int pmax, int epi, const KronPtrs& p, const KronGeom& g, const ToepConst& tc, double omega,
+                   hipStream_t st) {
+    (void)omega;
+    if (pmax != 3) { set_error("v7: p = 3 only"); return 1; }
+    V7Geom vg{};
+    v7_plan_p<3>(g.n1, g.n2, &vg);
+    if (vg.ntiles <= 0) return 0;
+    bool same = true;   // axis-1 / axis-2 Toeplitz rows, bitwise
+    for (int k = 0; k <= 3; ++k) same = same && tc.t1a[k] == tc.t2a[k] && tc.t1b[k] == tc.t2b[k];
+    switch (epi) {
+        case EPI_APPLY:
+            return same ? v7_launch_cn<3, EPI_APPLY, 4, 4, true>(p, g, vg, tc, st)
+                        : v7_launch_cn<3, EPI_APPLY, 4, 4, false>(p, g, vg, tc, st);
+    }
+    set_error("v7: epilogue not built");
+    return 1;
+}
+
+}  // namespace poms

@@ -25,6 +25,9 @@ int kron_v5_launch(int pmax, int epi, const KronPtrs& p, const KronGeom& g, cons
                    double omega, hipStream_t st, int diag_mode);
 void kron_v5_tile(int pmax, bool aligned, int* H, int* TO);
 int kron_v5_rows(int pmax, int epi);
+int kron_v7_launch(int pmax, int epi, const KronPtrs& p, const KronGeom& g, const ToepConst& tc, double omega,
+                   hipStream_t st);
+int kron_v7_tiles(int pmax, int n1, int n2);
 int kron_tile_rows();
 int kron_tile_cols();
 int vec_launch(int op, const RowGeom& g, double a, double b, const double* x, const double* y,
@@ -60,7 +63,6 @@ void band_lu_tables(int64_t n, int kl, int ku, const double* ab, int64_t ldab, c
                     std::vector<double>& L, std::vector<double>& U, std::vector<int>& piv);
 
 enum { V_AXPBY = 0, V_SCALE = 1, V_FILL = 2, V_DOT = 3, V_PCGUPD = 4, V_RUPD = 5, V_XPUPD = 6 };
-constexpr int64_t kScratch = 1 << 16;
 
 }  // namespace poms
 
@@ -524,9 +526,9 @@ int poms_op_set_variant(poms_op* op, int variant) {
     // 90/91, 92-100, 101-113: diagnostic / tuning builds of v3, v4, v5 (110-112: v5
     // two sweeps from zero without sums / x1 scaling, timing only; 113: the Jacobi
     // sweep streaming the x rows no other tile reads)
-    const bool known = variant == 0 || variant == 4 || (variant >= 7 && variant <= 10) ||
+    const bool known = variant == 0 || variant == 4 || (variant >= 7 && variant <= 11) ||
                        (variant >= 90 && variant <= 113);
-    if (!op || !known) { set_error("poms_op_set_variant: bad argument (0, 4, 7, 8, 9, 10; 90-113 diagnostic)"); return 1; }
+    if (!op || !known) { set_error("poms_op_set_variant: bad argument (0, 4, 7, 8, 9, 10, 11; 90-113 diagnostic)"); return 1; }
     if (variant > 0 && !op->v2_ok) { set_error("poms_op_set_variant: variant needs pads == pmax"); return 1; }
     op->variant = variant;
     return 0;
@@ -603,6 +605,17 @@ static bool v5_aligned(const poms_op* o, const double* x) {
     return pitch % 16 == 0 && (reinterpret_cast<uintptr_t>(x + o->L.pads[2]) & 127) == 0;
 }
 
+// v7 (variant 11, kron_v7.hip) runs 3D FORM_SUM operators at p = 3 on the
+// line-aligned layout whose non-Toeplitz axis-1 / axis-2 rows are among the first
+// and last p (uniform knots; the boundary tables hold 2p rows), with v5's corner rule.
+static bool v7_ok(const poms_op* o, const double* x, const double* y) {
+    if (!(v5_ok(o) && o->pmax == 3 && v5_aligned(o, x) && v5_aligned(o, y) && !o->ghost_corners)) return false;
+    const int P = o->pmax;
+    const int64_t n1 = o->L.n[1], n2 = o->L.n[2];
+    return n1 >= 4 * P && n2 >= 4 * P && o->tc.lo1 <= P && o->tc.hi1 >= n1 - P && o->tc.lo2 <= P &&
+           o->tc.hi2 >= n2 - P;
+}
+
 static int op_geom(poms_op* o, int64_t zb, int64_t ze, KronGeom& g, int v = -1, int v5_to = 0,
                    int64_t zb2 = 0, int64_t ze2 = 0, int epi = EPI_APPLY) {
     if (v < 0) v = o->variant;
@@ -618,6 +631,10 @@ static int op_geom(poms_op* o, int64_t zb, int64_t ze, KronGeom& g, int v = -1, 
     g.tiles1 = (int)((o->L.n[1] + trows - 1) / trows);
     g.tout = v == 10 ? v5_to : (o->tout > 0 ? o->tout : 64 - 2 * o->pmax);
     if (v >= 4) g.tiles2 = (int)((o->L.n[2] + g.tout - 1) / g.tout);
+    if (v == 11) {   // v7: the kernel maps its tiles itself; one flat tile index
+        g.tiles2 = 1;
+        g.tiles1 = kron_v7_tiles(o->pmax, (int)o->L.n[1], (int)o->L.n[2]);
+    }
     if (!is3d) {
         g.z_begin = 0; g.z_end = 1; g.chunk = 1; g.nchunks = 1; g.nch1 = 1; g.z2_begin = g.z2_end = 0;
         return 0;
@@ -642,7 +659,7 @@ static int op_geom(poms_op* o, int64_t zb, int64_t ze, KronGeom& g, int v = -1, 
     const int nz = (int)(ze - zb) + (int)(ze2 - zb2);
     int chunk = o->chunk;
     if (chunk <= 0) {
-        chunk = auto_chunk(nz, g.tiles2 * g.tiles1, o->pmax, v == 10 ? 256.0 : 512.0);
+        chunk = auto_chunk(nz, g.tiles2 * g.tiles1, o->pmax, (v == 10 || v == 11) ? 256.0 : 512.0);
         // the v5 two-sweeps-from-zero launch (VALU-bound) balances better over twice
         // as many chunks: 515^3 p = 3, 86 instead of 172 planes, 836-838 against
         // 865-882 us in two interleaved sweeps, equal medians (833 us) in a third
@@ -723,6 +740,8 @@ static int resolve_variant(const poms_op* o, int epi) {
         else
             v = ((epi == EPI_APPLY || epi == EPI_RESID) && o->pmax <= 3) ? 7 : 9;
     }
+    // v7: the apply at p = 3 (alignment and the Toeplitz ranges are checked per call)
+    if (v == 11 && !(epi == EPI_APPLY && v5_ok(o) && o->pmax == 3 && !o->ghost_corners)) v = 10;
     if (v == 10 && (!v5_ok(o) || (epi == EPI_JACOBI0 && o->pmax == 3 && !same_toeplitz12(o)))) v = 9;
     return v;
 }
@@ -755,6 +774,7 @@ static int op_run(poms_op* o, int epi, double omega, const double* x, double* y,
     // Variant 10 (v5) runs apply / residual / Jacobi / apply+dot of 3D p <= 3
     // operators, and is what 8 picks for them; 9 otherwise.
     int v = resolve_variant(o, epi);
+    if (v == 11 && !v7_ok(o, x, y)) v = 10;
     const int v5_diag = (v >= 101 && v <= 113) ? v - 100 : 0;   // v5 diagnostic / tuning builds
     if (v5_diag) v = 10;
     int v5_h = 0, v5_to = 0;
@@ -793,7 +813,9 @@ static int op_run(poms_op* o, int epi, double omega, const double* x, double* y,
         tlh->ndof = (int64_t)((ze - zb) + (ze2 - zb2)) * g.n1 * g.n2;
         POMS_HIP_CHECK(hipEventRecord(tlh->e0, as_stream(stream)));
     }
-    const int rc = v == 10
+    const int rc = v == 11
+        ? kron_v7_launch(o->pmax, epi, p, g, o->tc, omega, as_stream(stream))
+        : v == 10
         ? kron_v5_launch(o->pmax, epi, p, g, o->tc, v5_h, omega, as_stream(stream), v5_diag)
         : v == 0
         ? kron_launch(o->pmax, o->ndim == 3, o->form, epi, p, g, omega, as_stream(stream))
@@ -1715,13 +1737,11 @@ struct PcgRun {
         return h;
     }
     static int64_t host_partials_max() {   // tuning: POMS_HOST_PARTIALS (0: always reduce on the device)
-        static int64_t m = -1;
-        if (m < 0) {
-            const char* e = getenv("POMS_HOST_PARTIALS");
-            m = e ? std::max<int64_t>(0, atoll(e)) : poms_op::kSvPart / 2;
-            m = std::min<int64_t>(m, poms_op::kSvPart / 2);
-        }
-        return m;
+        // read per launch (a getenv against a kernel launch): the parity tests switch it
+        // inside one process to run the device-reduction fall-back
+        const char* e = getenv("POMS_HOST_PARTIALS");
+        const int64_t m = e ? std::max<int64_t>(0, atoll(e)) : poms_op::kSvPart / 2;
+        return std::min<int64_t>(m, poms_op::kSvPart / 2);
     }
     // Wait for every partial of slot h's region and add them on the host in the
     // order of reduce_partials_kernel (256 strided running sums, the 64-lane xor
@@ -1777,13 +1797,24 @@ struct PcgRun {
         volatile uint64_t* q = reinterpret_cast<volatile uint64_t*>(v);
         for (int i = 0; i < n; ++i) q[i] = kPartUnset;
     }
+    // A failed wait (the shm sum timed out, a launch never wrote its sum) sets
+    // `failed` and keeps poms_comm_wait's message: the loop returns 1 at its next
+    // check instead of carrying a NaN into the stop tests (advisor, round 3).
+    bool failed = false;
+    double fail() {
+        failed = true;
+        return std::nan("");
+    }
     double get(int h, int i = 0) {
         if (!direct()) {
-            if (poms_comm_wait(comm, tk[h])) return std::nan("");
+            if (poms_comm_wait(comm, tk[h])) return fail();
             return host[h + i];
         }
         if (op->sv_npart[h] > 0) {
-            if (settle_partials(h)) return std::nan("");
+            if (settle_partials(h)) {
+                set_error("poms_pcg_jacobi: a launch did not write its partial sums");
+                return fail();
+            }
             op->sv_done = std::max(op->sv_done, op->sv_seq[h] + 1);
             return host[h + i];
         }
@@ -1792,7 +1823,10 @@ struct PcgRun {
             __builtin_ia32_pause();
             if ((n & 4095) == 0 && hipStreamQuery(st) != hipErrorNotReady) {   // stream drained (or failed)
                 std::atomic_thread_fence(std::memory_order_seq_cst);
-                if (*v == -1.0) return std::nan("");   // never written: the launch failed
+                if (*v == -1.0) {   // never written: the launch failed
+                    set_error("poms_pcg_jacobi: a launch did not write its sum");
+                    return fail();
+                }
             }
         }
         std::atomic_thread_fence(std::memory_order_acquire);
@@ -1851,7 +1885,7 @@ struct PcgRun {
                 res = x;
             }
             pend = 0;
-            return 0;
+            return failed ? 1 : 0;
         };
         for (int k = k0; k <= maxit; ++k) {
             const bool last = k == maxit;
@@ -1925,6 +1959,7 @@ int poms_pcg_jacobi(poms_op* op, poms_comm* comm, const poms_pcg_opts* o, const 
         if (!d || poms_vec_dot(ctx, L, r, r, d, stream) || R.lazy_post(hrr0, 1)) return 1;
     }
     const double nrmr0 = std::sqrt(R.get(hrr0));
+    if (R.failed) return 1;
     double* s = nullptr;
     int dd = 0;
     if (R.damped_jacobi(r, z[0], z[1], SC_SR, &s, &dd)) return 1;
@@ -1947,6 +1982,7 @@ int poms_pcg_jacobi(poms_op* op, poms_comm* comm, const poms_pcg_opts* o, const 
         if (R.damped_jacobi(r, fa, fb, SC_SRN, &sn, &dd)) return 1;   // queued before the read
         if (!dd && R.dot(sn, r, R.sc + SC_SRN)) return 1;
         nrmr = R.get(hrr);
+        if (R.failed) return 1;
         if (nrmr < o->tol * nrmr0) {   // the reference stops before psolve: that one is discarded
             if (poms_vec_axpby_dev(ctx, L, R.sc + SC_ONE, x, p, x, stream)) return 1;
             k -= 1;

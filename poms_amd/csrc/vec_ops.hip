@@ -19,6 +19,8 @@ enum VecOp : int { V_AXPBY = 0, V_SCALE = 1, V_FILL = 2, V_DOT = 3, V_PCGUPD = 4
 // 1042 us; profiles/r03/s3/vec_blocks_16k_64k.log); the per-row kernels keep 4096
 constexpr int kMaxPartials = 65536;
 constexpr int kMaxRowPartials = 4096;
+static_assert(kMaxPartials <= kScratch && kMaxRowPartials <= kScratch,
+              "vector-kernel partials must fit the context scratch (advisor, round 3)");
 
 template <int OP>
 __global__ void __launch_bounds__(256)

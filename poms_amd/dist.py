@@ -62,13 +62,15 @@ class SlabDistribution:
 
     @classmethod
     def from_process_group(cls, n0_global: int, group=None, device_reductions: bool | None = None,
-                           host_transport: bool = False) -> "SlabDistribution":
+                           host_transport: bool = False, host_shm: bool = False) -> "SlabDistribution":
         """Slab of this rank.  With the ``nccl`` (RCCL) backend the library's own
         communicator is used (``POMS_NATIVE_COMM=0`` selects torch.distributed
         instead); if it cannot be created or fails its self-test this RAISES --
         a silent fall-back would hide a broken production path.  ``host_transport``
         (any backend, e.g. gloo): the same native schedule with the data moved by
-        torch.distributed host callbacks (``poms_comm_create_host``)."""
+        torch.distributed host callbacks (``poms_comm_create_host``); ``host_shm``
+        adds the node-local shared-memory block for the host-read sums, the path
+        every lazily read norm takes in a one-node RCCL run."""
         import torch.distributed as dist
         backend = dist.get_backend(group)
         d = cls(n0_global, dist.get_rank(group), dist.get_world_size(group), group,
@@ -76,7 +78,7 @@ class SlabDistribution:
         if host_transport:
             if d.device_reductions is None or not d.device_reductions:
                 d.device_reductions = True
-            d.native = NativeComm.create_host(group)
+            d.native = NativeComm.create_host(group, shm=host_shm)
         elif backend == "nccl" and d.world > 1 and os.environ.get("POMS_NATIVE_COMM", "1") != "0":
             d.native = NativeComm.create(group)
         return d
@@ -355,6 +357,15 @@ class NativeComm:
         _lib.call("poms_comm_is_host", self.h, C.byref(yes))
         self.is_host = bool(yes.value)
 
+    @property
+    def uses_shm(self) -> bool:
+        """The lazily read sums go through the node-local shared-memory block."""
+        import ctypes as C
+        from . import _lib
+        yes = C.c_int()
+        _lib.call("poms_comm_uses_shm", self.h, C.byref(yes))
+        return bool(yes.value)
+
     @classmethod
     def create(cls, group=None):
         """RCCL communicator over the group's ranks, self-tested; raises on failure."""
@@ -394,14 +405,17 @@ class NativeComm:
         return comm
 
     @classmethod
-    def create_host(cls, group=None):
+    def create_host(cls, group=None, shm: bool = False):
         """The native schedule over torch.distributed host callbacks (any backend).
 
         The C side stages the boundary planes / scalars through host memory and
         calls back: the exchange is one ``batch_isend_irecv`` with rank +-1 on CPU
         tensors, the sum one ``all_reduce``.  Used by the multi-rank tests to drive
         ``poms_op_run_dist``'s schedule with real neighbours where RCCL cannot run
-        (several ranks on one GPU)."""
+        (several ranks on one GPU).  ``shm``: attach the node-local shared-memory
+        block (``poms_comm_host_attach_shm``, id broadcast from rank 0) so that the
+        lazily read sums run ``shm_allsum`` as in a one-node RCCL run; raises if
+        the ranks do not all find each other in it."""
         import ctypes as C
         import numpy as np
         import torch.distributed as dist
@@ -445,6 +459,13 @@ class NativeComm:
         _lib.call("poms_comm_create_host", dev, dist.get_rank(group), dist.get_world_size(group),
                   C.cast(cbs[0], C.c_void_p), C.cast(cbs[1], C.c_void_p), None, C.byref(h))
         comm = cls(h, dev, callbacks=cbs)
+        if shm and dist.get_world_size(group) > 1:
+            obj = [os.urandom(32) if dist.get_rank(group) == 0 else None]
+            dist.broadcast_object_list(obj, src=peer(0), group=group)
+            att = C.c_int()
+            _lib.call("poms_comm_host_attach_shm", comm.h, C.c_char_p(obj[0]), len(obj[0]), C.byref(att))
+            if not att.value:
+                raise RuntimeError("host transport: the node-local shared-memory block was not attached on every rank")
         comm._check_self_test(group)
         return comm
 
@@ -479,6 +500,18 @@ class NativeComm:
         nxt = rank + 1 if rank + 1 < world else -1
         self.halo_start(data, n_loc, pad, width, prev, nxt, rt.stream_handle())
         self.halo_finish(rt.stream_handle())
+        # one round of the host-read sums (the damped-Jacobi / pcg stop tests): the
+        # rank's value goes straight into a ring slot (pinned host memory, the same
+        # address on the host), the wait adds the ranks' values on the host -- through
+        # the node-local shared-memory block when attached (one-node RCCL runs)
+        import ctypes as C
+        addr, ticket = self.slot()
+        vals = (C.c_double * 2).from_address(addr)
+        vals[0], vals[1] = float(rank + 1), float(2 * rank + 1)
+        host_slot = torch.zeros(2, dtype=torch.float64)
+        lz = self.to_host(ticket, 2, host_slot, rt.stream_handle())
+        s0, s1 = lz.value(0), lz.value(1)
+        ok = ok and s0 == world * (world + 1) / 2.0 and s1 == float(world * world)
         h = data.cpu()
         for j in range(width):
             lo = h[pad - width + j]   # planes n_loc-width+j of rank-1

@@ -129,8 +129,11 @@ def run_gpu():
     rng = np.random.default_rng(3)
     xg, bg = rng.standard_normal((n, n, n)), rng.standard_normal((n, n, n))
     host_tr = os.environ.get("POMS_TEST_HOST_TRANSPORT") == "1"
-    d = SlabDistribution.from_process_group(n, host_transport=host_tr)
+    host_shm = os.environ.get("POMS_TEST_HOST_SHM") == "1"
+    d = SlabDistribution.from_process_group(n, host_transport=host_tr, host_shm=host_shm)
     check(d.transport == ("native-host" if host_tr else "torch"), f"transport {d.transport}")
+    if host_tr:   # the host-read sums take the node-local shared-memory block when asked
+        check(d.native.uses_shm == host_shm, f"shm attached {d.native.uses_shm}")
     V = StencilVectorSpace([n] * 3, [p] * 3, dist=d)
     A = KronOperator.laplace(V, [M] * 3, [K] * 3)
     x, b = V.zeros().from_numpy(xg), V.zeros().from_numpy(bg)
@@ -167,7 +170,8 @@ def run_gpu():
     # two-level V-cycle over the slabs vs the global oracle (p=2: stable smoother)
     devred = os.environ.get("POMS_TEST_DEVRED") == "1"
     mg = TwoLevelVCycle(2, 16, 4, ndim=3, dist=SlabDistribution.from_process_group(18, device_reductions=devred,
-                                                                                   host_transport=host_tr))
+                                                                                   host_transport=host_tr,
+                                                                                   host_shm=host_shm))
     assert mg.space.lazy_reductions == devred or not devred
     bf = mg.rhs_ones()
     xf2, ipre, ipos = mg.cycle(bf)
@@ -181,6 +185,72 @@ def run_gpu():
     err = rel(got.numpy().reshape(xr.shape), xr)
     check(err <= tol, f"distributed V-cycle {err} > {tol}")
     check(ipre["niter"] == ipre_r["niter"] and ipos["niter"] == ipos_r["niter"], "iteration counts")
+
+
+def run_gpu_fullsize_slabs():
+    """The headline grid (515^3, p = 3; POMS_TEST_FULL_N cells) split over the ranks
+    exactly as the 8-GPU run splits it (65/64-plane slabs), every rank on cuda:0, the
+    production schedule (poms_op_run_dist, poms_pcg_jacobi) over the host transport
+    with the node-local shared-memory sums attached -- the code the driver's 8-GPU run
+    executes, bar RCCL's byte moves.  Each rank also builds the whole grid and runs
+    the same operations on one GPU; its slab of every result must agree to 1e-13
+    (fixed counts: apply, residual, a Jacobi sweep and its norm, the lazily read norm,
+    damped Jacobi, pcg with damped Jacobi) with identical iteration counts
+    (`sources/solvers.py:69-135, 167-235`)."""
+    import torch
+    from poms_amd import solvers
+    from poms_amd.stencil import KronOperator, StencilVectorSpace
+    torch.cuda.set_device(0)
+    p, N = 3, int(os.environ.get("POMS_TEST_FULL_N", "512"))
+    n = N + p
+    M, K = assemble_1d(uniform_knots(p, N), p)
+    d = SlabDistribution.from_process_group(n, host_transport=True, host_shm=True)
+    check(d.native.uses_shm, "node-local shared-memory sums attached")
+    Vl = StencilVectorSpace([n] * 3, [p] * 3, dist=d, align=True)
+    Al = KronOperator.laplace(Vl, [M] * 3, [K] * 3)
+    Vg = StencilVectorSpace([n] * 3, [p] * 3, align=True)
+    Ag = KronOperator.laplace(Vg, [M] * 3, [K] * 3)
+    gen = torch.Generator(device="cuda").manual_seed(17)
+    xg, bg = Vg.zeros(), Vg.zeros()
+    Vg.interior(xg._data).uniform_(-1, 1, generator=gen)
+    Vg.interior(bg._data).uniform_(-1, 1, generator=gen)
+    sl = slice(d.start, d.end)
+
+    def local(vg):
+        v = Vl.zeros()
+        Vl.interior(v._data).copy_(Vg.interior(vg._data)[sl])
+        return v
+
+    def cmp(tag, vl, vg, tol=1e-13):
+        a, b = Vl.interior(vl._data), Vg.interior(vg._data)[sl]
+        err = float(torch.linalg.vector_norm(a - b) / torch.linalg.vector_norm(b))
+        check(err <= tol, f"{tag}: slab vs one GPU, rel {err:.3e}")
+        return err
+
+    xl, bl = local(xg), local(bg)
+    errs = {"apply": cmp("apply", Al.dot(xl), Ag.dot(xg))}
+    errs["residual"] = cmp("residual", Al.residual(bl, xl), Ag.residual(bg, xg))
+    w = 2.0 / 3.0
+    xol, xog = Vl.zeros(), Vg.zeros()
+    nl = Al.jacobi_sweep(bl, xl, xol, w, want_norm=True)
+    ng = Ag.jacobi_sweep(bg, xg, xog, w, want_norm=True)
+    errs["jacobi"] = cmp("jacobi sweep", xol, xog)
+    check(abs(nl - ng) <= 1e-13 * ng, f"sweep norm {nl} vs {ng}")
+    lz = Al.jacobi_sweep(bl, xl, xol, w, want_norm=True, lazy=True)
+    check(abs(lz.value() - ng) <= 1e-13 * ng, f"lazy (shared-memory) sweep norm {lz.value()} vs {ng}")
+    errs["damped_jacobi"] = cmp("damped_jacobi", solvers.damped_jacobi(Al, bl, maxiter=10),
+                                solvers.damped_jacobi(Ag, bg, maxiter=10))
+    for m in (1, 2):
+        xl2, il = solvers.pcg(Al, solvers.damped_jacobi, bl, tol=0.0, maxiter=m)
+        xg2, ig = solvers.pcg(Ag, solvers.damped_jacobi, bg, tol=0.0, maxiter=m)
+        check(il["niter"] == ig["niter"] == m, f"pcg niter {il['niter']} / {ig['niter']}")
+        errs[f"pcg{m}"] = cmp(f"pcg maxiter {m}", xl2, xg2)
+        check(abs(il["res_norm"] - ig["res_norm"]) <= 1e-12 * ig["res_norm"], f"pcg res_norm {il} {ig}")
+    # the reference's stop test decides (tol 1e-6): both stop at the same iteration
+    xl3, il = solvers.pcg(Al, solvers.damped_jacobi, bl, tol=1e-6, maxiter=10)
+    xg3, ig = solvers.pcg(Ag, solvers.damped_jacobi, bg, tol=1e-6, maxiter=10)
+    check(il["niter"] == ig["niter"] and il["success"] == ig["success"], f"pcg stop {il} vs {ig}")
+    print(f"rank {dist.get_rank()} slab [{d.start}, {d.end}) errors {errs}", flush=True)
 
 
 def run_gpu_ksolve():
@@ -487,7 +557,8 @@ def main():
     mode = sys.argv[1]
     dist.init_process_group("gloo")
     try:
-        {"cpu": run_cpu, "gpu": run_gpu, "gpu_ksolve": run_gpu_ksolve, "cart_cpu": run_cart_cpu,
+        {"cpu": run_cpu, "gpu": run_gpu, "gpu_ksolve": run_gpu_ksolve, "gpu_fullsize_slabs": run_gpu_fullsize_slabs,
+         "cart_cpu": run_cart_cpu,
          "cart_gpu": run_cart_gpu, "cart_ksolve": run_cart_ksolve}[mode]()
         dist.barrier()
         print(f"rank {dist.get_rank()} ok", flush=True)

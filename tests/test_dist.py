@@ -83,18 +83,31 @@ def test_two_rank_distributed_operator_and_vcycle_gpu(device_reductions):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("world,boundary_on_cs", [(2, "1"), (3, "1"), (2, "0")])
-def test_two_rank_native_schedule_with_peers_gpu(world, boundary_on_cs):
+@pytest.mark.parametrize("world,boundary_on_cs,shm", [(2, "1", "0"), (3, "1", "0"), (2, "0", "0"),
+                                                      (2, "1", "1"), (3, "1", "1")])
+def test_two_rank_native_schedule_with_peers_gpu(world, boundary_on_cs, shm):
     """The production slab schedule (poms_op_run_dist: exchange, interior planes,
     both boundaries in one launch -- on the communication stream behind the
     exchange, or with POMS_BOUNDARY_ON_CS=0 on the compute stream; lazy ring-slot
     norms; device-scalar pcg; restriction all-reduce through the library
     communicator) with REAL neighbours: the communicator's host transport moves the
-    planes and sums over gloo, since RCCL cannot pair ranks that share one GPU."""
+    planes and sums over gloo, since RCCL cannot pair ranks that share one GPU.
+    shm=1: the host-read sums go through the node-local shared-memory block
+    (shm_allsum, poms_comm_wait's shared-memory branch) as in a one-node RCCL run."""
     import torch
     assert torch.cuda.device_count() >= 1, "GPU test selected but no GPU visible"
     _launch("gpu", world=world, extra_env={"POMS_TEST_DEVRED": "1", "POMS_TEST_HOST_TRANSPORT": "1",
-                                           "POMS_BOUNDARY_ON_CS": boundary_on_cs})
+                                           "POMS_BOUNDARY_ON_CS": boundary_on_cs, "POMS_TEST_HOST_SHM": shm})
+
+
+@pytest.mark.gpu
+def test_eight_rank_fullsize_slabs_host_transport_gpu():
+    """The 8-GPU run's split of the headline grid (515^3 over 8 ranks: 65/64-plane
+    slabs) on one GPU: the production schedule and the shared-memory sums against
+    the single-GPU result at 1e-13 with identical iteration counts."""
+    import torch
+    assert torch.cuda.device_count() >= 1, "GPU test selected but no GPU visible"
+    _launch("gpu_fullsize_slabs", world=8, timeout=900)
 
 
 @pytest.mark.gpu

@@ -360,6 +360,31 @@ def test_native_pcg_matches_python_loop(gpu, monkeypatch, ndim, N, p, scale, x0,
     assert out["1"][1]["res_norm"] == out["0"][1]["res_norm"]
 
 
+@pytest.mark.parametrize("cap", ["0", "16"])
+@pytest.mark.parametrize("ndim,N,p,scale", [(3, 20, 3, 1.0), (2, 64, 3, 1.0), (3, 16, 2, 1e-5)])
+def test_native_pcg_device_reduction_fallback(gpu, monkeypatch, cap, ndim, N, p, scale):
+    """The single-rank native loop's device-reduction fall-back (advisor, round 3):
+    POMS_HOST_PARTIALS=0 reduces every host-read norm on the device; a cap of 16
+    blocks takes the too-many-blocks branch for launches wider than that.  Both must
+    equal the Python device loop bitwise, like the host-partials default."""
+    from poms_amd import solvers
+    from poms_amd.stencil import KronOperator, StencilVectorSpace
+    M, K = assemble_1d(uniform_knots(p, N), p)
+    n = N + p
+    V = StencilVectorSpace([n] * ndim, [p] * ndim)
+    A = KronOperator.laplace(V, [M] * ndim, [K] * ndim)
+    b = V.zeros().from_numpy(scale * np.random.default_rng(N).standard_normal((n,) * ndim))
+    out = {}
+    for native in ("0", "1"):
+        monkeypatch.setenv("POMS_NATIVE_PCG", native)
+        monkeypatch.setenv("POMS_HOST_PARTIALS", cap)
+        x, info = solvers.pcg(A, solvers.damped_jacobi, b, tol=1e-6, maxiter=10)
+        out[native] = (x.to_local_numpy(), info)
+    np.testing.assert_array_equal(out["1"][0], out["0"][0])
+    for k in ("niter", "success", "res_norm"):
+        assert out["1"][1][k] == out["0"][1][k], k
+
+
 def test_op_timing_counts_native_launches(gpu):
     """poms_op_timing records every operator launch, including the native loop's."""
     from poms_amd import solvers

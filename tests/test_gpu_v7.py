@@ -1,0 +1,111 @@
+"""v7 (csrc/kron_v7.hip, variant 11): the flat-lane p = 3 apply.
+
+Its arithmetic is v5's in the same order (axis 1 pair sums, axis 2 pair sums on
+the Toeplitz tiles and per-column rows on the boundary tiles, the axis-0 scatter),
+so on the same operator and input it must equal v5 BITWISE; against the oracle
+the usual 1e-13.  The plane widths cover every tile plan: wide tiles only
+(224 = 2 x 112), one wide tile plus the remainder in a whole wide tile (211),
+narrow last columns of 16, 32, 48 and 80 (227, 131, 40, 515-wide via n0 thin
+slabs), and rows that do not divide the tile height.  Axis 0 is the first n0 rows
+of the 1D factors (its middle rows Toeplitz, its first / last p not).
+"""
+import numpy as np
+import pytest
+
+from oracle import poms_oracle as orc
+from poms_amd.splines import assemble_1d, uniform_knots
+
+pytestmark = pytest.mark.gpu
+
+TOL = 1e-13
+
+
+def rel(a, b):
+    return float(np.linalg.norm((a - b).ravel()) / max(np.linalg.norm(b.ravel()), 1e-300))
+
+
+def _truncate(F, n0, p):
+    G = np.array(F[:n0], copy=True)
+    for i in range(n0):
+        for k in range(2 * p + 1):
+            if not 0 <= i + k - p < n0:
+                G[i, k] = 0.0
+    return G
+
+
+def _op(n0, N1, N2, align=True):
+    from poms_amd.stencil import KronOperator, StencilVectorSpace
+    p = 3
+    M1, K1 = assemble_1d(uniform_knots(p, N1), p)
+    M2, K2 = assemble_1d(uniform_knots(p, N2), p)
+    Mb, Kb = (M1, K1) if N1 >= N2 else (M2, K2)
+    M0, K0 = _truncate(Mb, n0, p), _truncate(Kb, n0, p)
+    Ms, Ks = [M0, M1, M2], [K0, K1, K2]
+    npts = (n0, N1 + p, N2 + p)
+    V = StencilVectorSpace(npts, [p] * 3, align=align)
+    return V, KronOperator.laplace(V, Ms, Ks), Ms, Ks, npts
+
+
+@pytest.mark.parametrize("n0,N1,N2", [
+    (20, 221, 221),    # 224 x 224: two wide tiles, no narrow column
+    (17, 208, 208),    # 211: the remainder (99) takes a whole wide tile
+    (12, 224, 224),    # 227: two wide tiles + a 16-column narrow tile
+    (13, 128, 128),    # 131: one wide tile + a 32-column narrow tile
+    (30, 37, 37),      # 40: no wide tile, one 48-column narrow tile
+    (9, 300, 512),     # 303 x 515: four wide tiles + an 80-column narrow tile (the headline width)
+    (25, 77, 150),     # distinct axis-1 / axis-2 rows (the two-constant-set build)
+])
+def test_v7_apply_matches_v5_bitwise_and_oracle(gpu, n0, N1, N2):
+    V, A, Ms, Ks, npts = _op(n0, N1, N2)
+    A.set_variant(11)
+    assert A.kernel_variant("apply") == 11
+    assert A.kernel_variant("jacobi") == 10   # v7 builds the apply only
+    rng = np.random.default_rng(n0 * 7 + N2)
+    x = rng.uniform(-1, 1, npts)
+    xv = V.zeros().from_numpy(x)
+    y7 = A.dot(xv).to_local_numpy()
+    y_ref = orc.kron_sum_apply(x, Ms, Ks)
+    assert rel(y7, y_ref) <= TOL
+    A.set_variant(10)
+    y5 = A.dot(xv).to_local_numpy()
+    assert np.array_equal(y7, y5), f"v7 != v5 at {int((y7 != y5).sum())} points"
+    # ghosts and dead pitch columns stay zero
+    A.set_variant(11)
+    yv = A.dot(xv)
+    full = float(yv._store.abs().sum())     # the whole buffer: ghosts, dead pitch columns
+    inner = float(V.interior(yv._data).abs().sum())
+    assert full == inner
+
+
+def test_v7_unaligned_layout_falls_back(gpu):
+    V, A, Ms, Ks, npts = _op(10, 40, 40, align=False)
+    A.set_variant(11)
+    rng = np.random.default_rng(3)
+    x = rng.uniform(-1, 1, npts)
+    y = A.dot(V.zeros().from_numpy(x)).to_local_numpy()
+    assert rel(y, orc.kron_sum_apply(x, Ms, Ks)) <= TOL
+
+
+def test_v7_headline_grid_matches_v5(gpu):
+    """515^3 (the bench grid, 5 tile columns: 4 x 112 + 80): v7 == v5 bitwise on a
+    random input, with several axis-0 chunk lengths (chunk boundaries move)."""
+    import torch
+    from poms_amd.stencil import KronOperator, StencilVectorSpace
+    p, N = 3, 512
+    M, K = assemble_1d(uniform_knots(p, N), p)
+    n = N + p
+    V = StencilVectorSpace([n] * 3, [p] * 3, align=True)
+    A = KronOperator.laplace(V, [M] * 3, [K] * 3)
+    x, y5, y7 = V.zeros(), V.zeros(), V.zeros()
+    g = torch.Generator(device="cuda").manual_seed(5)
+    V.interior(x._data).uniform_(-1, 1, generator=g)
+    A.set_variant(10)
+    A.dot(x, out=y5)
+    A.set_variant(11)
+    for ch in (0, 37, 200):
+        A.set_chunk(ch)
+        y7._data.fill_(float("nan"))
+        A.dot(x, out=y7)
+        V.interior(y7._data)   # noqa: B018
+        assert bool(torch.equal(V.interior(y7._data), V.interior(y5._data))), f"chunk {ch}"
+    A.set_chunk(0)
