@@ -26,7 +26,7 @@ int kron_v5_launch(int pmax, int epi, const KronPtrs& p, const KronGeom& g, cons
 void kron_v5_tile(int pmax, bool aligned, int* H, int* TO);
 int kron_v5_rows(int pmax, int epi);
 int kron_v7_launch(int pmax, int epi, const KronPtrs& p, const KronGeom& g, const ToepConst& tc, double omega,
-                   hipStream_t st);
+                   hipStream_t st, int diag);
 int kron_v7_tiles(int pmax, int n1, int n2);
 int kron_tile_rows();
 int kron_tile_cols();
@@ -527,7 +527,7 @@ int poms_op_set_variant(poms_op* op, int variant) {
     // two sweeps from zero without sums / x1 scaling, timing only; 113: the Jacobi
     // sweep streaming the x rows no other tile reads)
     const bool known = variant == 0 || variant == 4 || (variant >= 7 && variant <= 11) ||
-                       (variant >= 90 && variant <= 113);
+                       (variant >= 90 && variant <= 113) || variant == 121 || variant == 122;
     if (!op || !known) { set_error("poms_op_set_variant: bad argument (0, 4, 7, 8, 9, 10, 11; 90-113 diagnostic)"); return 1; }
     if (variant > 0 && !op->v2_ok) { set_error("poms_op_set_variant: variant needs pads == pmax"); return 1; }
     op->variant = variant;
@@ -777,6 +777,9 @@ static int op_run(poms_op* o, int epi, double omega, const double* x, double* y,
     if (v == 11 && !v7_ok(o, x, y)) v = 10;
     const int v5_diag = (v >= 101 && v <= 113) ? v - 100 : 0;   // v5 diagnostic / tuning builds
     if (v5_diag) v = 10;
+    const int v7_diag = (v == 121 || v == 122) ? v - 120 : 0;   // v7 memory-only / arithmetic-only
+    if (v7_diag) v = v7_ok(o, x, y) && epi == EPI_APPLY ? 11 : -1;
+    if (v < 0) { set_error("v7 diagnostic build: aligned p = 3 apply only"); return 1; }
     int v5_h = 0, v5_to = 0;
     if (v == 10) kron_v5_tile(o->pmax, v5_aligned(o, x), &v5_h, &v5_to);
     KronGeom g;
@@ -814,7 +817,7 @@ static int op_run(poms_op* o, int epi, double omega, const double* x, double* y,
         POMS_HIP_CHECK(hipEventRecord(tlh->e0, as_stream(stream)));
     }
     const int rc = v == 11
-        ? kron_v7_launch(o->pmax, epi, p, g, o->tc, omega, as_stream(stream))
+        ? kron_v7_launch(o->pmax, epi, p, g, o->tc, omega, as_stream(stream), v7_diag)
         : v == 10
         ? kron_v5_launch(o->pmax, epi, p, g, o->tc, v5_h, omega, as_stream(stream), v5_diag)
         : v == 0
