@@ -37,7 +37,7 @@ sys.path.insert(0, str(ROOT))
 
 METRIC = "V-cycle DOF/s + Kron-SpMV GB/s vs HBM roofline, 3D Poisson p=3"
 HBM_PEAK_GBPS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md)
-KERNEL_NAMES = {10: "kron_v5_kernel", 9: "kron_v3_kernel(flat)", 7: "kron_v4_kernel", 4: "kron_v3_kernel"}
+KERNEL_NAMES = {11: "kron_v7_kernel", 10: "kron_v5_kernel", 9: "kron_v3_kernel(flat)", 7: "kron_v4_kernel", 4: "kron_v3_kernel"}
 
 
 def parse():
@@ -49,7 +49,8 @@ def parse():
     ap.add_argument("--p", type=int, default=3)
     ap.add_argument("--cells", type=int, default=None, help="cells per axis (default 512 in 3D, 1024 in 2D)")
     ap.add_argument("--flush-mall", type=int, default=None,
-                    help="MiB written between the isolated mat-vec launches (default 512 in 2D, 0 in 3D)")
+                    help="MiB written between the isolated mat-vec launches (default 512 in 2D and for 3D grids "
+                         "of <= 256 cells per axis, whose vectors fit the 256 MB MALL; 0 for the 512^3 headline)")
     ap.add_argument("--coarse", type=int, default=8)
     ap.add_argument("--chunk", type=int, default=0)
     ap.add_argument("--kron-reps", type=int, default=50, help="timed isolated applies")
@@ -73,8 +74,8 @@ def parse():
         a.warmup = 1 if a.ndim == 3 else 5
     if a.cells is None:
         a.cells = 512 if a.ndim == 3 else 1024
-    if a.flush_mall is None:
-        a.flush_mall = 512 if a.ndim == 2 else 0
+    if a.flush_mall is None:   # configs whose working set fits the MALL are flushed
+        a.flush_mall = 512 if (a.ndim == 2 or a.cells <= 256) else 0
     if a.ndim == 2 and a.cpu_cells == 160:
         a.cpu_cells = a.cells         # the 2D bench size runs on the host in seconds
     if a.ndim == 2 and a.cpu_cells_1core == 64:

@@ -141,9 +141,14 @@ int poms_op_set_tile_cols(poms_op* op, int cols);
  *       (3D FORM_SUM, arrays < 2 GiB, not at odd p with ghost corners; other
  *       operators, and two-sweeps-from-zero at p = 3 with distinct axis-1 /
  *       axis-2 Toeplitz rows, run variant 9);
+ *  11 = v7: flat lane mapping (lane -> row, column pair of an R x 112 tile),
+ *       axis-2 windows read from LDS instead of lane shifts, one barrier per
+ *       plane (p = 3 apply on the line-aligned layout with uniform-knot factors;
+ *       elsewhere it runs v5 -- poms_op_last_variant tells which ran);
  *  90-113 = diagnostic / tuning builds (memory-only, compute-only, cache policies;
- *  110-112: two sweeps from zero without sums / x1 scaling, timing only).
- * Variants 4-10 need storage pads == pmax on every used axis.                  */
+ *  110-112: two sweeps from zero without sums / x1 scaling, timing only);
+ *  121 / 122 = v7 memory only / arithmetic only (timing only).
+ * Variants 4-11 need storage pads == pmax on every used axis.                  */
 int poms_op_set_variant(poms_op* op, int variant);
 /* Declare that the ghost edges / corners of axes 1 and 2 may hold non-zero data:
  * the vector is a block of a decomposition of axes 1 and 2 (spl Cart,
@@ -155,6 +160,10 @@ int poms_op_get_variant(poms_op* op, int* variant);
  * fall-backs: 0 apply, 1 residual, 2 Jacobi sweep, 3 two sweeps from zero,
  * 4 apply + x.y.                                                              */
 int poms_op_kernel_variant(poms_op* op, int epilogue, int* variant);
+/* The kernel variant the operator's last launch actually ran, after the per-call
+ * fall-backs (layout alignment, Toeplitz ranges) that poms_op_kernel_variant cannot
+ * see; -1 before the first launch.                                               */
+int poms_op_last_variant(poms_op* op, int* variant);
 /* One operator launch on planes [z_begin, z_end) and its reductions, in one
  * call: epilogue as in poms_op_kernel_variant (0 apply y = A x; 1 residual
  * y = b - A x; 2 Jacobi sweep y = x + omega (b - A x)/diag; 3 sweeps 1-2 from

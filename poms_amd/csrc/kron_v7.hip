@@ -32,7 +32,8 @@
 // Preconditions (host, v7_ok in poms_abi.hip): 3D FORM_SUM, P == 3, storage pads ==
 // P, line-aligned layout (row pitch a multiple of 16 doubles, interior column 0 on a
 // 128-B line), array < 2 GiB, every non-Toeplitz row / column of the axis-1 / axis-2
-// factors among the first or last P, and no data in the corner ghosts (as v5 at odd P).
+// factors among the first or last 2P (open uniform knots: rows 0 .. 2p-1 touch a
+// non-uniform basis function), and no data in the corner ghosts (as v5 at odd P).
 #include "common.hpp"
 
 #include <algorithm>
@@ -58,6 +59,13 @@ constexpr int v7_rmax(int P, int C) { return 1024 / v7_xp(P, C); }
 // x-tile DMAs per plane at the largest R the lanes allow (R * XP <= 1024)
 constexpr int v7_ndma(int P, int C) { return ((v7_rmax(P, C) + 2 * P) * v7_xp(P, C) + 63) / 64; }
 constexpr int v7_max(int a, int b) { return a > b ? a : b; }
+// Entry of boundary-table row / column i of an n-long factor: the first and last NE
+// rows have their own entries (B-spline factors on open knots: rows 0 .. 2p-1 and
+// n-2p .. n-1 touch a non-uniform basis function), every other row the Toeplitz one
+// (entry 2 NE).  Host precondition (v7_ok): the Toeplitz range covers [NE, n - NE).
+__device__ __forceinline__ int v7_bidx(int i, int n, int NE) {
+    return i < NE ? i : (i >= n - NE ? NE + i - (n - NE) : 2 * NE);
+}
 
 template <int AUX = 0>
 __device__ __forceinline__ void v7_dma16(__amdgpu_buffer_rsrc_t r, double* lds_dst, int voff, unsigned soff) {
@@ -90,7 +98,8 @@ struct V7Lds {
     static constexpr int XS = 0;
     static constexpr int UVQ = 2048;               // one quantity (u or v) of one slot: 1024 pairs
     static constexpr int UV = XS + D * SLOT;       // 2 slots x (u, v)
-    static constexpr int NBT = (2 * P + 1) * W * 2;   // boundary rows 0..P-1, n-P..n-1, the Toeplitz row
+    static constexpr int NE = 2 * P;               // edge rows of a factor kept in the boundary tables
+    static constexpr int NBT = (2 * NE + 1) * W * 2;  // rows 0..NE-1, n-NE..n-1, the Toeplitz row
     static constexpr int BT1 = UV + 4 * UVQ;
     static constexpr int BT2 = BT1 + NBT;
     static constexpr int RED = BT2 + NBT;
@@ -221,10 +230,9 @@ __device__ __forceinline__ void v7_body(double* __restrict__ lds, const double* 
     };
     auto diag_xy = [&](int e, double& X, double& Y) {
         const int col = ocol + e;
-        const int b1 = orow < P ? orow : (orow >= g.n1 - P ? P + orow - (g.n1 - P) : 2 * P);   // (row of an active lane)
-        const int b2 = col < P ? col : (col >= g.n2 - P ? P + col - (g.n2 - P) : 2 * P);
-        const d2 f1 = *(const d2*)(lds + L::BT1 + 2 * (W * (act2 ? b1 : 2 * P) + P));
-        const d2 f2 = *(const d2*)(lds + L::BT2 + 2 * (W * (act2 ? b2 : 2 * P) + P));
+        const int b1 = v7_bidx(orow, g.n1, L::NE), b2 = v7_bidx(col, g.n2, L::NE);
+        const d2 f1 = *(const d2*)(lds + L::BT1 + 2 * (W * (act2 ? b1 : 2 * L::NE) + P));
+        const d2 f2 = *(const d2*)(lds + L::BT2 + 2 * (W * (act2 ? b2 : 2 * L::NE) + P));
         X = f1[0] * f2[0];
         Y = fma(f1[1], f2[0], f1[0] * f2[1]);
     };
@@ -299,8 +307,7 @@ __device__ __forceinline__ void v7_body(double* __restrict__ lds, const double* 
                         }
                     } else {
                         const int row = r0 + ru;
-                        const int bi = row < P ? row : (row >= g.n1 - P ? P + row - (g.n1 - P) : 2 * P);
-                        const double* bt = lds + L::BT1 + 2 * W * (act1 ? bi : 2 * P);
+                        const double* bt = lds + L::BT1 + 2 * W * (act1 ? v7_bidx(row, g.n1, L::NE) : 2 * L::NE);
                         u[0] = u[1] = v[0] = v[1] = 0.0;
 #pragma unroll
                         for (int k = 0; k < W; ++k) {
@@ -390,8 +397,7 @@ __device__ __forceinline__ void v7_body(double* __restrict__ lds, const double* 
 #pragma unroll
                         for (int e = 0; e < 2; ++e) {
                             const int col = ocol + e;
-                            const int bi = col < P ? col : (col >= g.n2 - P ? P + col - (g.n2 - P) : 2 * P);
-                            const double* bt = lds + L::BT2 + 2 * W * (act2 ? bi : 2 * P);
+                            const double* bt = lds + L::BT2 + 2 * W * (act2 ? v7_bidx(col, g.n2, L::NE) : 2 * L::NE);
                             double c = 0.0, d = 0.0;
 #pragma unroll
                             for (int k = 0; k < W; ++k) {
@@ -507,15 +513,17 @@ kron_v7_kernel(const double* __restrict__ x, double* __restrict__ y, const doubl
 
     // boundary coefficient tables (a, b interleaved) of both axes; entry 2P = the
     // Toeplitz row (lanes on interior rows / columns of a boundary tile read it)
-    for (int e = threadIdx.x; e < (2 * P + 1) * W; e += V7_NW * 64) {
+    constexpr int NE = L::NE;
+    for (int e = threadIdx.x; e < (2 * NE + 1) * W; e += V7_NW * 64) {
         const int i = e / W, k = e - i * W;
-        const int r1 = i < P ? i : g.n1 - 2 * P + i;
-        const int r2 = i < P ? i : g.n2 - 2 * P + i;
+        const int r1 = i < NE ? i : g.n1 - 2 * NE + i;
+        const int r2 = i < NE ? i : g.n2 - 2 * NE + i;
         const int ct = k < P ? P - k : k - P;
-        lds[L::BT1 + 2 * e] = i == 2 * P ? tc.t1a[ct] : a1[(int64_t)r1 * W + k];
-        lds[L::BT1 + 2 * e + 1] = i == 2 * P ? tc.t1b[ct] : b1[(int64_t)r1 * W + k];
-        lds[L::BT2 + 2 * e] = i == 2 * P ? (SAME12 ? tc.t1a[ct] : tc.t2a[ct]) : a2[(int64_t)r2 * W + k];
-        lds[L::BT2 + 2 * e + 1] = i == 2 * P ? (SAME12 ? tc.t1b[ct] : tc.t2b[ct]) : b2[(int64_t)r2 * W + k];
+        const bool toe = i == 2 * NE;
+        lds[L::BT1 + 2 * e] = toe ? tc.t1a[ct] : a1[(int64_t)r1 * W + k];
+        lds[L::BT1 + 2 * e + 1] = toe ? tc.t1b[ct] : b1[(int64_t)r1 * W + k];
+        lds[L::BT2 + 2 * e] = toe ? (SAME12 ? tc.t1a[ct] : tc.t2a[ct]) : a2[(int64_t)r2 * W + k];
+        lds[L::BT2 + 2 * e + 1] = toe ? (SAME12 ? tc.t1b[ct] : tc.t2b[ct]) : b2[(int64_t)r2 * W + k];
     }
 
     double nrm = 0.0, dotp = 0.0;

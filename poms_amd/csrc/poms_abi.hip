@@ -87,6 +87,7 @@ struct poms_op {
     double *dg2a = nullptr, *dg2b = nullptr;  // contiguous axis-2 band diagonals
     double* rdiag0 = nullptr;                  // 1/diag(A) per global plane (Toeplitz interior of axes 1, 2)
     int variant = 0;
+    int last_variant = -1;    // the kernel variant the last operator launch ran (after per-call fall-backs)
     bool v2_ok = false;       // storage pads == pmax on every used axis (the Toeplitz kernels' precondition)
     bool ghost_corners = false;   // ghost edges / corners of axes 1 and 2 may be non-zero (a Cart block)
     ToepConst tc{};
@@ -543,6 +544,12 @@ int poms_op_kernel_variant(poms_op* op, int epilogue, int* variant) {
     return 0;
 }
 
+int poms_op_last_variant(poms_op* op, int* variant) {
+    if (!op || !variant) { set_error("poms_op_last_variant: null argument"); return 1; }
+    *variant = op->last_variant;
+    return 0;
+}
+
 int poms_op_get_variant(poms_op* op, int* variant) {
     if (!op || !variant) { set_error("poms_op_get_variant: null argument"); return 1; }
     *variant = op->variant;
@@ -607,13 +614,14 @@ static bool v5_aligned(const poms_op* o, const double* x) {
 
 // v7 (variant 11, kron_v7.hip) runs 3D FORM_SUM operators at p = 3 on the
 // line-aligned layout whose non-Toeplitz axis-1 / axis-2 rows are among the first
-// and last p (uniform knots; the boundary tables hold 2p rows), with v5's corner rule.
+// and last 2p (uniform open knots; the boundary tables hold 4p rows), with v5's
+// corner rule.
 static bool v7_ok(const poms_op* o, const double* x, const double* y) {
     if (!(v5_ok(o) && o->pmax == 3 && v5_aligned(o, x) && v5_aligned(o, y) && !o->ghost_corners)) return false;
     const int P = o->pmax;
     const int64_t n1 = o->L.n[1], n2 = o->L.n[2];
-    return n1 >= 4 * P && n2 >= 4 * P && o->tc.lo1 <= P && o->tc.hi1 >= n1 - P && o->tc.lo2 <= P &&
-           o->tc.hi2 >= n2 - P;
+    return n1 >= 4 * P && n2 >= 4 * P && o->tc.lo1 <= 2 * P && o->tc.hi1 >= n1 - 2 * P && o->tc.lo2 <= 2 * P &&
+           o->tc.hi2 >= n2 - 2 * P;
 }
 
 static int op_geom(poms_op* o, int64_t zb, int64_t ze, KronGeom& g, int v = -1, int v5_to = 0,
@@ -780,6 +788,7 @@ static int op_run(poms_op* o, int epi, double omega, const double* x, double* y,
     const int v7_diag = (v == 121 || v == 122) ? v - 120 : 0;   // v7 memory-only / arithmetic-only
     if (v7_diag) v = v7_ok(o, x, y) && epi == EPI_APPLY ? 11 : -1;
     if (v < 0) { set_error("v7 diagnostic build: aligned p = 3 apply only"); return 1; }
+    o->last_variant = v7_diag ? 120 + v7_diag : v5_diag ? 100 + v5_diag : v;
     int v5_h = 0, v5_to = 0;
     if (v == 10) kron_v5_tile(o->pmax, v5_aligned(o, x), &v5_h, &v5_to);
     KronGeom g;

@@ -675,6 +675,13 @@ class KronOperator:
         _lib.call("poms_op_timing_read", self._h, self.EPILOGUES[epilogue], C.byref(ms), C.byref(n), C.byref(d))
         return ms.value * 1e-3, n.value, d.value
 
+    @property
+    def last_variant(self) -> int:
+        """Variant the last launch ran (after the per-call fall-backs; -1 before any)."""
+        v = C.c_int()
+        _lib.call("poms_op_last_variant", self._h, C.byref(v))
+        return v.value
+
     def kernel_variant(self, epilogue: str) -> int:
         """Variant one launch of ``epilogue`` runs after auto-selection / fall-backs."""
         v = C.c_int()

@@ -64,6 +64,7 @@ def test_v7_apply_matches_v5_bitwise_and_oracle(gpu, n0, N1, N2):
     x = rng.uniform(-1, 1, npts)
     xv = V.zeros().from_numpy(x)
     y7 = A.dot(xv).to_local_numpy()
+    assert A.last_variant == 11, "v7 did not run (a per-call fall-back took over)"
     y_ref = orc.kron_sum_apply(x, Ms, Ks)
     assert rel(y7, y_ref) <= TOL
     A.set_variant(10)
@@ -84,6 +85,7 @@ def test_v7_unaligned_layout_falls_back(gpu):
     rng = np.random.default_rng(3)
     x = rng.uniform(-1, 1, npts)
     y = A.dot(V.zeros().from_numpy(x)).to_local_numpy()
+    assert A.last_variant == 10
     assert rel(y, orc.kron_sum_apply(x, Ms, Ks)) <= TOL
 
 
@@ -107,6 +109,6 @@ def test_v7_headline_grid_matches_v5(gpu):
         A.set_chunk(ch)
         y7._data.fill_(float("nan"))
         A.dot(x, out=y7)
-        V.interior(y7._data)   # noqa: B018
+        assert A.last_variant == 11
         assert bool(torch.equal(V.interior(y7._data), V.interior(y5._data))), f"chunk {ch}"
     A.set_chunk(0)
