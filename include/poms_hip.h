@@ -147,7 +147,8 @@ int poms_op_set_tile_cols(poms_op* op, int cols);
  *       elsewhere it runs v5 -- poms_op_last_variant tells which ran);
  *  90-113 = diagnostic / tuning builds (memory-only, compute-only, cache policies;
  *  110-112: two sweeps from zero without sums / x1 scaling, timing only);
- *  121 / 122 = v7 memory only / arithmetic only (timing only).
+ *  121-124 = v7 memory only / arithmetic only (timing only) / non-temporal x
+ *  DMAs / y stores with the default cache policy.
  * Variants 4-11 need storage pads == pmax on every used axis.                  */
 int poms_op_set_variant(poms_op* op, int variant);
 /* Declare that the ghost edges / corners of axes 1 and 2 may hold non-zero data:

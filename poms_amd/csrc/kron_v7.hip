@@ -97,7 +97,9 @@ struct V7Lds {
     static constexpr int SLOT = 128 * NDMA;        // one x plane tile
     static constexpr int XS = 0;
     static constexpr int UVQ = 2048;               // one quantity (u or v) of one slot: 1024 pairs
-    static constexpr int UV = XS + D * SLOT;       // 2 slots x (u, v)
+    static constexpr int UV = XS + D * SLOT;       // 2 slots x (u, v); the two-barrier schedule
+                                                   // uses one and puts its b ring in the other
+    static constexpr int BRING = UV + 2 * UVQ;
     static constexpr int NE = 2 * P;               // edge rows of a factor kept in the boundary tables
     static constexpr int NBT = (2 * NE + 1) * W * 2;  // rows 0..NE-1, n-NE..n-1, the Toeplitz row
     static constexpr int BT1 = UV + 4 * UVQ;
@@ -118,10 +120,15 @@ __device__ __forceinline__ void v7_body(double* __restrict__ lds, const double* 
                                         double& nrm, double& dotp) {
     typedef V7Lds<P, D, CN> L;
     constexpr int W = L::W;
-    // rotating axis-0 accumulators: 8 (>= 2P+1) so that the unrolled march folds every
-    // ring index (x slot t % 4, b register pair t % 2, x history t % 4) at compile time
-    constexpr int NS = 8;
-    static_assert(NS >= W && NS % D == 0 && D == 4, "ring indices fold over the 8-plane unroll");
+    // Residual and Jacobi (b read) run the two-barrier schedule (TB2, below); apply and
+    // apply-dot the pipelined one.  Rotating axis-0 accumulators: the pipelined march
+    // keeps 8 (>= 2P+1) so that its ring indices (x slot t % 4, x history t % 4) fold
+    // at compile time over the 8-plane unroll; TB2 keeps 2P+1 (its slots are indexed at
+    // run time, its x history is a shift register).
+    constexpr bool HASB = EPI == EPI_RESID || EPI == EPI_JACOBI;
+    constexpr bool TB2 = HASB;
+    constexpr int NS = TB2 ? W : 8;
+    static_assert(NS >= W && (TB2 || (NS % D == 0 && D == 4)), "ring indices fold over the 8-plane unroll");
     constexpr int HP = v7_hp(P);
     constexpr int XP = v7_xp(P, C);     // x pairs per x-tile row
     constexpr int OP = C / 2;           // output pairs per row
@@ -129,11 +136,10 @@ __device__ __forceinline__ void v7_body(double* __restrict__ lds, const double* 
     constexpr int PFX = D - 1;          // x prefetch distance (planes)
     constexpr int YAUX = (CP & 4) ? 2 : 0;
     constexpr int BAUX = (CP & 2) ? 2 : 0;
-    constexpr bool HASB = EPI == EPI_RESID || EPI == EPI_JACOBI;
+    constexpr int XAUX = (CP & 1) ? 2 : 0;   // x DMAs non-temporal (tuning; the halo rows are re-read)
     constexpr bool JAC = EPI == EPI_JACOBI;
     constexpr bool APD = EPI == EPI_APPLYDOT;
-    constexpr bool HIST = JAC || APD;   // x at the output point (a 4-plane register history)
-    constexpr int NB = HASB ? 1 : 0;    // b loads per iteration (into VGPRs, two planes ahead)
+    constexpr bool HIST = JAC || APD;   // x at the output point (a register history)
     // diagnostic builds (apply, timing only): CP bit 256 = memory only (the DMAs and
     // stores, no LDS reads or arithmetic), bit 512 = arithmetic only (no DMA, no bytes
     // stored)
@@ -201,23 +207,14 @@ __device__ __forceinline__ void v7_body(double* __restrict__ lds, const double* 
         const bool ok = t < nplanes && sp >= 0 && sp < nsp;
         const uint32_t so = ok ? (uint32_t)sp * plane8 : 0u;
         double* dst = lds + L::XS + slot * L::SLOT + wv * 128;
-        v7_dma16<0>(rx, dst, ok ? (int)xvo[0] : (int)0x80000000u, so);
-        if (dma2) v7_dma16<0>(rx, dst + V7_NW * 128, ok ? (int)xvo[1] : (int)0x80000000u, so);
+        v7_dma16<XAUX>(rx, dst, ok ? (int)xvo[0] : (int)0x80000000u, so);
+        if (dma2) v7_dma16<XAUX>(rx, dst + V7_NW * 128, ok ? (int)xvo[1] : (int)0x80000000u, so);
     };
     // output point of stage 2 (row-and-column part; the plane goes in separately)
     const bool okrc0 = act2 && orow < g.n1 && ocol < g.n2;
     const bool okrc1 = act2 && orow < g.n1 && ocol + 1 < g.n2;
     const int vrc = ((orow + g.pd1) * s1 + g.pd2 + ocol) * 8;
     auto zo_of = [&](int t2) { return max(z0 - 2 * P + t2, z0); };
-    // b of the output plane of stage-2 plane t2 (16-B load into VGPRs; lanes with no
-    // output point load nothing)
-    auto load_b = [&](int t2) -> d2 {
-        const uint32_t so = (uint32_t)(zo_of(t2) + g.pd0) * plane8;
-        const u32x4 v = __builtin_amdgcn_raw_buffer_load_b128(rb, okrc0 ? vrc : (int)0x80000000u, (int)so, BAUX);
-        const u32x2 lo = {v.x, v.y}, hi = {v.z, v.w};
-        return d2{__builtin_bit_cast(double, lo), __builtin_bit_cast(double, hi)};
-    };
-
     // ---- Jacobi: omega / diag(A) at this lane's two output points on the planes of the
     // axis-0 Toeplitz interior (plane-invariant there: computed once), and the
     // plane-invariant factors X = d1a d2a, Y = d1b d2a + d1a d2b of diag(A) = d0a X + d0b Y
@@ -253,235 +250,302 @@ __device__ __forceinline__ void v7_body(double* __restrict__ lds, const double* 
     double acc[NS][2];
 #pragma unroll
     for (int s = 0; s < NS; ++s) { acc[s][0] = 0.0; acc[s][1] = 0.0; }
-    d2 hx[HIST ? 4 : 1];                // x at the output point, planes t-3 .. t (ring t % 4)
-#pragma unroll
-    for (int i = 0; i < (HIST ? 4 : 1); ++i) hx[i] = d2{0.0, 0.0};
-    d2 bq[2] = {d2{0.0, 0.0}, d2{0.0, 0.0}};   // b of stage-2 planes t2 (ring t2 % 2)
 
-    __syncthreads();   // boundary tables visible; no DMA in flight yet
+    // ---- stage 1 of one x plane tile (xsl): u = F1a x, v = F1b x of the lane's pair into
+    // the u/v buffer at uvb; returns the x tap at the lane's output point
+    auto stage1 = [&](const double* xsl, double* uvb) -> d2 {
+        const double* xs = xsl + 2 * fu;
+        d2 xv[W];
 #pragma unroll
-    for (int i = 0; i < PFX; ++i) dma_x(i, i);
-    if constexpr (HASB) {   // stage-2 planes 0 and 1 (used at iterations 1 and 2)
-        bq[0] = load_b(0);
-        bq[1] = load_b(1);
-    }
-
-    for (int tb = 0; tb <= nplanes; tb += NS) {
+        for (int k = 0; k < W; ++k) xv[k] = *(const d2*)(xs + 2 * k * XP);
+        double u[2], v[2];
+        if (fast1) {
 #pragma unroll
-        for (int q = 0; q < NS; ++q) {
-            const int t = tb + q;
-            if (t <= nplanes) {
-                // ---- x(t) landed: own DMAs by vmcnt (the loads issued after x(t)'s are the
-                // DMAs of planes t+1 .. t+PFX-1 and one b load per iteration since), everyone's
-                // by the barrier.  Stores never count (one may be acknowledged before an older
-                // load returns): vmcnt <= N implies the load has landed.
-                if (dma2) v7_wait_vm<(PFX - 1) * (2 + NB) + NB>();
-                else v7_wait_vm<(PFX - 1) * (1 + NB) + NB>();
-                v7_barrier();
-                dma_x(t + PFX, (q + PFX) % D);
-
-                const double* xsl = lds + L::XS + (q % D) * L::SLOT;   // x(t)
-                // ---- stage 1: u = F1a x, v = F1b x of plane t
-                d2 xnew = {0.0, 0.0};
-                if (t < nplanes && !MEMONLY) {
-                    const double* xs = xsl + 2 * fu;
-                    d2 xv[W];
+            for (int e = 0; e < 2; ++e) {
+                double pr[P + 1];
+                pr[0] = xv[P][e];
 #pragma unroll
-                    for (int k = 0; k < W; ++k) xv[k] = *(const d2*)(xs + 2 * k * XP);
-                    double u[2], v[2];
-                    if (fast1) {
+                for (int k = 1; k <= P; ++k) pr[k] = xv[P - k][e] + xv[P + k][e];
+                double su = tc.t1a[0] * pr[0], sv = tc.t1b[0] * pr[0];
 #pragma unroll
-                        for (int e = 0; e < 2; ++e) {
-                            double pr[P + 1];
-                            pr[0] = xv[P][e];
-#pragma unroll
-                            for (int k = 1; k <= P; ++k) pr[k] = xv[P - k][e] + xv[P + k][e];
-                            double su = tc.t1a[0] * pr[0], sv = tc.t1b[0] * pr[0];
-#pragma unroll
-                            for (int k = 1; k <= P; ++k) {
-                                su = fma(tc.t1a[k], pr[k], su);
-                                sv = fma(tc.t1b[k], pr[k], sv);
-                            }
-                            u[e] = su;
-                            v[e] = sv;
-                        }
-                    } else {
-                        const int row = r0 + ru;
-                        const double* bt = lds + L::BT1 + 2 * W * (act1 ? v7_bidx(row, g.n1, L::NE) : 2 * L::NE);
-                        u[0] = u[1] = v[0] = v[1] = 0.0;
-#pragma unroll
-                        for (int k = 0; k < W; ++k) {
-                            const d2 f = *(const d2*)(bt + 2 * k);
-#pragma unroll
-                            for (int e = 0; e < 2; ++e) {
-                                u[e] = fma(f[0], xv[k][e], u[e]);
-                                v[e] = fma(f[1], xv[k][e], v[e]);
-                            }
-                        }
-                    }
-                    if (act1) {
-                        double* uv = lds + L::UV + (q & 1) * 2 * L::UVQ + 2 * fl;
-                        *(d2*)uv = d2{u[0], u[1]};
-                        *(d2*)(uv + L::UVQ) = d2{v[0], v[1]};
-                    }
-                    if constexpr (HIST) xnew = xv[P];   // x at this lane's output point, plane t
+                for (int k = 1; k <= P; ++k) {
+                    su = fma(tc.t1a[k], pr[k], su);
+                    sv = fma(tc.t1b[k], pr[k], sv);
                 }
-                // the x history: x(t - 4) is the output plane of stage-2 plane t - 1
-                d2 xin = {0.0, 0.0};
-                if constexpr (HIST) {
-                    xin = hx[q % 4];
-                    hx[q % 4] = xnew;
+                u[e] = su;
+                v[e] = sv;
+            }
+        } else {
+            const int row = r0 + ru;
+            const double* bt = lds + L::BT1 + 2 * W * (act1 ? v7_bidx(row, g.n1, L::NE) : 2 * L::NE);
+            u[0] = u[1] = v[0] = v[1] = 0.0;
+#pragma unroll
+            for (int k = 0; k < W; ++k) {
+                const d2 f = *(const d2*)(bt + 2 * k);
+#pragma unroll
+                for (int e = 0; e < 2; ++e) {
+                    u[e] = fma(f[0], xv[k][e], u[e]);
+                    v[e] = fma(f[1], xv[k][e], v[e]);
                 }
+            }
+        }
+        if (act1) {
+            double* uv = uvb + 2 * fl;
+            *(d2*)uv = d2{u[0], u[1]};
+            *(d2*)(uv + L::UVQ) = d2{v[0], v[1]};
+        }
+        return xv[P];
+    };
+    // ---- stage 2, axis 2: c = F2a u, d = F2a v + F2b u at the lane's output pair from
+    // the u/v buffer at uvb
+    auto axis2 = [&](const double* uvb, double cc[2], double dd[2]) {
+        const double* us = uvb + 2 * fo;
+        // window values 2HP - P .. 2HP + 1 + P (columns ocol - P .. ocol + 1 + P): whole
+        // pairs inside, single doubles at odd-P edges
+        constexpr int W0 = 2 * HP - P, W1 = 2 * HP + 1 + P;
+        double wu[2 * NWIN], wvv[2 * NWIN];
+#pragma unroll
+        for (int m = 0; m < NWIN; ++m) {
+            if (2 * m + 1 < W0 || 2 * m > W1) continue;
+            if (2 * m < W0) {          // only the pair's second value is used
+                wu[2 * m + 1] = us[2 * m + 1];
+                wvv[2 * m + 1] = us[L::UVQ + 2 * m + 1];
+            } else if (2 * m + 1 > W1) {   // only the first
+                wu[2 * m] = us[2 * m];
+                wvv[2 * m] = us[L::UVQ + 2 * m];
+            } else {
+                const d2 a = *(const d2*)(us + 2 * m);
+                const d2 b = *(const d2*)(us + L::UVQ + 2 * m);
+                wu[2 * m] = a[0];
+                wu[2 * m + 1] = a[1];
+                wvv[2 * m] = b[0];
+                wvv[2 * m + 1] = b[1];
+            }
+        }
+        if (fast2) {
+#pragma unroll
+            for (int e = 0; e < 2; ++e) {
+                const int cen = 2 * HP + e;
+                double pu[P + 1], pv[P + 1];
+                pu[0] = wu[cen];
+                pv[0] = wvv[cen];
+#pragma unroll
+                for (int k = 1; k <= P; ++k) {
+                    pu[k] = wu[cen - k] + wu[cen + k];
+                    pv[k] = wvv[cen - k] + wvv[cen + k];
+                }
+                double c = T2A(0) * pu[0];
+                double d = fma(T2A(0), pv[0], T2B(0) * pu[0]);
+#pragma unroll
+                for (int k = 1; k <= P; ++k) {
+                    c = fma(T2A(k), pu[k], c);
+                    d = fma(T2A(k), pv[k], fma(T2B(k), pu[k], d));
+                }
+                cc[e] = c;
+                dd[e] = d;
+            }
+        } else {
+#pragma unroll
+            for (int e = 0; e < 2; ++e) {
+                const int col = ocol + e;
+                const double* bt = lds + L::BT2 + 2 * W * (act2 ? v7_bidx(col, g.n2, L::NE) : 2 * L::NE);
+                double c = 0.0, d = 0.0;
+#pragma unroll
+                for (int k = 0; k < W; ++k) {
+                    const d2 f = *(const d2*)(bt + 2 * k);
+                    const int wi = 2 * HP - P + e + k;
+                    c = fma(f[0], wu[wi], c);
+                    d = fma(f[0], wvv[wi], fma(f[1], wu[wi], d));
+                }
+                cc[e] = c;
+                dd[e] = d;
+            }
+        }
+    };
+    // ---- axis 0: scatter march plane tt's (c, d) into the rotating slots (qq = tt mod
+    // NS, folded by the unroll); returns the finished output plane's A x (plane tt - P)
+    auto axis0 = [&](int qq, int tt, const double cc[2], const double dd[2], double vo[2]) {
+        const int jrow = (g.g0 + z0 - P + tt + P) * W;
+#pragma unroll
+        for (int s = 0; s < W; ++s) {
+            const int slot = (qq - P + s + NS) % NS;
+            const double ka = a0t[jrow + s];
+            const double kb = b0t[jrow + s];
+#pragma unroll
+            for (int e = 0; e < 2; ++e) acc[slot][e] = fma(ka, cc[e], fma(kb, dd[e], acc[slot][e]));
+        }
+        const int done = (qq - P + NS) % NS;
+        vo[0] = acc[done][0];
+        vo[1] = acc[done][1];
+        acc[done][0] = 0.0;
+        acc[done][1] = 0.0;
+    };
+    // ---- epilogue of output plane zo (march plane tt = zo - z0 + 2P): x_in the x at the
+    // output point, bv b there
+    auto epilogue = [&](int tt, const double vo[2], const d2 xin, const d2 bv) {
+        const bool en = tt >= 2 * P;
+        const int zo = zo_of(tt);
+        const bool ok0 = en && okrc0, ok1 = en && okrc1;
+        double outv[2];
+        if constexpr (EPI == EPI_APPLY) {
+            outv[0] = vo[0];
+            outv[1] = vo[1];
+        } else if constexpr (APD) {
+            outv[0] = vo[0];
+            outv[1] = vo[1];
+            dotp = ok0 ? fma(xin[0], vo[0], dotp) : dotp;
+            dotp = ok1 ? fma(xin[1], vo[1], dotp) : dotp;
+        } else if constexpr (EPI == EPI_RESID) {
+            outv[0] = bv[0] - vo[0];
+            outv[1] = bv[1] - vo[1];
+        } else {
+            double rc[2];
+            const int gz = g.g0 + zo;
+            if (rfast) {
+                rc[0] = rc[1] = omega * rdiag0[gz];   // one multiply per plane
+            } else if (gz >= tc.lo0 && gz < tc.hi0) {
+                rc[0] = rci[0];
+                rc[1] = rci[1];
+            } else {   // the P planes next to each global end of axis 0
+                const int i0 = (gz + P) * W + P;
+                const double d0a = a0t[i0], d0b = b0t[i0];
+#pragma unroll
+                for (int e = 0; e < 2; ++e) {
+                    double X, Y;
+                    diag_xy(e, X, Y);
+                    rc[e] = omega * rcp_nr(fma(d0a, X, d0b * Y));
+                }
+            }
+#pragma unroll
+            for (int e = 0; e < 2; ++e) {
+                const double dr = (bv[e] - vo[e]) * rc[e];   // rc = omega / diag
+                outv[e] = xin[e] + dr;
+                const bool oke = e ? ok1 : ok0;
+                nrm = oke ? fma(dr, dr, nrm) : nrm;
+                if constexpr (JDOT) dotp = oke ? fma(outv[e], bv[e], dotp) : dotp;
+            }
+        }
+        // one 16-B store per lane; a second column past n2 (ghost or dead pitch column) is
+        // written 0.  The plane offset goes into voffset (gfx950 wait state before a VALU
+        // overwrites a >8-B store's data VGPRs; see v5).
+        const double o1 = ok1 ? outv[1] : 0.0;
+        const int voy = vrc + (zo + g.pd0) * (int)plane8;
+        v7_store16<YAUX>(ry, (ok0 || ok1) && (!ARITHONLY || outv[0] == 12345.678) ? voy : (int)0x80000000u,
+                         outv[0], o1);
+    };
 
-                // (no instruction moves across: stage 1's and stage 2's transients must not
-                // be live at once -- 128 VGPRs at 4 waves per SIMD)
-                __builtin_amdgcn_sched_barrier(0);
-                // ---- stage 2: plane t-1 -- axis 2 from the u/v windows, axis 0, epilogue
-                if constexpr (MEMONLY) {
-                    if (t >= 1) {
-                        const int zo = zo_of(t - 1);
-                        const bool any = t - 1 >= 2 * P && okrc0;
-                        v7_store16<YAUX>(ry, any ? vrc + (zo + g.pd0) * (int)plane8 : (int)0x80000000u, 1.0,
-                                         okrc1 ? 1.0 : 0.0);
-                    }
-                } else if (t >= 1) {
-                    const int q2 = (q + NS - 1) % NS;   // (t - 1) mod NS (folded by the unroll)
-                    const int t2 = t - 1;
-                    const double* us = lds + L::UV + (q2 & 1) * 2 * L::UVQ + 2 * fo;
-                    // window values 2HP - P .. 2HP + 1 + P (columns ocol - P .. ocol + 1 + P):
-                    // whole pairs inside, single doubles at odd-P edges
-                    constexpr int W0 = 2 * HP - P, W1 = 2 * HP + 1 + P;
-                    double wu[2 * NWIN], wvv[2 * NWIN];
+    if constexpr (TB2) {
+        // ---- residual / Jacobi: two barriers per plane, b DMA'd into LDS one plane ahead.
+        // Iteration t: [wait, barrier] DMA b(t+1), DMA x(t+PFX); stage 1 of x(t) into the
+        // single u/v slot; [barrier] stage 2 of plane t, output plane t - P.
+        // b: flat output pairs r*OP + j, DMA i moves pairs 64 i .. 64 i + 63 (one per
+        // wave, waves < ndb)
+        const int nbp = R * OP;
+        const bool hasb = wv * 64 < nbp;
+        uint32_t bvo;
+        {
+            const int f = wv * 64 + lane;
+            const int r = f / OP, j = f - r * OP;
+            const bool ok = f < nbp && r0 + r < g.n1 && c0 + 2 * j < g.n2;
+            bvo = ok ? (uint32_t)(((r0 + r + g.pd1) * s1 + g.pd2 + c0 + 2 * j) * 8) : 0x80000000u;
+        }
+        const int fb = act2 ? ru * OP + jo : 0;   // this lane's output pair in a b slot
+        auto dma_b = [&](int tt) {   // b of the output plane of march plane tt (dummy past the march)
+            if (!hasb) return;
+            const uint32_t so = (uint32_t)(zo_of(tt) + g.pd0) * plane8;
+            double* dst = lds + L::BRING + (tt & 1) * L::UVQ + wv * 128;
+            v7_dma16<BAUX>(rb, dst, tt < nplanes ? (int)bvo : (int)0x80000000u, so);
+        };
+        d2 hs[HIST ? P : 1];   // x at the output point, planes t-P .. t-1 (shift register)
 #pragma unroll
-                    for (int m = 0; m < NWIN; ++m) {
-                        if (2 * m + 1 < W0 || 2 * m > W1) continue;
-                        if (2 * m < W0) {          // only the pair's second value is used
-                            wu[2 * m + 1] = us[2 * m + 1];
-                            wvv[2 * m + 1] = us[L::UVQ + 2 * m + 1];
-                        } else if (2 * m + 1 > W1) {   // only the first
-                            wu[2 * m] = us[2 * m];
-                            wvv[2 * m] = us[L::UVQ + 2 * m];
-                        } else {
-                            const d2 a = *(const d2*)(us + 2 * m);
-                            const d2 b = *(const d2*)(us + L::UVQ + 2 * m);
-                            wu[2 * m] = a[0];
-                            wu[2 * m + 1] = a[1];
-                            wvv[2 * m] = b[0];
-                            wvv[2 * m + 1] = b[1];
-                        }
-                    }
-                    double cc[2], dd[2];
-                    if (fast2) {
+        for (int i = 0; i < (HIST ? P : 1); ++i) hs[i] = d2{0.0, 0.0};
+        __syncthreads();   // boundary tables visible; no DMA in flight yet
+        dma_b(0);
 #pragma unroll
-                        for (int e = 0; e < 2; ++e) {
-                            const int cen = 2 * HP + e;
-                            double pu[P + 1], pv[P + 1];
-                            pu[0] = wu[cen];
-                            pv[0] = wvv[cen];
+        for (int i = 0; i < PFX; ++i) dma_x(i, i);
+        for (int tb = 0; tb < nplanes; tb += NS) {
 #pragma unroll
-                            for (int k = 1; k <= P; ++k) {
-                                pu[k] = wu[cen - k] + wu[cen + k];
-                                pv[k] = wvv[cen - k] + wvv[cen + k];
-                            }
-                            double c = T2A(0) * pu[0];
-                            double d = fma(T2A(0), pv[0], T2B(0) * pu[0]);
-#pragma unroll
-                            for (int k = 1; k <= P; ++k) {
-                                c = fma(T2A(k), pu[k], c);
-                                d = fma(T2A(k), pv[k], fma(T2B(k), pu[k], d));
-                            }
-                            cc[e] = c;
-                            dd[e] = d;
-                        }
+            for (int q = 0; q < NS; ++q) {
+                const int t = tb + q;
+                if (t < nplanes) {
+                    // x(t) and b(t) landed.  Loads after b(t) (issued first in iteration t-1):
+                    // that iteration's x DMAs; after x(t): PFX-1 iterations of b + x DMAs
+                    if (hasb) {
+                        if (dma2) v7_wait_vm<2>();
+                        else v7_wait_vm<1>();
                     } else {
-#pragma unroll
-                        for (int e = 0; e < 2; ++e) {
-                            const int col = ocol + e;
-                            const double* bt = lds + L::BT2 + 2 * W * (act2 ? v7_bidx(col, g.n2, L::NE) : 2 * L::NE);
-                            double c = 0.0, d = 0.0;
-#pragma unroll
-                            for (int k = 0; k < W; ++k) {
-                                const d2 f = *(const d2*)(bt + 2 * k);
-                                const int wi = 2 * HP - P + e + k;
-                                c = fma(f[0], wu[wi], c);
-                                d = fma(f[0], wvv[wi], fma(f[1], wu[wi], d));
-                            }
-                            cc[e] = c;
-                            dd[e] = d;
-                        }
+                        if (dma2) v7_wait_vm<2 * (PFX - 1)>();
+                        else v7_wait_vm<PFX - 1>();
                     }
+                    v7_barrier();
+                    dma_b(t + 1);
+                    dma_x(t + PFX, (t + PFX) % D);
+                    const d2 xc = stage1(lds + L::XS + (t % D) * L::SLOT, lds + L::UV);
+                    d2 xin = {0.0, 0.0};
+                    if constexpr (HIST) {
+                        xin = hs[0];
+#pragma unroll
+                        for (int i = 0; i + 1 < P; ++i) hs[i] = hs[i + 1];
+                        hs[P - 1] = xc;
+                    }
+                    v7_barrier();
+                    double cc[2], dd[2], vo[2];
+                    axis2(lds + L::UV, cc, dd);
+                    axis0(q, t, cc, dd, vo);
+                    const d2 bv = *(const d2*)(lds + L::BRING + (t & 1) * L::UVQ + 2 * fb);
+                    epilogue(t, vo, xin, bv);
+                }
+            }
+        }
+    } else {
+        d2 hx[HIST ? 4 : 1];                // x at the output point, planes t-3 .. t (ring t % 4)
+#pragma unroll
+        for (int i = 0; i < (HIST ? 4 : 1); ++i) hx[i] = d2{0.0, 0.0};
+        __syncthreads();   // boundary tables visible; no DMA in flight yet
+#pragma unroll
+        for (int i = 0; i < PFX; ++i) dma_x(i, i);
 
-                    // ---- axis 0: scatter into the rotating slots (scalar loads of the
-                    // axis-0 factor column of the global input plane)
-                    const int jrow = (g.g0 + z0 - P + t2 + P) * W;
+        for (int tb = 0; tb <= nplanes; tb += NS) {
 #pragma unroll
-                    for (int s = 0; s < W; ++s) {
-                        const int slot = (q2 - P + s + NS) % NS;
-                        const double ka = a0t[jrow + s];
-                        const double kb = b0t[jrow + s];
-#pragma unroll
-                        for (int e = 0; e < 2; ++e) acc[slot][e] = fma(ka, cc[e], fma(kb, dd[e], acc[slot][e]));
-                    }
-                    const int done = (q2 - P + NS) % NS;   // output plane t2 - P is complete
-                    double vo[2] = {acc[done][0], acc[done][1]};
-                    acc[done][0] = 0.0;
-                    acc[done][1] = 0.0;
-                    const bool en = t2 >= 2 * P;
-                    const int zo = zo_of(t2);
-                    const bool ok0 = en && okrc0, ok1 = en && okrc1;
+            for (int q = 0; q < NS; ++q) {
+                const int t = tb + q;
+                if (t <= nplanes) {
+                    // ---- x(t) landed: own DMAs by vmcnt (the loads issued after x(t)'s are
+                    // the DMAs of planes t+1 .. t+PFX-1), everyone's by the barrier.  Stores
+                    // never count (one may be acknowledged before an older load returns):
+                    // vmcnt <= N implies the load has landed.
+                    if (dma2) v7_wait_vm<2 * (PFX - 1)>();
+                    else v7_wait_vm<PFX - 1>();
+                    v7_barrier();
+                    dma_x(t + PFX, (q + PFX) % D);
 
-                    // ---- epilogue of the finished plane zo
-                    double outv[2];
-                    if constexpr (EPI == EPI_APPLY) {
-                        outv[0] = vo[0];
-                        outv[1] = vo[1];
-                    } else if constexpr (APD) {
-                        outv[0] = vo[0];
-                        outv[1] = vo[1];
-                        dotp = ok0 ? fma(xin[0], vo[0], dotp) : dotp;
-                        dotp = ok1 ? fma(xin[1], vo[1], dotp) : dotp;
-                    } else {
-                        const d2 bv = bq[q2 & 1];
-                        if constexpr (EPI == EPI_RESID) {
-                            outv[0] = bv[0] - vo[0];
-                            outv[1] = bv[1] - vo[1];
-                        } else {
-                            double rc[2];
-                            const int gz = g.g0 + zo;
-                            if (rfast) {
-                                rc[0] = rc[1] = omega * rdiag0[gz];   // one multiply per plane
-                            } else if (gz >= tc.lo0 && gz < tc.hi0) {
-                                rc[0] = rci[0];
-                                rc[1] = rci[1];
-                            } else {   // the P planes next to each global end of axis 0
-                                const int i0 = (gz + P) * W + P;
-                                const double d0a = a0t[i0], d0b = b0t[i0];
-#pragma unroll
-                                for (int e = 0; e < 2; ++e) {
-                                    double X, Y;
-                                    diag_xy(e, X, Y);
-                                    rc[e] = omega * rcp_nr(fma(d0a, X, d0b * Y));
-                                }
-                            }
-#pragma unroll
-                            for (int e = 0; e < 2; ++e) {
-                                const double dr = (bv[e] - vo[e]) * rc[e];   // rc = omega / diag
-                                outv[e] = xin[e] + dr;
-                                const bool oke = e ? ok1 : ok0;
-                                nrm = oke ? fma(dr, dr, nrm) : nrm;
-                                if constexpr (JDOT) dotp = oke ? fma(outv[e], bv[e], dotp) : dotp;
-                            }
-                        }
+                    // ---- stage 1: u, v of plane t
+                    d2 xnew = {0.0, 0.0};
+                    if (t < nplanes && !MEMONLY) xnew = stage1(lds + L::XS + (q % D) * L::SLOT, lds + L::UV + (q & 1) * 2 * L::UVQ);
+                    // the x history: x(t - 4) is the output plane of stage-2 plane t - 1
+                    d2 xin = {0.0, 0.0};
+                    if constexpr (HIST) {
+                        xin = hx[q % 4];
+                        hx[q % 4] = xnew;
                     }
-                    // one 16-B store per lane; a second column past n2 (ghost or dead pitch
-                    // column) is written 0.  The plane offset goes into voffset (gfx950 wait
-                    // state before a VALU overwrites a >8-B store's data VGPRs; see v5).
-                    const double o1 = ok1 ? outv[1] : 0.0;
-                    const int voy = vrc + (zo + g.pd0) * (int)plane8;
-                    v7_store16<YAUX>(ry, (ok0 || ok1) && (!ARITHONLY || outv[0] == 12345.678) ? voy : (int)0x80000000u,
-                                     outv[0], o1);
-                    // b of stage-2 plane t2 + 2 (used two iterations on) into the pair just read
-                    if constexpr (HASB) bq[q2 & 1] = load_b(t2 + 2);
+                    // (no instruction moves across: stage 1's and stage 2's transients must
+                    // not be live at once -- 128 VGPRs at 4 waves per SIMD)
+                    __builtin_amdgcn_sched_barrier(0);
+                    // ---- stage 2: plane t-1 -- axis 2 from the u/v windows, axis 0, epilogue
+                    if constexpr (MEMONLY) {
+                        if (t >= 1) {
+                            const int zo = zo_of(t - 1);
+                            const bool any = t - 1 >= 2 * P && okrc0;
+                            v7_store16<YAUX>(ry, any ? vrc + (zo + g.pd0) * (int)plane8 : (int)0x80000000u, 1.0,
+                                             okrc1 ? 1.0 : 0.0);
+                        }
+                    } else if (t >= 1) {
+                        const int q2 = (q + NS - 1) % NS;   // (t - 1) mod NS (folded by the unroll)
+                        double cc[2], dd[2], vo[2];
+                        axis2(lds + L::UV + (q2 & 1) * 2 * L::UVQ, cc, dd);
+                        axis0(q2, t - 1, cc, dd, vo);
+                        epilogue(t - 1, vo, xin, d2{0.0, 0.0});
+                    }
                 }
             }
         }
@@ -672,10 +736,15 @@ int kron_v7_launch(int pmax, int epi, const KronPtrs& p, const KronGeom& g, cons
     if (vg.ntiles <= 0) return 0;
     bool same = true;   // axis-1 / axis-2 Toeplitz rows, bitwise
     for (int k = 0; k <= 3; ++k) same = same && tc.t1a[k] == tc.t2a[k] && tc.t1b[k] == tc.t2b[k];
-    if (diag) {   // diagnostic builds (apply): 1 memory only, 2 arithmetic only
-        if (epi != EPI_APPLY || diag > 2) { set_error("v7 diag: apply, modes 1-2"); return 1; }
-        return diag == 1 ? v7_launch_e<EPI_APPLY, 4 | 256, false>(same, p, g, vg, tc, omega, st)
-                         : v7_launch_e<EPI_APPLY, 4 | 512, false>(same, p, g, vg, tc, omega, st);
+    if (diag) {   // diagnostic / tuning builds (apply): 1 memory only, 2 arithmetic only,
+                  // 3 non-temporal x DMAs, 4 y stores with the default policy
+        if (epi != EPI_APPLY || diag > 4) { set_error("v7 diag: apply, modes 1-4"); return 1; }
+        switch (diag) {
+            case 1: return v7_launch_e<EPI_APPLY, 4 | 256, false>(same, p, g, vg, tc, omega, st);
+            case 2: return v7_launch_e<EPI_APPLY, 4 | 512, false>(same, p, g, vg, tc, omega, st);
+            case 3: return v7_launch_e<EPI_APPLY, 4 | 1, false>(same, p, g, vg, tc, omega, st);
+            default: return v7_launch_e<EPI_APPLY, 0, false>(same, p, g, vg, tc, omega, st);
+        }
     }
     switch (epi) {
         case EPI_APPLY: return v7_launch_e<EPI_APPLY, 4, false>(same, p, g, vg, tc, omega, st);

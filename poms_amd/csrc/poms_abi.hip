@@ -528,7 +528,7 @@ int poms_op_set_variant(poms_op* op, int variant) {
     // two sweeps from zero without sums / x1 scaling, timing only; 113: the Jacobi
     // sweep streaming the x rows no other tile reads)
     const bool known = variant == 0 || variant == 4 || (variant >= 7 && variant <= 11) ||
-                       (variant >= 90 && variant <= 113) || variant == 121 || variant == 122;
+                       (variant >= 90 && variant <= 113) || (variant >= 121 && variant <= 124);
     if (!op || !known) { set_error("poms_op_set_variant: bad argument (0, 4, 7, 8, 9, 10, 11; 90-113 diagnostic)"); return 1; }
     if (variant > 0 && !op->v2_ok) { set_error("poms_op_set_variant: variant needs pads == pmax"); return 1; }
     op->variant = variant;
@@ -748,8 +748,9 @@ static int resolve_variant(const poms_op* o, int epi) {
         else
             v = ((epi == EPI_APPLY || epi == EPI_RESID) && o->pmax <= 3) ? 7 : 9;
     }
-    // v7: the apply at p = 3 (alignment and the Toeplitz ranges are checked per call)
-    if (v == 11 && !(epi == EPI_APPLY && v5_ok(o) && o->pmax == 3 && !o->ghost_corners)) v = 10;
+    // v7: apply, residual, Jacobi sweep and apply + dot at p = 3 (alignment and the
+    // Toeplitz ranges are checked per call; the sweeps from zero stay on v5)
+    if (v == 11 && !(epi != EPI_JACOBI0 && v5_ok(o) && o->pmax == 3 && !o->ghost_corners)) v = 10;
     if (v == 10 && (!v5_ok(o) || (epi == EPI_JACOBI0 && o->pmax == 3 && !same_toeplitz12(o)))) v = 9;
     return v;
 }
@@ -785,7 +786,7 @@ static int op_run(poms_op* o, int epi, double omega, const double* x, double* y,
     if (v == 11 && !v7_ok(o, x, y)) v = 10;
     const int v5_diag = (v >= 101 && v <= 113) ? v - 100 : 0;   // v5 diagnostic / tuning builds
     if (v5_diag) v = 10;
-    const int v7_diag = (v == 121 || v == 122) ? v - 120 : 0;   // v7 memory-only / arithmetic-only
+    const int v7_diag = (v >= 121 && v <= 124) ? v - 120 : 0;   // v7 diagnostic / tuning builds
     if (v7_diag) v = v7_ok(o, x, y) && epi == EPI_APPLY ? 11 : -1;
     if (v < 0) { set_error("v7 diagnostic build: aligned p = 3 apply only"); return 1; }
     o->last_variant = v7_diag ? 120 + v7_diag : v5_diag ? 100 + v5_diag : v;

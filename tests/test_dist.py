@@ -84,7 +84,7 @@ def test_two_rank_distributed_operator_and_vcycle_gpu(device_reductions):
 
 @pytest.mark.gpu
 @pytest.mark.parametrize("world,boundary_on_cs,shm", [(2, "1", "0"), (3, "1", "0"), (2, "0", "0"),
-                                                      (2, "1", "1"), (3, "1", "1")])
+                                                      (2, "1", "1"), (3, "1", "1"), (1, "1", "0")])
 def test_two_rank_native_schedule_with_peers_gpu(world, boundary_on_cs, shm):
     """The production slab schedule (poms_op_run_dist: exchange, interior planes,
     both boundaries in one launch -- on the communication stream behind the
@@ -93,7 +93,10 @@ def test_two_rank_native_schedule_with_peers_gpu(world, boundary_on_cs, shm):
     communicator) with REAL neighbours: the communicator's host transport moves the
     planes and sums over gloo, since RCCL cannot pair ranks that share one GPU.
     shm=1: the host-read sums go through the node-local shared-memory block
-    (shm_allsum, poms_comm_wait's shared-memory branch) as in a one-node RCCL run."""
+    (shm_allsum, poms_comm_wait's shared-memory branch) as in a one-node RCCL run.
+    world=1: a communicator with no neighbour takes the single-launch path (no
+    exchange is queued, so no split launch may run unordered on the communication
+    stream; advisor, round 3)."""
     import torch
     assert torch.cuda.device_count() >= 1, "GPU test selected but no GPU visible"
     _launch("gpu", world=world, extra_env={"POMS_TEST_DEVRED": "1", "POMS_TEST_HOST_TRANSPORT": "1",

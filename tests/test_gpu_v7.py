@@ -58,8 +58,7 @@ def _op(n0, N1, N2, align=True):
 def test_v7_apply_matches_v5_bitwise_and_oracle(gpu, n0, N1, N2):
     V, A, Ms, Ks, npts = _op(n0, N1, N2)
     A.set_variant(11)
-    assert A.kernel_variant("apply") == 11
-    assert A.kernel_variant("jacobi") == 10   # v7 builds the apply only
+    assert A.kernel_variant("apply") == 11 and A.kernel_variant("jacobi") == 11
     rng = np.random.default_rng(n0 * 7 + N2)
     x = rng.uniform(-1, 1, npts)
     xv = V.zeros().from_numpy(x)
@@ -77,6 +76,43 @@ def test_v7_apply_matches_v5_bitwise_and_oracle(gpu, n0, N1, N2):
     rest = yv._store.clone()   # the whole buffer (ghosts, dead pitch columns) minus the interior
     V.interior(V.view(rest)).zero_()
     assert not bool(rest.any())
+
+
+@pytest.mark.parametrize("n0,N1,N2", [(20, 221, 221), (12, 224, 224), (9, 300, 512), (25, 77, 150), (30, 37, 37)])
+def test_v7_epilogues_match_v5(gpu, n0, N1, N2):
+    """Residual, Jacobi sweep (norm, and the fused x_out . b), apply + x.Ax: the
+    vectors equal v5's bitwise; the per-block sums are added in another block order,
+    so the scalars agree to 1e-13 (and with the oracle)."""
+    V, A, Ms, Ks, npts = _op(n0, N1, N2)
+    rng = np.random.default_rng(n0 + 3 * N2)
+    x, b = rng.uniform(-1, 1, npts), rng.uniform(-1, 1, npts)
+    xv, bv = V.zeros().from_numpy(x), V.zeros().from_numpy(b)
+    w = 2.0 / 3.0
+    out = {}
+    for v in (11, 10):
+        A.set_variant(v)
+        r = V.zeros()
+        A.residual(bv, xv, out=r)
+        assert A.last_variant == v
+        xo1, xo2 = V.zeros(), V.zeros()
+        n1 = A.jacobi_sweep(bv, xv, xo1, w, want_norm=True)
+        assert A.last_variant == v
+        n2, d2 = A.jacobi_sweep(bv, xv, xo2, w, want_norm=True, want_dot=True)
+        y = V.zeros()
+        xy = A.dot_inner(xv, y)
+        assert A.last_variant == v
+        out[v] = (r.to_local_numpy(), xo1.to_local_numpy(), xo2.to_local_numpy(), y.to_local_numpy(), n1, n2, d2, xy)
+    for i in range(4):
+        assert np.array_equal(out[11][i], out[10][i]), f"vector {i}: {int((out[11][i] != out[10][i]).sum())} points differ"
+    for i in range(4, 8):
+        assert abs(out[11][i] - out[10][i]) <= 1e-13 * abs(out[10][i]), (i, out[11][i], out[10][i])
+    y_ref = orc.kron_sum_apply(x, Ms, Ks)
+    D = orc.kron_sum_diag(Ms, Ks).reshape(npts)
+    dr = w * (b - y_ref) / D
+    assert rel(out[11][0], b - y_ref) <= TOL and rel(out[11][1], x + dr) <= TOL
+    assert abs(out[11][4] - float(np.vdot(dr, dr))) <= 1e-12 * float(np.vdot(dr, dr))
+    assert abs(out[11][6] - float(np.vdot(x + dr, b))) <= 1e-12 * abs(float(np.vdot(x + dr, b)))
+    assert abs(out[11][7] - float(np.vdot(x, y_ref))) <= 1e-12 * abs(float(np.vdot(x, y_ref)))
 
 
 def test_v7_unaligned_layout_falls_back(gpu):
