@@ -120,13 +120,14 @@ __device__ __forceinline__ void v7_body(double* __restrict__ lds, const double* 
                                         double& nrm, double& dotp) {
     typedef V7Lds<P, D, CN> L;
     constexpr int W = L::W;
-    // Residual and Jacobi (b read) run the two-barrier schedule (TB2, below); apply and
-    // apply-dot the pipelined one.  Rotating axis-0 accumulators: the pipelined march
+    // Residual, Jacobi and apply-dot (b read, or an x history) run the two-barrier
+    // schedule (TB2, below); the apply the pipelined one.  Rotating axis-0 accumulators: the pipelined march
     // keeps 8 (>= 2P+1) so that its ring indices (x slot t % 4, x history t % 4) fold
     // at compile time over the 8-plane unroll; TB2 keeps 2P+1 (its slots are indexed at
     // run time, its x history is a shift register).
     constexpr bool HASB = EPI == EPI_RESID || EPI == EPI_JACOBI;
-    constexpr bool TB2 = HASB;
+    constexpr bool J0 = EPI == EPI_JACOBI0;   // sweeps 1 and 2 from x = 0 (the x ring holds b)
+    constexpr bool TB2 = HASB || J0 || EPI == EPI_APPLYDOT;   // (apply-dot: its x history)
     constexpr int NS = TB2 ? W : 8;
     static_assert(NS >= W && (TB2 || (NS % D == 0 && D == 4)), "ring indices fold over the 8-plane unroll");
     constexpr int HP = v7_hp(P);
@@ -139,7 +140,7 @@ __device__ __forceinline__ void v7_body(double* __restrict__ lds, const double* 
     constexpr int XAUX = (CP & 1) ? 2 : 0;   // x DMAs non-temporal (tuning; the halo rows are re-read)
     constexpr bool JAC = EPI == EPI_JACOBI;
     constexpr bool APD = EPI == EPI_APPLYDOT;
-    constexpr bool HIST = JAC || APD;   // x at the output point (a register history)
+    constexpr bool HIST = JAC || APD || J0;   // x (J0: x1) at the output point (a register history)
     // diagnostic builds (apply, timing only): CP bit 256 = memory only (the DMAs and
     // stores, no LDS reads or arithmetic), bit 512 = arithmetic only (no DMA, no bytes
     // stored)
@@ -168,8 +169,11 @@ __device__ __forceinline__ void v7_body(double* __restrict__ lds, const double* 
     const int orow = r0 + ru;           // output row (stage 2)
     const int ocol = c0 + 2 * jo;       // output column of element 0
 
-    // tile-uniform fast paths: every row / column the tile computes is Toeplitz
-    const bool fast1 = r0 >= tc.lo1 && min(r0 + R, g.n1) <= tc.hi1;
+    // fast paths: axis 1 per lane (its row inside the Toeplitz interior: the same choice
+    // per output row as v5, whose waves are rows, so the two agree bitwise), axis 2 per
+    // tile (every column of the tile Toeplitz: v5's per-workgroup choice, on the same
+    // 112-column tile boundaries)
+    const bool fast1 = orow >= tc.lo1 && orow < tc.hi1;
     const bool fast2 = c0 >= tc.lo2 && min(c0 + C, g.n2) <= tc.hi2;
 
     int z0, z1;
@@ -247,17 +251,64 @@ __device__ __forceinline__ void v7_body(double* __restrict__ lds, const double* 
         }
     }
 
+    // ---- two sweeps from zero: s = omega / diag(A) (x1 = s b, x2 = x1 + s (b - A x1)).
+    // s at (plane with axis-0 diagonal d0a, d0b; row; column), as v5's j0_scale; and
+    // sc[e] at this lane's columns on Toeplitz rows and planes, where s depends on the
+    // column only (the stage-1 columns of the lane are its output columns)
+    auto s_at = [&](double d0a, double d0b, int row, int col) {
+        row = min(max(row, 0), g.n1 - 1);
+        col = min(max(col, 0), g.n2 - 1);
+        const d2 f1 = *(const d2*)(lds + L::BT1 + 2 * (W * v7_bidx(row, g.n1, L::NE) + P));
+        const d2 f2 = *(const d2*)(lds + L::BT2 + 2 * (W * v7_bidx(col, g.n2, L::NE) + P));
+        const double dg = fma(d0a, f1[0] * f2[0], d0b * fma(f1[1], f2[0], f1[0] * f2[1]));
+        return dg != 0.0 ? omega * rcp_nr(dg) : 0.0;   // zero diagonal: a ghost plane (b = 0)
+    };
+    // J0: every x-tile row (the 2P halo rows too) has the Toeplitz axis-1 band: on such a
+    // tile and a Toeplitz plane x1 = sc(col) b, and the scaling commutes with the axis-1
+    // pass (applied to u, v after it, as v5 does on its row-Toeplitz tiles)
+    const bool jrf = J0 && r0 - P >= tc.lo1 && r0 + R + P <= tc.hi1;
+    double sc[2] = {0.0, 0.0};
+    auto j0_sc_after = [&](int tt) {   // (tile-uniform)
+        const int m = g.g0 + z0 - P + tt;   // global plane of x(tt)
+        return jrf && m >= tc.lo0 && m < tc.hi0;
+    };
+    // Otherwise (boundary tile rows, the P planes next to each global end of axis 0) the
+    // ring slot of x(tt) = b is scaled to x1 = s b in place, each wave the pairs it
+    // DMA'd, between the plane's barrier and one more (rare: a few % of the work)
+    auto j0_scale_slot = [&](double* slot, int tt) {
+        const int m = g.g0 + z0 - P + tt;
+        const bool tp = m >= tc.lo0 && m < tc.hi0;
+        const int i0 = (m + P) * W + P;   // (a0t is padded by P planes on each side)
+        const double d0a = tp ? tc.t0a[0] : a0t[i0], d0b = tp ? tc.t0b[0] : b0t[i0];
+        const int nxp2 = (R + 2 * P) * XP;
+#pragma unroll
+        for (int sdma = 0; sdma < 2; ++sdma) {
+            const int f = (wv + sdma * V7_NW) * 64 + lane;
+            if (f < nxp2) {
+                const int qq = f / XP, kk = f - qq * XP;
+                d2* pr = (d2*)(slot + 2 * f);
+                d2 vv = *pr;
+#pragma unroll
+                for (int e = 0; e < 2; ++e) vv[e] *= s_at(d0a, d0b, r0 - P + qq, c0 - 2 * HP + 2 * kk + e);
+                *pr = vv;
+            }
+        }
+    };
+
     double acc[NS][2];
 #pragma unroll
     for (int s = 0; s < NS; ++s) { acc[s][0] = 0.0; acc[s][1] = 0.0; }
 
     // ---- stage 1 of one x plane tile (xsl): u = F1a x, v = F1b x of the lane's pair into
     // the u/v buffer at uvb; returns the x tap at the lane's output point
-    auto stage1 = [&](const double* xsl, double* uvb) -> d2 {
+    auto stage1 = [&](const double* xsl, double* uvb, int tt) -> d2 {
         const double* xs = xsl + 2 * fu;
         d2 xv[W];
 #pragma unroll
         for (int k = 0; k < W; ++k) xv[k] = *(const d2*)(xs + 2 * k * XP);
+        // J0: scale u, v (and the centre) after the axis-1 pass; elsewhere the ring slot was
+        // scaled in place before this pass (j0_scale_slot)
+        const bool jsc = J0 && j0_sc_after(tt);
         double u[2], v[2];
         if (fast1) {
 #pragma unroll
@@ -286,6 +337,18 @@ __device__ __forceinline__ void v7_body(double* __restrict__ lds, const double* 
                 for (int e = 0; e < 2; ++e) {
                     u[e] = fma(f[0], xv[k][e], u[e]);
                     v[e] = fma(f[1], xv[k][e], v[e]);
+                }
+            }
+        }
+        if constexpr (J0) {
+            if (jsc) {
+                const d2 scl = *(const d2*)(lds + L::BRING + L::UVQ + 2 * fl);
+                double sc[2] = {scl[0], scl[1]};
+#pragma unroll
+                for (int e = 0; e < 2; ++e) {
+                    u[e] *= sc[e];
+                    v[e] *= sc[e];
+                    xv[P][e] *= sc[e];   // the centre tap the x1 history keeps
                 }
             }
         }
@@ -398,6 +461,35 @@ __device__ __forceinline__ void v7_body(double* __restrict__ lds, const double* 
         } else if constexpr (EPI == EPI_RESID) {
             outv[0] = bv[0] - vo[0];
             outv[1] = bv[1] - vo[1];
+        } else if constexpr (J0) {
+            // x1 = s b, x2 = x1 + s (b - A x1) = x1 + (x1 - s A x1); xin = x1 at the output point
+            const int m = g.g0 + zo;
+            const bool tp = m >= tc.lo0 && m < tc.hi0;
+            double so[2];
+            if (fast1 && tp) {
+                const d2 scl = *(const d2*)(lds + L::BRING + L::UVQ + 2 * fl);
+                so[0] = scl[0];
+                so[1] = scl[1];
+            } else {
+                const int i0 = (m + P) * W + P;
+                const double d0a = tp ? tc.t0a[0] : a0t[i0], d0b = tp ? tc.t0b[0] : b0t[i0];
+                so[0] = s_at(d0a, d0b, orow, ocol);
+                so[1] = s_at(d0a, d0b, orow, ocol + 1);
+            }
+            // the two running sums live in LDS (this lane's slot in the unused b ring): the 4
+            // VGPRs they would pin across the march are what the build lacks at 128
+            d2* jsum = (d2*)(lds + L::BRING + 2 * fl);
+            d2 js = *jsum;
+#pragma unroll
+            for (int e = 0; e < 2; ++e) {
+                const double x1 = xin[e];
+                const double dr = fma(-vo[e], so[e], x1);
+                outv[e] = x1 + dr;
+                const bool oke = e ? ok1 : ok0;
+                js[0] = oke ? fma(dr, dr, js[0]) : js[0];   // ||dr_2||^2
+                js[1] = oke ? fma(x1, x1, js[1]) : js[1];   // ||x1||^2 = ||dr_1||^2
+            }
+            *jsum = js;
         } else {
             double rc[2];
             const int gz = g.g0 + zo;
@@ -460,6 +552,12 @@ __device__ __forceinline__ void v7_body(double* __restrict__ lds, const double* 
 #pragma unroll
         for (int i = 0; i < (HIST ? P : 1); ++i) hs[i] = d2{0.0, 0.0};
         __syncthreads();   // boundary tables visible; no DMA in flight yet
+        if constexpr (J0) {
+#pragma unroll
+            for (int e = 0; e < 2; ++e) sc[e] = s_at(tc.t0a[0], tc.t0b[0], max(tc.lo1, 0), ocol + e);
+            *(d2*)(lds + L::BRING + 2 * fl) = d2{0.0, 0.0};   // the lane's running sums
+            *(d2*)(lds + L::BRING + L::UVQ + 2 * fl) = d2{sc[0], sc[1]};   // and its sc (re-read per plane)
+        }
         dma_b(0);
 #pragma unroll
         for (int i = 0; i < PFX; ++i) dma_x(i, i);
@@ -480,7 +578,13 @@ __device__ __forceinline__ void v7_body(double* __restrict__ lds, const double* 
                     v7_barrier();
                     dma_b(t + 1);
                     dma_x(t + PFX, (t + PFX) % D);
-                    const d2 xc = stage1(lds + L::XS + (t % D) * L::SLOT, lds + L::UV);
+                    if constexpr (J0) {
+                        if (!j0_sc_after(t)) {
+                            j0_scale_slot(lds + L::XS + (t % D) * L::SLOT, t);
+                            v7_barrier();
+                        }
+                    }
+                    const d2 xc = stage1(lds + L::XS + (t % D) * L::SLOT, lds + L::UV, t);
                     d2 xin = {0.0, 0.0};
                     if constexpr (HIST) {
                         xin = hs[0];
@@ -492,10 +596,16 @@ __device__ __forceinline__ void v7_body(double* __restrict__ lds, const double* 
                     double cc[2], dd[2], vo[2];
                     axis2(lds + L::UV, cc, dd);
                     axis0(q, t, cc, dd, vo);
-                    const d2 bv = *(const d2*)(lds + L::BRING + (t & 1) * L::UVQ + 2 * fb);
+                    d2 bv = {0.0, 0.0};
+                    if constexpr (HASB) bv = *(const d2*)(lds + L::BRING + (t & 1) * L::UVQ + 2 * fb);
                     epilogue(t, vo, xin, bv);
                 }
             }
+        }
+        if constexpr (J0) {
+            const d2 js = *(const d2*)(lds + L::BRING + 2 * fl);
+            nrm = js[0];
+            dotp = js[1];
         }
     } else {
         d2 hx[HIST ? 4 : 1];                // x at the output point, planes t-3 .. t (ring t % 4)
@@ -521,7 +631,7 @@ __device__ __forceinline__ void v7_body(double* __restrict__ lds, const double* 
 
                     // ---- stage 1: u, v of plane t
                     d2 xnew = {0.0, 0.0};
-                    if (t < nplanes && !MEMONLY) xnew = stage1(lds + L::XS + (q % D) * L::SLOT, lds + L::UV + (q & 1) * 2 * L::UVQ);
+                    if (t < nplanes && !MEMONLY) xnew = stage1(lds + L::XS + (q % D) * L::SLOT, lds + L::UV + (q & 1) * 2 * L::UVQ, t);
                     // the x history: x(t - 4) is the output plane of stage-2 plane t - 1
                     d2 xin = {0.0, 0.0};
                     if constexpr (HIST) {
@@ -605,7 +715,7 @@ kron_v7_kernel(const double* __restrict__ x, double* __restrict__ y, const doubl
     }
 
     // per-block partial sums (wave butterflies, then the waves in order)
-    if constexpr (EPI == EPI_JACOBI || EPI == EPI_APPLYDOT) {
+    if constexpr (EPI == EPI_JACOBI || EPI == EPI_APPLYDOT || EPI == EPI_JACOBI0) {
         const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
         double* red = lds + L::RED;
         if (partial != nullptr) {
@@ -753,6 +863,8 @@ int kron_v7_launch(int pmax, int epi, const KronPtrs& p, const KronGeom& g, cons
             return p.partial2 ? v7_launch_e<EPI_JACOBI, 6, true>(same, p, g, vg, tc, omega, st)
                               : v7_launch_e<EPI_JACOBI, 6, false>(same, p, g, vg, tc, omega, st);
         case EPI_APPLYDOT: return v7_launch_e<EPI_APPLYDOT, 4, false>(same, p, g, vg, tc, omega, st);
+        // (EPI_JACOBI0 compiles -- the body has it -- but spills a few VGPRs in the
+        // epilogue of the P planes next to each global end; not built until it fits)
     }
     set_error("v7: epilogue not built");
     return 1;

@@ -684,7 +684,7 @@ static int op_geom(poms_op* o, int64_t zb, int64_t ze, KronGeom& g, int v = -1, 
 
 // variants whose Jacobi epilogue also accumulates x_out . b (v3 and v4 kernels)
 static bool fused_dot_ok(const poms_op* o) {
-    return o->form == FORM_STENCIL || (o->variant >= 4 && o->variant <= 10);
+    return o->form == FORM_STENCIL || (o->variant >= 4 && o->variant <= 11);
 }
 
 // General-stencil launch (FORM_STENCIL): the epilogues of op_run plus EPI_DIAG.
@@ -748,8 +748,8 @@ static int resolve_variant(const poms_op* o, int epi) {
         else
             v = ((epi == EPI_APPLY || epi == EPI_RESID) && o->pmax <= 3) ? 7 : 9;
     }
-    // v7: apply, residual, Jacobi sweep and apply + dot at p = 3 (alignment and the
-    // Toeplitz ranges are checked per call; the sweeps from zero stay on v5)
+    // v7: apply, residual, Jacobi sweep, apply + dot at p = 3 (alignment and the Toeplitz
+    // ranges are checked per call); the sweeps from zero run v5
     if (v == 11 && !(epi != EPI_JACOBI0 && v5_ok(o) && o->pmax == 3 && !o->ghost_corners)) v = 10;
     if (v == 10 && (!v5_ok(o) || (epi == EPI_JACOBI0 && o->pmax == 3 && !same_toeplitz12(o)))) v = 9;
     return v;
@@ -762,15 +762,16 @@ static int op_run(poms_op* o, int epi, double omega, const double* x, double* y,
     if (epi != EPI_APPLY && !b) { set_error("null right-hand side"); return 1; }
     if (o->form == FORM_STENCIL)
         return stencil_run(o, epi, omega, x, y, b, zb, ze, want_norm, stream, want_dot, zb2, ze2);
-    if (epi == EPI_APPLYDOT && !(o->variant == 4 || o->variant == 8 || o->variant == 9 || o->variant == 10)) {
-        set_error("apply + x.y: kernel variants 4, 8, 9, 10 only");
+    if (epi == EPI_APPLYDOT && !(o->variant == 4 || o->variant == 8 || o->variant == 9 || o->variant == 10 ||
+                                 o->variant == 11)) {
+        set_error("apply + x.y: kernel variants 4, 8, 9, 10, 11 only");
         return 1;
     }
     if (want_dot && ((epi != EPI_JACOBI && epi != EPI_JACOBI0 && epi != EPI_APPLYDOT) || !fused_dot_ok(o))) {
-        set_error("fused x_out.b needs a Jacobi sweep on kernel variants 4-10");
+        set_error("fused x_out.b needs a Jacobi sweep on kernel variants 4-11");
         return 1;
     }
-    if (epi == EPI_JACOBI0 && !(o->variant == 8 || o->variant == 9 || o->variant == 10 ||
+    if (epi == EPI_JACOBI0 && !(o->variant == 8 || o->variant == 9 || o->variant == 10 || o->variant == 11 ||
                                 (o->variant >= 110 && o->variant <= 112))) {
         set_error("two sweeps from zero: kernel variant 8, 9 or 10 only");
         return 1;
@@ -783,7 +784,8 @@ static int op_run(poms_op* o, int epi, double omega, const double* x, double* y,
     // Variant 10 (v5) runs apply / residual / Jacobi / apply+dot of 3D p <= 3
     // operators, and is what 8 picks for them; 9 otherwise.
     int v = resolve_variant(o, epi);
-    if (v == 11 && !v7_ok(o, x, y)) v = 10;
+    if (v == 11 && !v7_ok(o, x, y))   // (as resolve_variant would pick for variant 10)
+        v = (v5_ok(o) && !(epi == EPI_JACOBI0 && o->pmax == 3 && !same_toeplitz12(o))) ? 10 : 9;
     const int v5_diag = (v >= 101 && v <= 113) ? v - 100 : 0;   // v5 diagnostic / tuning builds
     if (v5_diag) v = 10;
     const int v7_diag = (v >= 121 && v <= 124) ? v - 120 : 0;   // v7 diagnostic / tuning builds
@@ -872,7 +874,7 @@ int poms_op_apply_dot(poms_op* op, const double* x, double* y, int64_t zb, int64
 int poms_op_apply_dot_supported(poms_op* op, int* yes) {
     if (!op || !yes) { set_error("poms_op_apply_dot_supported: null argument"); return 1; }
     const int v = op->variant;
-    *yes = (op->form == FORM_STENCIL || v == 4 || v == 8 || v == 9 || v == 10) ? 1 : 0;
+    *yes = (op->form == FORM_STENCIL || v == 4 || v == 8 || v == 9 || v == 10 || v == 11) ? 1 : 0;
     return 0;
 }
 
@@ -888,7 +890,8 @@ int poms_op_from_zero_supported(poms_op* op, int* yes) {
     if (!op || !yes) { set_error("poms_op_from_zero_supported: null argument"); return 1; }
     const int64_t bytes = (int64_t)(op->L.n[0] + 2 * op->L.pads[0]) * row_geom(&op->L).s0 * 8;
     *yes = (op->ndim == 3 && op->form != FORM_STENCIL &&
-            (op->variant == 8 || op->variant == 9 || op->variant == 10 || (op->variant >= 110 && op->variant <= 112)) &&
+            (op->variant == 8 || op->variant == 9 || op->variant == 10 || op->variant == 11 ||
+             (op->variant >= 110 && op->variant <= 112)) &&
             bytes < 0x7ffffff0LL) ? 1 : 0;
     return 0;
 }
