@@ -160,12 +160,14 @@ __device__ __forceinline__ void v7_body(double* __restrict__ lds, const double* 
     // (lanes on the 2 HP halo pairs of a row have no output), so the stage-1 centre
     // tap is the x at the lane's own output point (the Jacobi / apply-dot history).
     // Idle lanes read pair 0 (in range) and write nothing.
+    // (idle lanes keep their own, distinct addresses: a shared dummy address puts a
+    // second address on some bank of almost every lane group -- 2-way LDS conflicts)
     const int ru = fl / XP, ku = fl - ru * XP;
     const bool act1 = ru < R;
-    const int fu = act1 ? fl : 0;
+    const int fu = act1 ? fl : fl - R * XP;   // (idle lanes: pairs 0.. of the tile, in range)
     const int jo = ku - HP;
     const bool act2 = act1 && jo >= 0 && jo < OP;
-    const int fo = act2 ? fl - HP : 0;  // first window pair (row ru, x pair jo) in the u/v buffer
+    const int fo = max(fu - HP, 0);     // first window pair (row ru, x pair jo) in the u/v buffer
     const int orow = r0 + ru;           // output row (stage 2)
     const int ocol = c0 + 2 * jo;       // output column of element 0
 
@@ -370,20 +372,27 @@ __device__ __forceinline__ void v7_body(double* __restrict__ lds, const double* 
 #pragma unroll
         for (int m = 0; m < NWIN; ++m) {
             if (2 * m + 1 < W0 || 2 * m > W1) continue;
-            if (2 * m < W0) {          // only the pair's second value is used
-                wu[2 * m + 1] = us[2 * m + 1];
-                wvv[2 * m + 1] = us[L::UVQ + 2 * m + 1];
-            } else if (2 * m + 1 > W1) {   // only the first
-                wu[2 * m] = us[2 * m];
-                wvv[2 * m] = us[L::UVQ + 2 * m];
-            } else {
-                const d2 a = *(const d2*)(us + 2 * m);
-                const d2 b = *(const d2*)(us + L::UVQ + 2 * m);
-                wu[2 * m] = a[0];
-                wu[2 * m + 1] = a[1];
-                wvv[2 * m] = b[0];
-                wvv[2 * m + 1] = b[1];
+            // whole pairs (ds_read_b128) even where one value is used: single doubles at a
+            // 16-B lane stride (ds_read_b64) conflict 2-way on every lane group.  (The
+            // Jacobi build with the fused dot lacks the 4 VGPRs: single doubles there.)
+            if constexpr (JAC && JDOT) {
+                if (2 * m < W0) {
+                    wu[2 * m + 1] = us[2 * m + 1];
+                    wvv[2 * m + 1] = us[L::UVQ + 2 * m + 1];
+                    continue;
+                }
+                if (2 * m + 1 > W1) {
+                    wu[2 * m] = us[2 * m];
+                    wvv[2 * m] = us[L::UVQ + 2 * m];
+                    continue;
+                }
             }
+            const d2 a = *(const d2*)(us + 2 * m);
+            const d2 b = *(const d2*)(us + L::UVQ + 2 * m);
+            wu[2 * m] = a[0];
+            wu[2 * m + 1] = a[1];
+            wvv[2 * m] = b[0];
+            wvv[2 * m + 1] = b[1];
         }
         if (fast2) {
 #pragma unroll
@@ -699,6 +708,7 @@ kron_v7_kernel(const double* __restrict__ x, double* __restrict__ y, const doubl
         lds[L::BT2 + 2 * e] = toe ? (SAME12 ? tc.t1a[ct] : tc.t2a[ct]) : a2[(int64_t)r2 * W + k];
         lds[L::BT2 + 2 * e + 1] = toe ? (SAME12 ? tc.t1b[ct] : tc.t2b[ct]) : b2[(int64_t)r2 * W + k];
     }
+    __syncthreads();   // the tables are read from the body's set-up on (Jacobi's omega/diag)
 
     double nrm = 0.0, dotp = 0.0;
     const int nwide = vg.nw2 * vg.t1w;
