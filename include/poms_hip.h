@@ -452,7 +452,13 @@ int poms_op_run_dist(poms_op* op, poms_comm* comm, int epilogue, double omega, c
  * poms_op_run_dist with neighbours prev / next, sums all-reduced).
  * x: in = x0 when has_x0, out = the solution (current ghosts not required).
  * work: 5 vectors of the operator's layout with zero ghosts (r, q and three
- * preconditioner buffers), not aliasing b or x.                                  */
+ * preconditioner buffers), not aliasing b or x.
+ * Speculative mode (opt-in, POMS_PCG_SPEC=1; slower on the measured cycles): the whole
+ * call is queued without reading a stop test, the tests are evaluated once the stream
+ * drains, and if one fires the call is repeated step by step from the restored x0 --
+ * the same bits either way.  Its launches are captured once into a hipGraph per
+ * (buffers, options, timing) and replayed when there is no communicator
+ * (POMS_PCG_GRAPH=0: never).                                                      */
 typedef struct poms_pcg_opts {
     double tol;      /* pcg: stop when r.r < tol * ||r0|| (the reference's mixed norms) */
     int maxiter;
@@ -476,6 +482,10 @@ int poms_pcg_jacobi(poms_op* op, poms_comm* comm, const poms_pcg_opts* opts, con
  * poms_op_timing_read sums the recorded launches of one epilogue: total
  * milliseconds, launch count and output DOFs (synchronises on the events).      */
 int poms_op_timing(poms_op* op, int enable, int epilogue, int every, int reserve);
+/* Speculative smoother calls of this operator: stats[0] calls, [1] calls repeated
+ * step by step (a stop test fired), [2] graph captures, [3] graph replays of an
+ * earlier capture.                                                                */
+int poms_op_spec_stats(poms_op* op, int* stats);
 int poms_op_timing_read(poms_op* op, int epilogue, double* total_ms, int64_t* launches, int64_t* dofs);
 
 #ifdef __cplusplus

@@ -76,6 +76,7 @@ _SIGS = {
     "poms_op_get_variant": [_vp, C.POINTER(_i)],
     "poms_op_kernel_variant": [_vp, _i, C.POINTER(_i)],
     "poms_op_last_variant": [_vp, C.POINTER(_i)],
+    "poms_op_spec_stats": [_vp, C.POINTER(_i)],
     "poms_vec_axpby_dev": [_vp, _LP, _vp, _vp, _vp, _vp, _vp],
     "poms_op_run_reduce": [_vp, _i, _d, _vp, _vp, _vp, _i64, _i64, _vp, _vp, _i, _vp],
     "poms_op_run_reduce2": [_vp, _i, _d, _vp, _vp, _vp, _i64, _i64, _i64, _i64, _vp, _vp, _i, _vp],

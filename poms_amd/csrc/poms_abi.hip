@@ -73,6 +73,29 @@ struct poms_ctx {
     double* scratch = nullptr;  // reduction partials
 };
 
+// A launch-timing event; under stream capture it becomes an event-record node of the
+// graph (every replay records it again), not a capture-ordering marker.
+static hipError_t timing_record(hipEvent_t e, hipStream_t s) {
+    hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
+    const hipError_t q = hipStreamIsCapturing(s, &cs);
+    if (q != hipSuccess) return q;
+    if (cs != hipStreamCaptureStatusActive) return hipEventRecord(e, s);
+    // an event-record node after the capture's current frontier, which it then replaces
+    hipGraph_t g = nullptr;
+    const hipGraphNode_t* deps = nullptr;
+    size_t nd = 0;
+    hipError_t r = hipStreamGetCaptureInfo_v2(s, &cs, nullptr, &g, &deps, &nd);
+    if (r != hipSuccess) return r;
+    hipGraphNode_t node = nullptr;
+    r = hipGraphAddEventRecordNode(&node, g, deps, nd, e);
+    if (r != hipSuccess) return r;
+    return hipStreamUpdateCaptureDependencies(s, &node, 1, hipStreamSetCaptureDependencies);
+}
+
+// Host-reduced partials of one speculative launch: blocks n at offset off of the pinned
+// region, kind bit 0 norm / bit 1 dot, into value index vi (+1 when both).
+struct SpecPart { int64_t off; int n; int kind; int vi; };
+
 struct poms_op {
     poms_ctx* ctx = nullptr;
     // where a launch writes its per-block partials: norms at scratch + part_off, dots
@@ -112,6 +135,30 @@ struct poms_op {
     // partials at [0, n), bit 1 dot partials after them.
     static constexpr int kSvPart = 4096;
     double* sv_part = nullptr;   // kSvRing x kSvPart, pinned, device-mapped, armed unset
+    // poms_pcg_jacobi, speculative mode: the sweeps' per-block partials (pinned,
+    // device-mapped; kSpecPart doubles), the device array of the other host-read sums,
+    // and the backup of x0
+    static constexpr int64_t kSpecPart = 1 << 19;
+    static constexpr int kSpecVals = 4096;
+    double* spec_part = nullptr;
+    double* spec_dev = nullptr;
+    double* spec_host = nullptr;    // kSpecVals, pinned
+    double* spec_bak = nullptr;
+    int64_t spec_bak_n = 0;
+    struct SpecGraph {   // a captured speculative call (see pcg_speculative)
+        uint64_t key[16] = {};
+        hipGraphExec_t exec = nullptr;
+        std::vector<SpecPart> parts;
+        std::vector<int> chk, rr;
+        int sn = 0, vrr0 = 0;
+        int64_t use = 0;
+    };
+    static constexpr int kSpecGraphs = 4;
+    SpecGraph spec_graphs[kSpecGraphs];
+    int64_t spec_graph_clock = 0;
+    int spec_graph_hits = 0, spec_graph_caps = 0;   // graphs stop when captures outnumber hits
+    int spec_calls = 0, spec_repeats = 0;            // speculative calls, and those repeated step by step
+    hipStream_t cap_stream = nullptr;                 // private non-blocking capture stream
     int sv_npart[kSvRing] = {};
     int sv_pkind[kSvRing] = {};
     // op_run: write the partials to part_dst instead of the scratch when they fit
@@ -511,10 +558,14 @@ int poms_op_stencil_data(poms_op* o, double* data_host) {
 
 int poms_op_destroy(poms_op* o) {
     if (!o) return 0;
-    for (double* p : {o->a0t, o->b0t, o->a1, o->b1, o->a2, o->b2, o->dg2a, o->dg2b, o->rdiag0, o->coef, o->sv_dev})
+    for (double* p : {o->a0t, o->b0t, o->a1, o->b1, o->a2, o->b2, o->dg2a, o->dg2b, o->rdiag0, o->coef, o->sv_dev,
+                      o->spec_dev, o->spec_bak})
         if (p) (void)hipFree(p);
-    if (o->sv_host) (void)hipHostFree(o->sv_host);
-    if (o->sv_part) (void)hipHostFree(o->sv_part);
+    for (double* p : {o->sv_host, o->sv_part, o->spec_part, o->spec_host})
+        if (p) (void)hipHostFree(p);
+    for (auto& g : o->spec_graphs)
+        if (g.exec) (void)hipGraphExecDestroy(g.exec);
+    if (o->cap_stream) (void)hipStreamDestroy(o->cap_stream);
     for (auto& t : o->tl) {
         (void)hipEventDestroy(t.e0);
         (void)hipEventDestroy(t.e1);
@@ -547,6 +598,15 @@ int poms_op_kernel_variant(poms_op* op, int epilogue, int* variant) {
 int poms_op_last_variant(poms_op* op, int* variant) {
     if (!op || !variant) { set_error("poms_op_last_variant: null argument"); return 1; }
     *variant = op->last_variant;
+    return 0;
+}
+
+int poms_op_spec_stats(poms_op* op, int* stats) {
+    if (!op || !stats) { set_error("poms_op_spec_stats: null argument"); return 1; }
+    stats[0] = op->spec_calls;
+    stats[1] = op->spec_repeats;
+    stats[2] = op->spec_graph_caps;
+    stats[3] = op->spec_graph_hits;
     return 0;
 }
 
@@ -826,7 +886,7 @@ static int op_run(poms_op* o, int epi, double omega, const double* x, double* y,
         tlh = &o->tl[o->tl_used++];
         tlh->epi = epi;
         tlh->ndof = (int64_t)((ze - zb) + (ze2 - zb2)) * g.n1 * g.n2;
-        POMS_HIP_CHECK(hipEventRecord(tlh->e0, as_stream(stream)));
+        POMS_HIP_CHECK(timing_record(tlh->e0, as_stream(stream)));
     }
     const int rc = v == 11
         ? kron_v7_launch(o->pmax, epi, p, g, o->tc, omega, as_stream(stream), v7_diag)
@@ -838,7 +898,7 @@ static int op_run(poms_op* o, int epi, double omega, const double* x, double* y,
         ? kron_v4_launch(o->pmax, o->ndim == 3, o->form, epi, p, g, o->tc, omega, as_stream(stream),
                          v == 7 ? 0 : v - 91)
         : kron_v3_launch(v, o->pmax, o->ndim == 3, o->form, epi, p, g, o->tc, omega, as_stream(stream));
-    if (tlh) POMS_HIP_CHECK(hipEventRecord(tlh->e1, as_stream(stream)));
+    if (tlh) POMS_HIP_CHECK(timing_record(tlh->e1, as_stream(stream)));
     if (rc) return 1;
     POMS_HIP_CHECK(hipGetLastError());
     o->last_partials = (want_norm || want_dot) ? nblk : 0;
@@ -1861,6 +1921,80 @@ struct PcgRun {
         return lazy_post(h, 1);
     }
 
+    // ---- speculative mode (spec_*): the whole smoother call is queued without reading a
+    // single stop test; every host-read sum goes to its own place (a partials region of
+    // op->spec_part, or op->spec_dev[i]) and the tests are evaluated once the stream has
+    // drained.  If one of them fires, the call is repeated step by step (x0 restored).
+    // The launches and their order are those of the step-by-step loop when no test
+    // fires, so the result is the same bits (tests/test_gpu_solvers.py).
+    using SPart = SpecPart;
+    std::vector<SPart> sparts;
+    int64_t scur = 0;       // next free double of op->spec_part
+    int sn = 0;             // next free value index
+    std::vector<int> schk;  // value indices tested against jtol^2 (< fires)
+    std::vector<int> srr;   // pcg r.r value index per iteration (k = 1..)
+    int svals(int cnt) {
+        const int i = sn;
+        sn += cnt;
+        return i;
+    }
+    // an operator launch whose sums are tested at the end: [dot, norm] at value vi
+    int sjrun(int epi, const double* x, double* y, const double* b, bool wn, bool wd, int* vi_out) {
+        const int cnt = (wn ? 1 : 0) + (wd ? 1 : 0);
+        const int vi = svals(cnt);
+        *vi_out = vi;
+        double* dn = wn ? op->spec_dev + vi + (wd ? 1 : 0) : nullptr;
+        double* dd = wd ? op->spec_dev + vi : nullptr;
+        if (!direct()) return run(epi, x, y, b, dn, dd);
+        op->part_dst = op->spec_part + scur;
+        op->part_cap = poms_op::kSpecPart - scur;
+        const int rc = op_run_epi(op, epi, o->omega, x, y, b, 0, n0, 0, 0, wn, wd, stv);
+        op->part_dst = nullptr;
+        if (rc) return 1;
+        const int64_t n = op->last_partials;
+        if (op->last_part_host) {
+            sparts.push_back(SPart{scur, (int)n, (wn ? 1 : 0) | (wd ? 2 : 0), vi});
+            scur += cnt * n;
+            return 0;
+        }
+        double* pdot = op->ctx->scratch + (op->dot_base < 0 ? n : op->dot_base);
+        if (wn) reduce_launch(op->ctx->scratch, (int)n, dn, st);
+        if (wd) reduce_launch(pdot, (int)n, dd, st);
+        POMS_HIP_CHECK(hipGetLastError());
+        return 0;
+    }
+    // damped_jacobi with every sweep queued (no stop test read); as damped_jacobi below
+    int spec_damped_jacobi(const double* rhs, double* A, double* B, int dot_idx, double** out) {
+        const int maxit = o->jmaxiter;
+        double *x = A, *xn = B;
+        int fz = 0, k0;
+        if (op->ndim == 3 && maxit >= 2 && maxit != 2 && op->form != FORM_STENCIL) (void)poms_op_from_zero_supported(op, &fz);
+        if (fz) {   // sweeps 1, 2 from x = 0: [||x1||^2, ||dr2||^2]
+            int vi;
+            if (sjrun(EPI_JACOBI0, rhs, A, rhs, true, true, &vi)) return 1;
+            schk.push_back(vi);
+            schk.push_back(vi + 1);
+            k0 = 3;
+        } else {
+            const int vi = svals(1);
+            if (poms_op_diag_scale(op, o->omega, rhs, A, 1, stv)) return 1;
+            reduce_launch(op->ctx->scratch, (int)op->last_partials, op->spec_dev + vi, st);   // (rank sums at the end)
+            schk.push_back(vi);
+            k0 = 2;
+        }
+        for (int k = k0; k <= maxit; ++k) {
+            if (k == maxit) {   // the last sweep's norm cannot change the result: x . rhs instead
+                if (run(EPI_JACOBI, x, xn, rhs, nullptr, sc + dot_idx) || allsum(sc + dot_idx, 1)) return 1;
+            } else {
+                int vi;
+                if (sjrun(EPI_JACOBI, x, xn, rhs, true, false, &vi)) return 1;
+                schk.push_back(vi);
+            }
+            std::swap(x, xn);
+        }
+        *out = x;
+        return 0;
+    }
     // damped_jacobi(A, rhs) with x0 = None into buffers {A, B}; the last sweep also
     // forms x . rhs into sc[dot_idx] (*dot_done = 1), else the caller forms it.
     int damped_jacobi(const double* rhs, double* A, double* B, int dot_idx, double** out, int* dot_done) {
@@ -1937,6 +2071,180 @@ struct PcgRun {
 
 }  // namespace
 
+// Speculative smoother call (see PcgRun::spec_*), in two halves: spec_issue queues every
+// launch of the call (and, last, the copy of the device-held sums to the host); the
+// values it needs later are described by R.sparts / schk / srr / sn / vrr0.
+// spec_finish waits for the stream and evaluates the stop tests: 0 done, 1 error, 2 a
+// stop test fired (the caller repeats the call step by step).
+static int spec_issue(PcgRun& R, const double* b, double* x, int has_x0, double* const* work, int* vrr0_out) {
+    poms_op* op = R.op;
+    const poms_pcg_opts* o = R.o;
+    poms_ctx* ctx = op->ctx;
+    const poms_layout* L = &op->L;
+    void* stream = R.stv;
+    double *r = work[0], *q = work[1];
+    double* z[3] = {work[2], work[3], work[4]};
+    if (has_x0) {   // x0 is kept for the step-by-step repeat
+        const int64_t nbak = (int64_t)(op->L.n[0] + 2 * op->L.pads[0]) * row_geom(&op->L).s0;
+        POMS_HIP_CHECK(hipMemcpyAsync(op->spec_bak, x, nbak * sizeof(double), hipMemcpyDeviceToDevice, R.st));
+    }
+    if (!has_x0) {
+        if (poms_vec_fill(ctx, L, 0.0, x, stream) || poms_vec_scale(ctx, L, 1.0, b, r, stream)) return 1;
+    } else if (R.run(EPI_RESID, x, r, b, nullptr, nullptr)) {
+        return 1;
+    }
+    const int vrr0 = R.svals(1);
+    *vrr0_out = vrr0;
+    if (poms_vec_dot(ctx, L, r, r, op->spec_dev + vrr0, stream)) return 1;
+    double* s = nullptr;
+    if (R.spec_damped_jacobi(r, z[0], z[1], SC_SR, &s)) return 1;
+    double* p = s;   // p keeps this buffer; the later psolves use the other two
+    double* fa = nullptr;
+    double* fb = nullptr;
+    for (double* c : z)
+        if (c != p) (fa ? fb : fa) = c;
+    for (int k = 1; k <= o->maxiter; ++k) {
+        if (R.run(EPI_APPLYDOT, p, q, p, nullptr, R.sc + SC_PQ) || R.allsum(R.sc + SC_PQ, 1)) return 1;
+        hipLaunchKernelGGL(pcg_scalars_kernel, dim3(1), dim3(64), 0, R.st, R.sc, 0);
+        const int vrr = R.svals(1);
+        R.srr.push_back(vrr);
+        if (poms_pcg_r_update_dev(ctx, L, R.sc + SC_ALPHA, r, q, op->spec_dev + vrr, stream)) return 1;
+        double* sn = nullptr;
+        if (R.spec_damped_jacobi(r, fa, fb, SC_SRN, &sn)) return 1;
+        hipLaunchKernelGGL(pcg_scalars_kernel, dim3(1), dim3(64), 0, R.st, R.sc, 1);
+        if (poms_pcg_xp_update_dev(ctx, L, R.sc + SC_ALPHA2, x, p, sn, stream)) return 1;
+    }
+    if (R.sn > poms_op::kSpecVals) { set_error("pcg speculative: too many values"); return 1; }
+    if (R.comm && R.sn > 0 && poms_allreduce_sum(R.comm, op->spec_dev, R.sn, stream, 1)) return 1;
+    if (R.sn > 0)
+        POMS_HIP_CHECK(hipMemcpyAsync(op->spec_host, op->spec_dev, R.sn * sizeof(double), hipMemcpyDeviceToHost, R.st));
+    POMS_HIP_CHECK(hipGetLastError());
+    return 0;
+}
+
+static int spec_finish(PcgRun& R, int vrr0, poms_pcg_info* info) {
+    const poms_pcg_opts* o = R.o;
+    POMS_HIP_CHECK(hipStreamSynchronize(R.st));
+    std::vector<double> v(R.op->spec_host, R.op->spec_host + R.sn);
+    for (const PcgRun::SPart& s : R.sparts) {
+        const bool wn = s.kind & 1, wd = s.kind & 2;
+        const double* reg = R.op->spec_part + s.off;
+        if (wn) v[s.vi + (wd ? 1 : 0)] = PcgRun::host_reduce(reg, s.n);
+        if (wd) v[s.vi] = PcgRun::host_reduce(reg + (wn ? s.n : 0), s.n);
+    }
+    const double tol2 = o->jtol * o->jtol;
+    for (int i : R.schk)
+        if (v[i] < tol2) return 2;
+    const double nrmr0 = std::sqrt(v[vrr0]);
+    for (int i : R.srr)
+        if (v[i] < o->tol * nrmr0) return 2;
+    const double nrmr = R.srr.empty() ? nrmr0 * nrmr0 : v[R.srr.back()];
+    info->niter = o->maxiter;
+    info->success = 0;
+    info->res_norm = std::sqrt(nrmr);
+    return 0;
+}
+
+// One speculative call, through a captured graph of its launches when POMS_PCG_GRAPH
+// is not 0 and there is no host-transport communicator (its callbacks synchronise).
+// Graphs are cached per operator by the call's buffers, options and launch-timing
+// state (kSpecGraphs entries, least recently used replaced).
+static int pcg_speculative(PcgRun& R, const double* b, double* x, int has_x0, double* const* work,
+                           poms_pcg_info* info) {
+    poms_op* op = R.op;
+    const poms_pcg_opts* o = R.o;
+    // POMS_PCG_GRAPH=0: never.  Not with a communicator: the distributed operator call's
+    // ring-slot and exchange bookkeeping is host-side per call (a captured RCCL
+    // loopback call crashed in the attempt, r04graph logs).  A caller whose buffers
+    // never repeat would capture every call: after 8 more captures than hits the
+    // operator stops using graphs.
+    const char* ge = getenv("POMS_PCG_GRAPH");
+    const bool graph = !(ge && ge[0] == '0') && !R.comm && op->spec_graph_caps <= op->spec_graph_hits + 8;
+    if (!graph) {
+        int vrr0 = 0;
+        if (spec_issue(R, b, x, has_x0, work, &vrr0)) return 1;
+        return spec_finish(R, vrr0, info);
+    }
+    uint64_t key[16] = {};
+    auto bits = [](double d) { uint64_t u; std::memcpy(&u, &d, 8); return u; };
+    key[0] = (uint64_t)(uintptr_t)b;
+    key[1] = (uint64_t)(uintptr_t)x;
+    for (int i = 0; i < 5; ++i) key[2 + i] = (uint64_t)(uintptr_t)work[i];
+    key[7] = (uint64_t)has_x0 | ((uint64_t)(uint32_t)o->maxiter << 8) | ((uint64_t)(uint32_t)o->jmaxiter << 40);
+    key[8] = bits(o->tol);
+    key[9] = bits(o->jtol);
+    key[10] = bits(o->omega);
+    key[11] = (uint64_t)(uint32_t)op->variant | ((uint64_t)(uint32_t)op->chunk << 32);
+    key[12] = (uint64_t)(op->timing ? 1 : 0) | ((uint64_t)(uint32_t)op->t_epi << 8) | ((uint64_t)(uint32_t)op->t_every << 32);
+    key[13] = (uint64_t)(uintptr_t)R.comm | ((uint64_t)(uint32_t)(o->prev + 1) << 48) | ((uint64_t)(uint32_t)(o->next + 1) << 56);
+    poms_op::SpecGraph* hit = nullptr;
+    for (auto& g : op->spec_graphs)
+        if (g.exec && std::memcmp(g.key, key, sizeof(key)) == 0) hit = &g;
+    if (!hit) {   // capture the call's launches once
+        poms_op::SpecGraph* slot = &op->spec_graphs[0];
+        for (auto& g : op->spec_graphs)
+            if (!g.exec || g.use < slot->use) slot = &g;
+        if (slot->exec) {
+            (void)hipGraphExecDestroy(slot->exec);
+            slot->exec = nullptr;
+        }
+        // captured on a private stream (torch's default stream is the null stream, which
+        // cannot be captured); nothing runs until the graph is launched on the caller's
+        if (!op->cap_stream) POMS_HIP_CHECK(hipStreamCreateWithFlags(&op->cap_stream, hipStreamNonBlocking));
+        const hipStream_t cst = R.st;
+        void* const cstv = R.stv;
+        R.st = op->cap_stream;
+        R.stv = op->cap_stream;
+        POMS_HIP_CHECK(hipStreamBeginCapture(R.st, hipStreamCaptureModeRelaxed));
+        int vrr0 = 0;
+        const int rc = spec_issue(R, b, x, has_x0, work, &vrr0);
+        hipGraph_t gr = nullptr;
+        const hipError_t ce = hipStreamEndCapture(R.st, &gr);
+        R.st = cst;
+        R.stv = cstv;
+        ++op->spec_graph_caps;
+        if (rc || ce != hipSuccess) {
+            if (gr) (void)hipGraphDestroy(gr);
+            if (!rc) set_error(std::string("pcg graph capture: ") + hipGetErrorString(ce));
+            return 1;
+        }
+        hipGraphExec_t ex = nullptr;
+        const hipError_t ie = hipGraphInstantiate(&ex, gr, nullptr, nullptr, 0);
+        (void)hipGraphDestroy(gr);
+        if (ie != hipSuccess) { set_error(std::string("pcg graph instantiate: ") + hipGetErrorString(ie)); return 1; }
+        std::memcpy(slot->key, key, sizeof(key));
+        slot->exec = ex;
+        slot->parts = R.sparts;
+        slot->chk = R.schk;
+        slot->rr = R.srr;
+        slot->sn = R.sn;
+        slot->vrr0 = vrr0;
+        hit = slot;
+    } else {
+        ++op->spec_graph_hits;
+    }
+    hit->use = ++op->spec_graph_clock;
+    POMS_HIP_CHECK(hipGraphLaunch(hit->exec, R.st));
+    R.sparts = hit->parts;
+    R.schk = hit->chk;
+    R.srr = hit->rr;
+    R.sn = hit->sn;
+    return spec_finish(R, hit->vrr0, info);
+}
+
+// Speculative mode: POMS_PCG_SPEC=1 always, 0 never; by default when a sweep is short
+// (< 32 M local DOF: the 2D grids, the 8-GPU slabs), where the host's turn-around per
+// sweep, not the GPU, set the pace of the step-by-step loop.
+// Speculative mode is opt-in (POMS_PCG_SPEC=1): on the 2D 1024^2 cycle, measured in one
+// process against the step-by-step loop, it costs 3.8 ms per cycle vs 3.1 (graph replay
+// included; profiles/r04/graph): the stream drain it needs at the end of every call
+// exposes the host's issue of the next phase, and the step-by-step loop's lazy reads
+// already keep the queue ahead of the GPU.
+static bool pcg_spec_wanted(const poms_op*, const poms_pcg_opts* o) {
+    const char* e = getenv("POMS_PCG_SPEC");
+    return e && e[0] == '1' && o->maxiter >= 1 && o->jmaxiter >= 3;
+}
+
 int poms_pcg_jacobi(poms_op* op, poms_comm* comm, const poms_pcg_opts* o, const double* b, double* x, int has_x0,
                     double* const* work, poms_pcg_info* info, void* stream) {
     if (!op || !o || !b || !x || !work || !info) { set_error("poms_pcg_jacobi: null argument"); return 1; }
@@ -1956,6 +2264,32 @@ int poms_pcg_jacobi(poms_op* op, poms_comm* comm, const poms_pcg_opts* o, const 
                                      hipHostMallocMapped | hipHostMallocCoherent));
         PcgRun::part_arm(op->sv_part, poms_op::kSvRing * poms_op::kSvPart);
         for (int64_t& q : op->sv_seq) q = -1;
+    }
+    if (pcg_spec_wanted(op, o)) {
+        const int64_t nbak = (int64_t)(op->L.n[0] + 2 * op->L.pads[0]) * row_geom(&op->L).s0;
+        if (!op->spec_dev) {
+            POMS_HIP_CHECK(hipMalloc(reinterpret_cast<void**>(&op->spec_dev), poms_op::kSpecVals * sizeof(double)));
+            POMS_HIP_CHECK(hipHostMalloc(reinterpret_cast<void**>(&op->spec_host), poms_op::kSpecVals * sizeof(double),
+                                         hipHostMallocDefault));
+            POMS_HIP_CHECK(hipHostMalloc(reinterpret_cast<void**>(&op->spec_part), poms_op::kSpecPart * sizeof(double),
+                                         hipHostMallocMapped | hipHostMallocCoherent));
+        }
+        if (has_x0 && op->spec_bak_n < nbak) {
+            if (op->spec_bak) POMS_HIP_CHECK(hipFree(op->spec_bak));
+            op->spec_bak = nullptr;
+            op->spec_bak_n = 0;
+            POMS_HIP_CHECK(hipMalloc(reinterpret_cast<void**>(&op->spec_bak), nbak * sizeof(double)));
+            op->spec_bak_n = nbak;
+        }
+        PcgRun RS{op, comm, o, as_stream(stream), stream, op->sv_dev, op->sv_host};
+        RS.n0 = op->ndim == 3 ? op->L.n[0] : 1;
+        ++op->spec_calls;
+        const int rc = pcg_speculative(RS, b, x, has_x0, work, info);
+        if (rc != 2) return rc;
+        ++op->spec_repeats;
+        // a stop test fired: the step-by-step loop from the same inputs
+        if (has_x0)
+            POMS_HIP_CHECK(hipMemcpyAsync(x, op->spec_bak, nbak * sizeof(double), hipMemcpyDeviceToDevice, as_stream(stream)));
     }
     PcgRun R{op, comm, o, as_stream(stream), stream, op->sv_dev, op->sv_host};
     R.n0 = op->ndim == 3 ? op->L.n[0] : 1;

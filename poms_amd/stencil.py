@@ -682,6 +682,14 @@ class KronOperator:
         _lib.call("poms_op_last_variant", self._h, C.byref(v))
         return v.value
 
+    @property
+    def spec_stats(self) -> dict:
+        """The native smoother's speculative calls: calls, repeats (a stop test fired,
+        the call ran again step by step), graph captures and graph replays."""
+        v = (C.c_int * 4)()
+        _lib.call("poms_op_spec_stats", self._h, v)
+        return {"calls": v[0], "repeats": v[1], "captures": v[2], "replays": v[3]}
+
     def kernel_variant(self, epilogue: str) -> int:
         """Variant one launch of ``epilogue`` runs after auto-selection / fall-backs."""
         v = C.c_int()

@@ -385,6 +385,79 @@ def test_native_pcg_device_reduction_fallback(gpu, monkeypatch, cap, ndim, N, p,
         assert out["1"][1][k] == out["0"][1][k], k
 
 
+@pytest.mark.parametrize("ndim,N,p,scale,x0,tol,maxiter", [
+    (2, 64, 3, 1.0, False, 1e-6, 10),      # no stop test fires: the speculative run stands
+    (2, 64, 3, 1.0, True, 1e-6, 10),       # (with x0)
+    (3, 20, 3, 1.0, True, 1e-6, 4),        # 3D: sweeps 1-2 from zero in one launch
+    (3, 16, 2, 1e-5, False, 1e-6, 10),     # damped Jacobi stops: repeated step by step
+    (2, 40, 1, 1e-9, True, 1e-6, 10),      # ... with x0 restored first
+    (3, 16, 3, 1.0, False, 0.5, 10),       # pcg stops early
+])
+def test_speculative_pcg_matches_step_by_step(gpu, monkeypatch, ndim, N, p, scale, x0, tol, maxiter):
+    """poms_pcg_jacobi's speculative mode (every launch of the smoother call queued, the
+    stop tests evaluated once the stream drains; POMS_PCG_SPEC=1) == the step-by-step
+    loop (POMS_PCG_SPEC=0) == the Python device loop, bitwise -- including the cases
+    where a stop test fires and the call is repeated from the restored x0."""
+    from poms_amd import solvers
+    from poms_amd.stencil import KronOperator, StencilVectorSpace
+    M, K = assemble_1d(uniform_knots(p, N), p)
+    n = N + p
+    V = StencilVectorSpace([n] * ndim, [p] * ndim)
+    A = KronOperator.laplace(V, [M] * ndim, [K] * ndim)
+    rng = np.random.default_rng(N + 7 * p)
+    b = V.zeros().from_numpy(scale * rng.standard_normal((n,) * ndim))
+    xi = V.zeros().from_numpy(rng.standard_normal((n,) * ndim)) if x0 else None
+    out = {}
+    xin = None if xi is None else xi.copy()   # one buffer for every native call: the graph key repeats
+    for mode in ("python", "0", "1", "g", "g2"):
+        monkeypatch.setenv("POMS_NATIVE_PCG", "0" if mode == "python" else "1")
+        monkeypatch.setenv("POMS_PCG_SPEC", {"python": "0", "0": "0"}.get(mode, "1"))
+        monkeypatch.setenv("POMS_PCG_GRAPH", "1" if mode.startswith("g") else "0")
+        if xi is not None:
+            xin._data.copy_(xi._data)
+        x, info = solvers.pcg(A, solvers.damped_jacobi, b, x0=xin, tol=tol, maxiter=maxiter,
+                              _x0_owned=mode != "python")
+        out[mode] = (x.to_local_numpy(), info)
+        del x
+    st = A.spec_stats
+    caps, hits = st["captures"], st["replays"]
+    assert st["calls"] == 3
+    if x0:   # same b, x, work and options: "g" captured, "g2" replayed
+        assert caps == 1 and hits == 1, (caps, hits)
+    else:    # (x = V.zeros() per call: the allocator decides whether the key repeats)
+        assert caps + hits == 2, (caps, hits)
+    for mode in ("0", "1", "g", "g2"):
+        np.testing.assert_array_equal(out[mode][0], out["python"][0])
+        for k in ("niter", "success", "res_norm"):
+            assert out[mode][1][k] == out["python"][1][k], (mode, k)
+
+
+def test_graph_replay_records_launch_timing(gpu, monkeypatch):
+    """Speculative calls replayed from a captured graph: the timed launches are event
+    nodes of the graph, recorded again by every replay."""
+    from poms_amd import solvers
+    from poms_amd.stencil import KronOperator, StencilVectorSpace
+    p, N = 3, 16
+    M, K = assemble_1d(uniform_knots(p, N), p)
+    V = StencilVectorSpace([N + p] * 3, [p] * 3)
+    A = KronOperator.laplace(V, [M] * 3, [K] * 3)
+    b = V.zeros().from_numpy(np.ones((N + p,) * 3))
+    x = V.zeros()
+    monkeypatch.setenv("POMS_PCG_SPEC", "1")
+    monkeypatch.setenv("POMS_PCG_GRAPH", "1")
+    A.timing(True)
+    for _ in range(3):
+        x._data.zero_()
+        solvers.pcg(A, solvers.damped_jacobi, b, x0=x, tol=1e-6, maxiter=3, _x0_owned=True)
+    st = A.spec_stats
+    assert st["calls"] == 3 and st["repeats"] == 0 and st["captures"] == 1 and st["replays"] == 2, st
+    t, n, d = A.timing_read("jacobi")
+    A.timing(False)
+    # the capture's launches (one call: 3 + 1 preconditioner calls of 8 sweep launches),
+    # their events holding the last replay's times
+    assert n == 4 * 8 and t > 0
+
+
 def test_op_timing_counts_native_launches(gpu):
     """poms_op_timing records every operator launch, including the native loop's."""
     from poms_amd import solvers
