@@ -131,12 +131,29 @@ def run_gpu():
     host_tr = os.environ.get("POMS_TEST_HOST_TRANSPORT") == "1"
     host_shm = os.environ.get("POMS_TEST_HOST_SHM") == "1"
     d = SlabDistribution.from_process_group(n, host_transport=host_tr, host_shm=host_shm)
-    check(d.transport == ("native-host" if host_tr else "torch"), f"transport {d.transport}")
+    world = dist.get_world_size()
+    check(d.transport == ("none" if world == 1 else "native-host" if host_tr else "torch"), f"transport {d.transport}")
     if host_tr:   # the host-read sums take the node-local shared-memory block when asked
         check(d.native.uses_shm == host_shm, f"shm attached {d.native.uses_shm}")
     V = StencilVectorSpace([n] * 3, [p] * 3, dist=d)
     A = KronOperator.laplace(V, [M] * 3, [K] * 3)
     x, b = V.zeros().from_numpy(xg), V.zeros().from_numpy(bg)
+    if world == 1 and host_tr:
+        # one rank, no neighbour: poms_op_run_dist itself (the space is not distributed, so
+        # only a direct call reaches it) must take the single-launch path -- no exchange is
+        # queued -- and equal the plain launch bitwise, sums included
+        y_ref, xo_ref = A.dot(x), V.zeros()
+        nrm_ref = A.jacobi_sweep(b, x, xo_ref, 2.0 / 3.0, want_norm=True)
+        for _ in range(3):
+            x._ghost_valid = False   # asks for an exchange, which has no neighbour to go to
+            y = V.zeros()
+            A._run_native("apply", x, y)
+            check(bool(torch.equal(y._data, y_ref._data)), "no-neighbour run_dist apply")
+            x._ghost_valid = False
+            xo, nd = V.zeros(), torch.zeros(1, dtype=torch.float64, device="cuda")
+            A._run_native("jacobi", x, xo, b, omega=2.0 / 3.0, norm_out=nd)
+            check(bool(torch.equal(xo._data, xo_ref._data)), "no-neighbour run_dist jacobi")
+            check(abs(float(nd) - nrm_ref) <= 1e-13 * nrm_ref, f"no-neighbour run_dist norm {float(nd)} vs {nrm_ref}")
     sl = slice(d.start, d.end)
     Ag = orc.kron_sum_apply(xg, [M] * 3, [K] * 3)
     y = A.dot(x).to_local_numpy()
@@ -219,6 +236,7 @@ def run_gpu_fullsize_slabs():
     def local(vg):
         v = Vl.zeros()
         Vl.interior(v._data).copy_(Vg.interior(vg._data)[sl])
+        v._mark_written()   # the ghosts now stale: the next operator call exchanges them
         return v
 
     def cmp(tag, vl, vg, tol=1e-13):
