@@ -165,7 +165,9 @@ kron_v5_kernel(const double* __restrict__ x, double* __restrict__ y, const doubl
     constexpr bool J0NS = J0 && (MODE == 3 || MODE == 5);
     constexpr bool J0NX = J0 && (MODE == 4 || MODE == 5);
     constexpr int JS_OFF = (D1_OFF + (J0 ? 2 * XR : 0) + 1) & ~1;
-    constexpr int LDS_N = JS_OFF + (JSL ? 2 * NW * 64 : 0);
+    // J0: a row of ones, the post-axis-1 scale of the planes / tiles scaled in the ring
+    constexpr int ONE_OFF = JS_OFF + (JSL ? 2 * NW * 64 : 0);
+    constexpr int LDS_N = ONE_OFF + (J0 ? TC : 0);
     __shared__ __attribute__((aligned(16))) double lds[LDS_N];
 
     // SAME12: axis 2's Toeplitz rows equal axis 1's bitwise (one knot vector on both
@@ -337,6 +339,7 @@ kron_v5_kernel(const double* __restrict__ x, double* __restrict__ y, const doubl
         for (int e = tid; e < XR * TC; e += NW * 64)
             lds[RS_OFF + e] = j0_scale(e / TC, e % TC, tc.t0a[0], tc.t0b[0]);
         if constexpr (JSL) *(d2*)(lds + JS_OFF + 2 * tid) = d2{0.0, 0.0};
+        if (tid < TC) lds[ONE_OFF + tid] = 1.0;
         __syncthreads();
     }
     if constexpr (RCIL) {
@@ -392,41 +395,50 @@ kron_v5_kernel(const double* __restrict__ x, double* __restrict__ y, const doubl
                     dma_x(t + PFX < nplanes ? z0 - P + t + PFX : -(1 << 20), (t + PFX) % D);
                 }
 
-                // ---- axis 1: u = F1a x, v = F1b x on this wave's row, 2 columns per lane
-                const double* xs = lds + XS_OFF + (t % D) * XR * TC + 2 * lane;
-                d2 xv[W];
-#pragma unroll
-                for (int k = 0; k < W; ++k) xv[k] = *(const d2*)(xs + (wv + k) * TC);
                 // J0: the ring holds b; x1 = s b with s = omega / diag.  On a row-Toeplitz tile
                 // (jrf) and a plane of the axis-0 Toeplitz interior s depends on the column only
-                // and is applied after the axis-1 pass (below); elsewhere each of the 2P+1 rows
-                // is scaled as it is read (s from the LDS table, or -- the P planes next to each
-                // global end -- formed from the plane's axis-0 diagonal entries).  Nothing is
-                // written back into the ring: no read-modify-write before the plane's barrier.
+                // and is applied after the axis-1 pass (below).  Elsewhere -- the two tile rows
+                // at the axis-1 ends, and every tile on the P planes next to each global end --
+                // the plane's rows are scaled in the ring in place (s from the LDS table, or
+                // formed from the plane's axis-0 diagonal entries), behind a second barrier, and
+                // the post-axis-1 scale is a row of ones.  (Scaling those rows in registers
+                // instead made the compiler merge three versions of the 2P+1 rows at every
+                // plane: 14 64-bit moves on the hot path, round 4.)
                 bool jsc = false;
                 if constexpr (J0 && !J0NX) {
                     const int m = g.g0 + z0 - P + t;   // global plane of x(t)
                     const bool tp = m >= tc.lo0 && m < tc.hi0;
                     jsc = jrf && tp;
                     if (!jsc) {
+                        double* xsl = lds + XS_OFF + (t % D) * XR * TC;
                         if (tp) {
-#pragma unroll
-                            for (int k = 0; k < W; ++k) {
-                                const d2 sc = *(const d2*)(lds + RS_OFF + (wv + k) * TC + 2 * lane);
-                                xv[k][0] *= sc[0];
-                                xv[k][1] *= sc[1];
+#pragma unroll 1
+                            for (int e = tid; e < XR * TC / 2; e += NW * 64) {
+                                d2 v = *(const d2*)(xsl + 2 * e);
+                                const d2 s = *(const d2*)(lds + RS_OFF + 2 * e);
+                                v[0] *= s[0];
+                                v[1] *= s[1];
+                                *(d2*)(xsl + 2 * e) = v;
                             }
                         } else {
                             const int i0 = (m + P) * W + P;
                             const double d0a = a0t[i0], d0b = b0t[i0];
-#pragma unroll
-                            for (int k = 0; k < W; ++k) {
-                                xv[k][0] *= j0_scale(wv + k, 2 * lane, d0a, d0b);
-                                xv[k][1] *= j0_scale(wv + k, 2 * lane + 1, d0a, d0b);
+#pragma unroll 1
+                            for (int q = wv; q < XR; q += NW) {   // (row q uniform per wave)
+                                d2 v = *(const d2*)(xsl + q * TC + 2 * lane);
+                                v[0] *= j0_scale(q, 2 * lane, d0a, d0b);
+                                v[1] *= j0_scale(q, 2 * lane + 1, d0a, d0b);
+                                *(d2*)(xsl + q * TC + 2 * lane) = v;
                             }
                         }
+                        __syncthreads();
                     }
                 }
+                // ---- axis 1: u = F1a x, v = F1b x on this wave's row, 2 columns per lane
+                const double* xs = lds + XS_OFF + (t % D) * XR * TC + 2 * lane;
+                d2 xv[W];
+#pragma unroll
+                for (int k = 0; k < W; ++k) xv[k] = *(const d2*)(xs + (wv + k) * TC);
                 if constexpr (MODE == 1) {
                     const bool ok0 = t >= 2 * P && row_ok && (cok & 1);
                     bstore2_s(ry, ok0 ? (orow + P) * s1 * 8 + colb + (zo_of(t) + g.pd0) * (int)plane8 : 0x7ffffff0,
@@ -463,16 +475,17 @@ kron_v5_kernel(const double* __restrict__ x, double* __restrict__ y, const doubl
                         v[e] = sv;
                     }
                 }
-                if constexpr (J0) {
-                    if (jsc) {   // x1 = s(column) b: the scaling commutes with the axis-1 pass
-                        __asm__ volatile("" ::: "memory");   // (load sc here, not beside the 2P+1 rows)
-                        const d2 sc = *(const d2*)(lds + RS_OFF + 2 * lane);   // (every table row is equal here)
+                if constexpr (J0 && !J0NX) {
+                    // x1 = s(column) b: the scaling commutes with the axis-1 pass (every table
+                    // row is equal on a jsc plane); ones where the ring holds x1 already (x 1.0
+                    // is exact), so that no path merges register copies
+                    const int so = __builtin_amdgcn_readfirstlane(jsc ? RS_OFF : ONE_OFF);
+                    const d2 sc = *(const d2*)(lds + so + 2 * lane);
 #pragma unroll
-                        for (int e = 0; e < 2; ++e) {
-                            u[e] *= sc[e];
-                            v[e] *= sc[e];
-                            xv[P][e] *= sc[e];   // the centre tap the x1 history keeps
-                        }
+                    for (int e = 0; e < 2; ++e) {
+                        u[e] *= sc[e];
+                        v[e] *= sc[e];
+                        xv[P][e] *= sc[e];   // the centre tap the x1 history keeps
                     }
                 }
 
@@ -594,8 +607,12 @@ kron_v5_kernel(const double* __restrict__ x, double* __restrict__ y, const doubl
                         const double dr = fma(-vo[e], sc[e], x1);
                         outv[e] = x1 + dr;
                         if constexpr (!J0NS) {
-                            js[0] = ok[e] ? fma(dr, dr, js[0]) : js[0];   // ||dr_2||^2
-                            js[1] = ok[e] ? fma(x1, x1, js[1]) : js[1];   // ||x1||^2 = ||dr_1||^2
+                            // masked terms as 0 * 0 (the sums are >= 0, so + 0 is exact): two
+                            // selects and a non-destructive fma per sum instead of a copy, an
+                            // fma and two selects
+                            const double drm = ok[e] ? dr : 0.0, x1m = ok[e] ? x1 : 0.0;
+                            js[0] = fma(drm, drm, js[0]);   // ||dr_2||^2
+                            js[1] = fma(x1m, x1m, js[1]);   // ||x1||^2 = ||dr_1||^2
                         }
                     }
                     if constexpr (J0NS) {
@@ -637,7 +654,8 @@ kron_v5_kernel(const double* __restrict__ x, double* __restrict__ y, const doubl
                         for (int e = 0; e < 2; ++e) {
                             const double dr = (bv[e] - vo[e]) * rc[e];   // rc = omega / diag
                             outv[e] = xin[e] + dr;
-                            nrm = ok[e] ? fma(dr, dr, nrm) : nrm;
+                            const double drm = ok[e] ? dr : 0.0;   // (nrm >= 0: + 0 * 0 is exact)
+                            nrm = fma(drm, drm, nrm);
                             if constexpr (JDOT) dotp = ok[e] ? fma(outv[e], bv[e], dotp) : dotp;
                         }
                     }
