@@ -479,8 +479,9 @@ kron_v5_kernel(const double* __restrict__ x, double* __restrict__ y, const doubl
                     // x1 = s(column) b: the scaling commutes with the axis-1 pass (every table
                     // row is equal on a jsc plane); ones where the ring holds x1 already (x 1.0
                     // is exact), so that no path merges register copies
-                    const int so = __builtin_amdgcn_readfirstlane(jsc ? RS_OFF : ONE_OFF);
-                    const d2 sc = *(const d2*)(lds + so + 2 * lane);
+                    static_assert(RS_OFF % 2 == 0 && ONE_OFF % 2 == 0, "16-B aligned scale rows");
+                    const int so = __builtin_amdgcn_readfirstlane(jsc ? RS_OFF / 2 : ONE_OFF / 2);
+                    const d2 sc = reinterpret_cast<const d2*>(lds)[so + lane];   // (one 16-B read)
 #pragma unroll
                     for (int e = 0; e < 2; ++e) {
                         u[e] *= sc[e];
