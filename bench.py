@@ -53,6 +53,8 @@ def parse():
                          "of <= 256 cells per axis, whose vectors fit the 256 MB MALL; 0 for the 512^3 headline)")
     ap.add_argument("--coarse", type=int, default=8)
     ap.add_argument("--chunk", type=int, default=0)
+    ap.add_argument("--timing-every", type=int, default=4,
+                    help="HIP events around every n-th Jacobi launch of the timed cycles (roofline.achieved)")
     ap.add_argument("--kron-reps", type=int, default=50, help="timed isolated applies")
     ap.add_argument("--kron-warm", type=int, default=30,
                     help="untimed applies before them: the apply's launch time falls from ~700 to ~530 us over "
@@ -136,9 +138,9 @@ def main():
     for _ in range(args.warmup):
         mg.cycle(bf)
     barrier()
-    # HIP events around every 4th Jacobi launch of the timed region (a host event record
+    # HIP events around every --timing-every-th (default 4th) Jacobi launch of the timed region (a host event record
     # costs a few us: a sample keeps the measured cycle unperturbed)
-    A.timing(True, "jacobi", every=4, reserve=64 * args.steps + 64)
+    A.timing(True, "jacobi", every=args.timing_every, reserve=64 * args.steps + 64)
     t0 = time.perf_counter()
     for _ in range(args.steps):
         x, ipre, ipos = mg.cycle(bf)
