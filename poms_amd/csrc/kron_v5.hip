@@ -326,7 +326,18 @@ kron_v5_kernel(const double* __restrict__ x, double* __restrict__ y, const doubl
     for (int i = 0; i < (HIST ? P : 1); ++i) { hist[i][0] = 0.0; hist[i][1] = 0.0; }
     double nrm = 0.0, dotp = 0.0;
 
-    __syncthreads();  // C2 table visible; no DMA in flight yet
+    // The rings start zeroed (builds with running sums): lane-columns and rows no DMA
+    // fills then hold zeros, every lane's epilogue terms are finite, and the sums can
+    // take every lane of the wave, the lanes that are not output points being zeroed
+    // once after the march (see the epilogues).
+    if constexpr ((JAC || APD || J0) && MODE == 0) {
+        // (x ring, then b and x_in rings: contiguous from XS_OFF)
+        static_assert(BS_OFF == XS_OFF + D * XR * TC && XI_OFF == BS_OFF + (HASB ? NB * T1 * TC : 0), "ring layout");
+        constexpr int NZ = (XI_OFF + (XIN ? 2 * T1 * TC : 0) - XS_OFF) / 2;
+#pragma unroll 1
+        for (int e = tid; e < NZ; e += NW * 64) *(d2*)(lds + XS_OFF + 2 * e) = d2{0.0, 0.0};
+    }
+    __syncthreads();  // C2 table visible, rings zeroed; no DMA in flight yet
     // J0: omega/diag at x-tile row q, lane-column ci, of a plane with axis-0 diagonal
     // entries d0a, d0b (LDS tables only: no VMEM inside the march)
     auto j0_scale = [&](int q, int ci, double d0a, double d0b) {
@@ -583,8 +594,10 @@ kron_v5_kernel(const double* __restrict__ x, double* __restrict__ y, const doubl
                 } else if constexpr (APD) {
                     outv[0] = vo[0];
                     outv[1] = vo[1];
-#pragma unroll
-                    for (int e = 0; e < 2; ++e) dotp = ok[e] ? fma(xin[e], outv[e], dotp) : dotp;
+                    if (en) {   // every lane (the rings start zeroed); see the J0 epilogue below
+                        dotp = fma(xin[0], outv[0], dotp);
+                        dotp = fma((cok & 2) ? xin[1] : 0.0, outv[1], dotp);
+                    }
                 } else if constexpr (J0) {
                     // x1 = s b, x2 = x1 + s (b - A x1) = x1 + (x1 - s A x1), s = omega/diag;
                     // xin = x1 at the output point (the scaled centre tap)
@@ -600,28 +613,35 @@ kron_v5_kernel(const double* __restrict__ x, double* __restrict__ y, const doubl
                         sc[0] = j0_scale(wv + P, 2 * lane, d0a, d0b);
                         sc[1] = j0_scale(wv + P, 2 * lane + 1, d0a, d0b);
                     }
-                    d2 js = {nrm, dotp};
-                    if constexpr (JSL && !J0NS) js = *(const d2*)(lds + JS_OFF + 2 * tid);   // this lane's own slot
+                    double dr[2];
 #pragma unroll
                     for (int e = 0; e < 2; ++e) {
-                        const double x1 = xin[e];
-                        const double dr = fma(-vo[e], sc[e], x1);
-                        outv[e] = x1 + dr;
-                        if constexpr (!J0NS) {
-                            // masked terms as 0 * 0 (the sums are >= 0, so + 0 is exact): two
-                            // selects and a non-destructive fma per sum instead of a copy, an
-                            // fma and two selects
-                            const double drm = ok[e] ? dr : 0.0, x1m = ok[e] ? x1 : 0.0;
-                            js[0] = fma(drm, drm, js[0]);   // ||dr_2||^2
-                            js[1] = fma(x1m, x1m, js[1]);   // ||x1||^2 = ||dr_1||^2
-                        }
+                        dr[e] = fma(-vo[e], sc[e], xin[e]);
+                        outv[e] = xin[e] + dr[e];
                     }
-                    if constexpr (J0NS) {
-                    } else if constexpr (JSL) {
-                        *(d2*)(lds + JS_OFF + 2 * tid) = js;
-                    } else {
-                        nrm = js[0];
-                        dotp = js[1];
+                    // The running sums (||dr_2||^2, ||x1||^2 = ||dr_1||^2) take every lane of the
+                    // wave on the output planes (en: uniform) and the lanes that are not output
+                    // columns, or whose wave's row is past n1, are zeroed once after the march.
+                    // Their terms are finite: the x ring starts zeroed, so the lane-columns no DMA
+                    // fills hold zeros.  Only a lane whose second column lies past n2 (odd n2, the
+                    // last tile column) masks its second terms, as 0 * 0 (the sums are >= 0, so
+                    // + 0 is exact): the same sums, term for term, as masking every term.
+                    if constexpr (!J0NS) {
+                        if (en) {
+                            d2 js = {nrm, dotp};
+                            if constexpr (JSL) js = *(const d2*)(lds + JS_OFF + 2 * tid);   // this lane's own slot
+                            js[0] = fma(dr[0], dr[0], js[0]);
+                            js[1] = fma(xin[0], xin[0], js[1]);
+                            const double dr1 = (cok & 2) ? dr[1] : 0.0, x11 = (cok & 2) ? xin[1] : 0.0;
+                            js[0] = fma(dr1, dr1, js[0]);
+                            js[1] = fma(x11, x11, js[1]);
+                            if constexpr (JSL) {
+                                *(d2*)(lds + JS_OFF + 2 * tid) = js;
+                            } else {
+                                nrm = js[0];
+                                dotp = js[1];
+                            }
+                        }
                     }
                 } else {
                     const d2 bv = *(const d2*)(lds + BS_OFF + ((t % NB) * T1 + wv) * TC + 2 * lane);
@@ -655,9 +675,12 @@ kron_v5_kernel(const double* __restrict__ x, double* __restrict__ y, const doubl
                         for (int e = 0; e < 2; ++e) {
                             const double dr = (bv[e] - vo[e]) * rc[e];   // rc = omega / diag
                             outv[e] = xin[e] + dr;
-                            const double drm = ok[e] ? dr : 0.0;   // (nrm >= 0: + 0 * 0 is exact)
-                            nrm = fma(drm, drm, nrm);
-                            if constexpr (JDOT) dotp = ok[e] ? fma(outv[e], bv[e], dotp) : dotp;
+                            if (en) {   // every lane (the rings start zeroed); see the J0 epilogue
+                                const bool k = e == 0 || (cok & 2);
+                                const double drm = k ? dr : 0.0;   // (nrm >= 0: + 0 * 0 is exact)
+                                nrm = fma(drm, drm, nrm);
+                                if constexpr (JDOT) dotp = fma(k ? outv[e] : 0.0, bv[e], dotp);
+                            }
                         }
                     }
                 }
@@ -688,6 +711,12 @@ kron_v5_kernel(const double* __restrict__ x, double* __restrict__ y, const doubl
         const d2 js = *(const d2*)(lds + JS_OFF + 2 * tid);
         nrm = js[0];
         dotp = js[1];
+    }
+    if constexpr ((JAC || APD || J0) && !J0NS) {   // the lanes whose terms are not output points
+        if (!(row_ok && (cok & 1))) {
+            nrm = 0.0;
+            dotp = 0.0;
+        }
     }
 
     if constexpr (JAC || APD || J0) {
@@ -814,9 +843,8 @@ static int v5_launch_p(int epi, const KronPtrs& p, const KronGeom& g, const Toep
             if (store_policy() == 2) return v5_launch_t<P, EPI_APPLY, 4, 0, 2 | 32>(p, g, tc, H, omega, st);
             return v5_launch_t<P, EPI_APPLY, 4, 0, 6>(p, g, tc, H, omega, st);
         case EPI_RESID: return v5_launch_t<P, EPI_RESID, 3, 0, 6 | 64>(p, g, tc, H, omega, st);
-        case EPI_JACOBI:
-            if (store_policy() == 1) return v5_launch_t<P, EPI_JACOBI, 3, 0, 2 | 16, true>(p, g, tc, H, omega, st);
-            if (store_policy() == 2) return v5_launch_t<P, EPI_JACOBI, 3, 0, 2 | 32, true>(p, g, tc, H, omega, st);
+        case EPI_JACOBI:   // (the sc1 / sc0 sc1 store builds of round 2 no longer fit 128 VGPRs with the
+                           // zeroed rings: POMS_V5_STORE applies to the apply only)
             return v5_launch_t<P, EPI_JACOBI, 4, 0, 6 | 64, true>(p, g, tc, H, omega, st);
         case EPI_APPLYDOT: return v5_launch_t<P, EPI_APPLYDOT, 4, 0, 6>(p, g, tc, H, omega, st);
         // x ring = b (read once, apply's policy), scaled to x1 as it is read; y = x2
