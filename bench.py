@@ -71,9 +71,12 @@ def parse():
                          "when its recorded p and kernel variant are this run's")
     a = ap.parse_args()
     if a.steps is None:
-        a.steps = 3 if a.ndim == 3 else 20
+        a.steps = 3 if a.ndim == 3 else 50
     if a.warmup is None:
-        a.warmup = 1 if a.ndim == 3 else 5
+        # 2D: a cycle takes ~3.5 ms, and 5 untimed cycles left the GPU's clocks / the
+        # host's state short of steady: 3.96-5.84 ms per cycle measured after 5, 3.44-3.59
+        # after 200, on one box (profiles/r04/wu/)
+        a.warmup = 1 if a.ndim == 3 else 200
     if a.cells is None:
         a.cells = 512 if a.ndim == 3 else 1024
     if a.flush_mall is None:   # configs whose working set fits the MALL are flushed

@@ -143,6 +143,8 @@ struct poms_op {
     double* spec_part = nullptr;
     double* spec_dev = nullptr;
     double* spec_host = nullptr;    // kSpecVals, pinned
+    double* la_buf = nullptr;   // the two-sweep lookahead's fourth preconditioner buffer (zero ghosts)
+    int64_t la_n = 0;
     double* spec_bak = nullptr;
     int64_t spec_bak_n = 0;
     struct SpecGraph {   // a captured speculative call (see pcg_speculative)
@@ -559,7 +561,7 @@ int poms_op_stencil_data(poms_op* o, double* data_host) {
 int poms_op_destroy(poms_op* o) {
     if (!o) return 0;
     for (double* p : {o->a0t, o->b0t, o->a1, o->b1, o->a2, o->b2, o->dg2a, o->dg2b, o->rdiag0, o->coef, o->sv_dev,
-                      o->spec_dev, o->spec_bak})
+                      o->spec_dev, o->spec_bak, o->la_buf})
         if (p) (void)hipFree(p);
     for (double* p : {o->sv_host, o->sv_part, o->spec_part, o->spec_host})
         if (p) (void)hipHostFree(p);
@@ -1995,76 +1997,91 @@ struct PcgRun {
         *out = x;
         return 0;
     }
-    // damped_jacobi(A, rhs) with x0 = None into buffers {A, B}; the last sweep also
-    // forms x . rhs into sc[dot_idx] (*dot_done = 1), else the caller forms it.
-    int damped_jacobi(const double* rhs, double* A, double* B, int dot_idx, double** out, int* dot_done) {
+    // damped_jacobi(A, rhs) with x0 = None into buffers {A, B} (and C: see below); the
+    // last sweep also forms x . rhs into sc[dot_idx] (*dot_done = 1), else the caller
+    // forms it.  Each sweep's stop test is read after the next sweep is queued -- or,
+    // with a third buffer C (one rank), after the next TWO are queued: the sweeps rotate
+    // over three buffers, so the two queued past a stop that fires (abandoned) cannot
+    // overwrite the result, and the host's turn-around per sweep can take up to two
+    // sweeps' time before the GPU waits.  The same launches and bits either way.
+    int damped_jacobi(const double* rhs, double* A, double* B, int dot_idx, double** out, int* dot_done,
+                      double* C = nullptr) {
         const double tol2 = o->jtol * o->jtol;
         const int maxit = o->jmaxiter;
         *dot_done = 0;
-        double *x = A, *xn = B;
-        int pend = 0;   // 0 none, 1 one sweep norm in host slot pend_h, 2 the from-zero pair in h0
-        int pend_h = H_JN, ring = 0, k0, h0 = H_J0;
+        double* bufs[3] = {A, B, C};
+        const int nb = C ? 3 : 2, depth = C ? 2 : 1;
+        int cur = 0;                         // buffer of the latest queued x
+        struct Pend { int kind, h, buf; };   // 1: sweep norm in slot h; 2: the from-zero pair
+        Pend q[2];
+        int nq = 0, ring = 0, k0;
         int fz = 0;
         if (op->ndim == 3 && maxit >= 2 && maxit != 2 && op->form != FORM_STENCIL) (void)poms_op_from_zero_supported(op, &fz);
-        if (fz) {   // sweeps 1, 2 from x = 0 in one pass over rhs
-            h0 = arm(H_J0, 2);
-            if (jrun(EPI_JACOBI0, rhs, A, rhs, true, true, h0)) return 1;   // [||x1||^2, ||dr2||^2]
-            pend = 2;
+        if (fz) {   // sweeps 1, 2 from x = 0 in one pass over rhs: [||x1||^2, ||dr2||^2]
+            const int h0 = arm(H_J0, 2);
+            if (jrun(EPI_JACOBI0, rhs, A, rhs, true, true, h0)) return 1;
+            q[nq++] = Pend{2, h0, 0};
             k0 = 3;
         } else {
             if (maxit < 1) { set_error("pcg: jacobi maxiter < 1"); return 1; }
-            pend_h = arm(H_JN, 1);
-            if (diag_scale_norm(rhs, A, pend_h)) return 1;
-            pend = 1;
+            const int h = arm(H_JN, 1);
+            if (diag_scale_norm(rhs, A, h)) return 1;
+            q[nq++] = Pend{1, h, 0};
             ring = 1;
             k0 = 2;
         }
+        // the oldest open stop test: done with *res when it fires
         auto settle = [&](bool& done, double*& res) {
             done = false;
-            if (pend == 2) {
-                if (get(h0, 0) < tol2) {   // the reference stops after sweep 1: x1 itself
-                    if (poms_op_diag_scale(op, o->omega, rhs, xn, 0, stv)) return 1;
+            const Pend f = q[0];
+            q[0] = q[1];
+            --nq;
+            if (f.kind == 2) {
+                if (get(f.h, 0) < tol2) {   // the reference stops after sweep 1: x1 itself
+                    // (into the buffer the abandoned sweep 3 wrote; queued after every sweep
+                    // that reads it)
+                    double* x1 = bufs[(f.buf + 1) % nb];
+                    if (poms_op_diag_scale(op, o->omega, rhs, x1, 0, stv)) return 1;
                     done = true;
-                    res = xn;
-                } else if (get(h0, 1) < tol2) {
+                    res = x1;
+                } else if (get(f.h, 1) < tol2) {
                     done = true;
-                    res = x;
+                    res = bufs[f.buf];
                 }
-            } else if (pend == 1 && get(pend_h) < tol2) {
+            } else if (get(f.h) < tol2) {
                 done = true;
-                res = x;
+                res = bufs[f.buf];
             }
-            pend = 0;
             return failed ? 1 : 0;
         };
         for (int k = k0; k <= maxit; ++k) {
             const bool last = k == maxit;
+            const int nxt = (cur + 1) % nb;
             int h = -1;
             if (last) {   // the last sweep's norm cannot change the result: x . rhs instead
-                if (run(EPI_JACOBI, x, xn, rhs, nullptr, sc + dot_idx) || allsum(sc + dot_idx, 1)) return 1;
+                if (run(EPI_JACOBI, bufs[cur], bufs[nxt], rhs, nullptr, sc + dot_idx) || allsum(sc + dot_idx, 1)) return 1;
             } else {
                 h = arm(H_JN + ring, 1);
-                if (jrun(EPI_JACOBI, x, xn, rhs, true, false, h)) return 1;
+                if (jrun(EPI_JACOBI, bufs[cur], bufs[nxt], rhs, true, false, h)) return 1;
                 ring ^= 1;
             }
-            if (pend) {   // stop test of the previous sweep, read after this one is queued
+            cur = nxt;
+            if (nq == depth) {   // the test of the sweep `depth` back, read after this one is queued
                 bool done;
                 double* res = nullptr;
                 if (settle(done, res)) return 1;
                 if (done) { *out = res; return 0; }
             }
-            std::swap(x, xn);
-            if (last) { *dot_done = 1; break; }
-            pend = 1;
-            pend_h = h;
+            if (!last) q[nq++] = Pend{1, h, cur};
         }
-        if (pend == 2) {   // maxiter == 2 from zero: sweep 1's test still open
+        while (nq > 0) {   // tests still open after the last sweep (its own has none)
             bool done;
             double* res = nullptr;
             if (settle(done, res)) return 1;
             if (done) { *out = res; return 0; }
         }
-        *out = x;
+        *dot_done = k0 <= maxit ? 1 : 0;
+        *out = bufs[cur];
         return 0;
     }
 };
@@ -2310,15 +2327,40 @@ int poms_pcg_jacobi(poms_op* op, poms_comm* comm, const poms_pcg_opts* o, const 
     }
     const double nrmr0 = std::sqrt(R.get(hrr0));
     if (R.failed) return 1;
+    // Two-sweep lookahead in the damped-Jacobi calls (one rank; POMS_PCG_LOOKAHEAD=1 /
+    // 0 forces it on / off, default on for 2D operators, where the host's turn-around
+    // per sweep is close to a sweep's GPU time): a fourth preconditioner buffer
+    double* e4 = nullptr;
+    {
+        const char* le = getenv("POMS_PCG_LOOKAHEAD");
+        const bool la = R.direct() && (le && le[0] ? le[0] == '1' : op->ndim == 2);
+        if (la) {
+            const int64_t nbuf = (int64_t)(op->L.n[0] + 2 * op->L.pads[0]) * row_geom(&op->L).s0;
+            if (op->la_n < nbuf) {
+                if (op->la_buf) POMS_HIP_CHECK(hipFree(op->la_buf));
+                op->la_buf = nullptr;
+                op->la_n = 0;
+                POMS_HIP_CHECK(hipMalloc(reinterpret_cast<void**>(&op->la_buf), nbuf * sizeof(double)));
+                POMS_HIP_CHECK(hipMemsetAsync(op->la_buf, 0, nbuf * sizeof(double), R.st));   // zero ghosts
+                op->la_n = nbuf;
+            }
+            e4 = op->la_buf;
+        }
+    }
     double* s = nullptr;
     int dd = 0;
-    if (R.damped_jacobi(r, z[0], z[1], SC_SR, &s, &dd)) return 1;
+    if (R.damped_jacobi(r, z[0], z[1], SC_SR, &s, &dd, e4)) return 1;
     if (!dd && R.dot(s, r, R.sc + SC_SR)) return 1;
-    double* p = s;   // p keeps this buffer; later psolves use the other two
-    double* fa = nullptr;
-    double* fb = nullptr;
-    for (double* c : z)
-        if (c != p) (fa ? fb : fa) = c;
+    double* p = s;   // p keeps this buffer; later psolves use the others
+    double* fp[3] = {nullptr, nullptr, nullptr};
+    {
+        int nf = 0;
+        for (double* c : {z[0], z[1], z[2], e4})
+            if (c && c != p) fp[nf++] = c;
+    }
+    double* fa = fp[0];
+    double* fb = fp[1];
+    double* fc = fp[2];   // (nullptr without the lookahead)
     int k = 0;
     double nrmr = nrmr0 * nrmr0;
     for (k = 1; k <= o->maxiter; ++k) {
@@ -2329,7 +2371,7 @@ int poms_pcg_jacobi(poms_op* op, poms_comm* comm, const poms_pcg_opts* o, const 
         if (!drr || poms_pcg_r_update_dev(ctx, L, R.sc + SC_ALPHA, r, q, drr, stream) || R.lazy_post(hrr, 1))
             return 1;
         double* sn = nullptr;
-        if (R.damped_jacobi(r, fa, fb, SC_SRN, &sn, &dd)) return 1;   // queued before the read
+        if (R.damped_jacobi(r, fa, fb, SC_SRN, &sn, &dd, fc)) return 1;   // queued before the read
         if (!dd && R.dot(sn, r, R.sc + SC_SRN)) return 1;
         nrmr = R.get(hrr);
         if (R.failed) return 1;

@@ -336,9 +336,13 @@ def test_damped_jacobi_maxiter2_stops_after_sweep1(gpu, ndim, N, p):
     (3, 128, 3, 1e-10, False, 1e-6, 3),
     (3, 96, 3, 1e-7, True, 1e-6, 4),
 ])
-def test_native_pcg_matches_python_loop(gpu, monkeypatch, ndim, N, p, scale, x0, tol, maxiter):
+@pytest.mark.parametrize("lookahead", ["0", "1"])
+def test_native_pcg_matches_python_loop(gpu, monkeypatch, lookahead, ndim, N, p, scale, x0, tol, maxiter):
     """poms_pcg_jacobi (the whole pcg + damped-Jacobi loop in C) == the Python device
-    loop, bitwise: same launches, same device scalars, same stop decisions."""
+    loop, bitwise: same launches, same device scalars, same stop decisions -- with the
+    stop tests read one sweep late, and two sweeps late over a fourth buffer
+    (POMS_PCG_LOOKAHEAD=1: up to two abandoned sweeps past an early stop)."""
+    monkeypatch.setenv("POMS_PCG_LOOKAHEAD", lookahead)
     from poms_amd import solvers
     from poms_amd.stencil import KronOperator, StencilVectorSpace
     M, K = assemble_1d(uniform_knots(p, N), p)
