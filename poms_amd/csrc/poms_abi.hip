@@ -1717,6 +1717,22 @@ __global__ void pcg_scalars_kernel(double* sc, int mode) {
     }
 }
 
+// p.q from the apply + dot launch's per-block partials -- reduce_partials_kernel's
+// order, so the same bits -- and alpha from it, in one launch (one rank: saves the
+// one-block reduction launch per pcg iteration)
+__global__ void __launch_bounds__(256) pcg_alpha_kernel(const double* __restrict__ part, int count, double* sc) {
+    __shared__ double red[4];
+    double s = 0.0;
+    for (int i = threadIdx.x; i < count; i += 256) s += part[i];
+    const double pq = block_sum_256(s, red);
+    if (threadIdx.x != 0) return;
+    sc[SC_PQ] = pq;
+    const double a = sc[SC_SR] / pq;
+    sc[SC_ONE] = 1.0;
+    sc[SC_ALPHA] = a;
+    sc[SC_ALPHA2] = a;
+}
+
 struct PcgRun {
     poms_op* op;
     poms_comm* comm;
@@ -1736,6 +1752,20 @@ struct PcgRun {
                                     dot, 0, nullptr, &tk, stv);
         }
         return poms_op_run_reduce2(op, epi, o->omega, x, y, b, 0, n0, 0, 0, nrm, dot, 0, stv);
+    }
+    // q = A p, p.q and alpha: one rank folds p.q's reduction into the alpha kernel
+    int apd_alpha(const double* p, double* q) {
+        if (comm || op->dot_base >= 0 || op->part_off != 0 || op->part_dst || op->form == FORM_STENCIL) {
+            if (run(EPI_APPLYDOT, p, q, p, nullptr, sc + SC_PQ) || allsum(sc + SC_PQ, 1)) return 1;
+            hipLaunchKernelGGL(pcg_scalars_kernel, dim3(1), dim3(64), 0, st, sc, 0);
+            POMS_HIP_CHECK(hipGetLastError());
+            return 0;
+        }
+        if (op_run_epi(op, EPI_APPLYDOT, o->omega, p, q, p, 0, n0, 0, 0, false, true, stv)) return 1;
+        const int64_t n = op->last_partials;   // (the dot's partials at scratch + n, as poms_op_run_reduce2 reads them)
+        hipLaunchKernelGGL(pcg_alpha_kernel, dim3(1), dim3(256), 0, st, op->ctx->scratch + n, (int)n, sc);
+        POMS_HIP_CHECK(hipGetLastError());
+        return 0;
     }
     int tk[poms_op::kSvRing] = {};   // with a communicator: the ring ticket of host slot h
     // a sum the device needs (alpha, beta): all-reduced, the compute stream waits
@@ -2364,8 +2394,7 @@ int poms_pcg_jacobi(poms_op* op, poms_comm* comm, const poms_pcg_opts* o, const 
     int k = 0;
     double nrmr = nrmr0 * nrmr0;
     for (k = 1; k <= o->maxiter; ++k) {
-        if (R.run(EPI_APPLYDOT, p, q, p, nullptr, R.sc + SC_PQ) || R.allsum(R.sc + SC_PQ, 1)) return 1;
-        hipLaunchKernelGGL(pcg_scalars_kernel, dim3(1), dim3(64), 0, R.st, R.sc, 0);
+        if (R.apd_alpha(p, q)) return 1;
         const int hrr = R.arm(H_RR, 1);
         double* drr = R.hslot(hrr);
         if (!drr || poms_pcg_r_update_dev(ctx, L, R.sc + SC_ALPHA, r, q, drr, stream) || R.lazy_post(hrr, 1))
