@@ -39,6 +39,7 @@ int vec_flat_launch(int op, int64_t count, double a, double b, const double* x, 
                     double* z, double* w, const double* q, double* partial, hipStream_t st,
                     int* nblk_out, const double* ab = nullptr);
 int zero_ghosts_launch(const RowGeom& g, double* z, hipStream_t st);
+int diag_scale_blocks(bool is3d, const RowGeom& g);
 int diag_scale_launch(bool is3d, int form, const RowGeom& g, int P, int g0, double scale,
                       const double* b, double* x, const double* a0t, const double* b0t,
                       const double* a1, const double* b1, const double* a2, const double* b2,
@@ -1946,6 +1947,22 @@ struct PcgRun {
         return allsum(dst, 1);
     }
     int diag_scale_norm(const double* b, double* x, int h) {   // x = omega b / diag, ||x||^2 -> host slot h
+        if (direct() && op->form != FORM_STENCIL) {   // partials straight into slot h's host region
+            const RowGeom g = row_geom(&op->L);
+            const int nb = diag_scale_blocks(op->ndim == 3, g);
+            if (nb <= host_partials_max()) {
+                int nl = 0;
+                diag_scale_launch(op->ndim == 3, op->form, g, op->pmax, (int)op->g0, o->omega, b, x, op->a0t,
+                                  op->b0t, op->a1, op->b1, op->dg2a, op->dg2b,
+                                  op->sv_part + (size_t)h * poms_op::kSvPart, st, &nl);
+                POMS_HIP_CHECK(hipGetLastError());
+                if (nl != nb) { set_error("diag scale: block count mismatch"); return 1; }
+                op->last_partials = nb;
+                op->sv_npart[h] = nb;
+                op->sv_pkind[h] = 1;
+                return 0;
+            }
+        }
         if (poms_op_diag_scale(op, o->omega, b, x, 1, stv)) return 1;
         double* d = hslot(h);
         if (!d) return 1;
