@@ -1946,6 +1946,32 @@ struct PcgRun {
         if (poms_vec_dot(op->ctx, &op->L, a, b, dst, stv)) return 1;
         return allsum(dst, 1);
     }
+    // r -= alpha q, r.r -> host slot h.  One rank: the flat kernel writes its per-block
+    // partials straight into the slot's host region (the host adds them in the order
+    // of the device reduction it replaces, so the same bits) -- one launch less per
+    // pcg iteration
+    int rupd(double* r, const double* q, int h) {
+        if (direct() && !(op->L.flags & POMS_LAYOUT_GHOST_DATA)) {
+            const RowGeom g = row_geom(&op->L);
+            const int64_t off = (int64_t)g.pd0 * g.s0, count = (int64_t)g.n0 * g.s0;
+            const int head = (reinterpret_cast<uintptr_t>(r + off) & 15) ? 1 : 0;
+            const int64_t nbp = std::max<int64_t>(1, ((count - head) / 2 + 1023) / 1024);   // (vec_flat_launch's grid, before its cap)
+            if (nbp <= host_partials_max()) {
+                int nb = 0;
+                double* reg = op->sv_part + (size_t)h * poms_op::kSvPart;
+                if (vec_flat_launch(V_RUPD, count, 0.0, 0.0, nullptr, nullptr, nullptr, r + off, q + off, reg, st, &nb,
+                                    sc + SC_ALPHA) == 0) {
+                    POMS_HIP_CHECK(hipGetLastError());
+                    op->sv_npart[h] = nb;
+                    op->sv_pkind[h] = 1;
+                    return 0;
+                }
+            }
+        }
+        double* d = hslot(h);
+        if (!d || poms_pcg_r_update_dev(op->ctx, &op->L, sc + SC_ALPHA, r, q, d, stv) || lazy_post(h, 1)) return 1;
+        return 0;
+    }
     int diag_scale_norm(const double* b, double* x, int h) {   // x = omega b / diag, ||x||^2 -> host slot h
         if (direct() && op->form != FORM_STENCIL) {   // partials straight into slot h's host region
             const RowGeom g = row_geom(&op->L);
@@ -2413,9 +2439,7 @@ int poms_pcg_jacobi(poms_op* op, poms_comm* comm, const poms_pcg_opts* o, const 
     for (k = 1; k <= o->maxiter; ++k) {
         if (R.apd_alpha(p, q)) return 1;
         const int hrr = R.arm(H_RR, 1);
-        double* drr = R.hslot(hrr);
-        if (!drr || poms_pcg_r_update_dev(ctx, L, R.sc + SC_ALPHA, r, q, drr, stream) || R.lazy_post(hrr, 1))
-            return 1;
+        if (R.rupd(r, q, hrr)) return 1;
         double* sn = nullptr;
         if (R.damped_jacobi(r, fa, fb, SC_SRN, &sn, &dd, fc)) return 1;   // queued before the read
         if (!dd && R.dot(sn, r, R.sc + SC_SRN)) return 1;
