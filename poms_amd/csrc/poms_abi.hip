@@ -1734,6 +1734,20 @@ __global__ void __launch_bounds__(256) pcg_alpha_kernel(const double* __restrict
     sc[SC_ALPHA2] = a;
 }
 
+// s.r_new from the last damped-Jacobi sweep's per-block partials (reduce_partials_kernel's
+// order: the same bits), then beta = s.r_new / s.r_old and s.r_old <- s.r_new, in one
+// launch (one rank: saves the one-block reduction launch per pcg iteration)
+__global__ void __launch_bounds__(256) pcg_beta_kernel(const double* __restrict__ part, int count, double* sc) {
+    __shared__ double red[4];
+    double s = 0.0;
+    for (int i = threadIdx.x; i < count; i += 256) s += part[i];
+    const double srn = block_sum_256(s, red);
+    if (threadIdx.x != 0) return;
+    sc[SC_SRN] = srn;
+    sc[SC_BETA] = srn / sc[SC_SR];
+    sc[SC_SR] = srn;
+}
+
 struct PcgRun {
     poms_op* op;
     poms_comm* comm;
@@ -1768,6 +1782,10 @@ struct PcgRun {
         POMS_HIP_CHECK(hipGetLastError());
         return 0;
     }
+    // the last sweep of a psolve left x . rhs as per-block partials (dot_part, dot_part_n
+    // blocks) for pcg_beta_kernel instead of reducing them itself (-1: it did not)
+    const double* dot_part = nullptr;
+    int64_t dot_part_n = -1;
     int tk[poms_op::kSvRing] = {};   // with a communicator: the ring ticket of host slot h
     // a sum the device needs (alpha, beta): all-reduced, the compute stream waits
     int allsum(double* d, int cnt) { return comm ? poms_allreduce_sum(comm, d, cnt, stv, 1) : 0; }
@@ -2132,7 +2150,16 @@ struct PcgRun {
             const int nxt = (cur + 1) % nb;
             int h = -1;
             if (last) {   // the last sweep's norm cannot change the result: x . rhs instead
-                if (run(EPI_JACOBI, bufs[cur], bufs[nxt], rhs, nullptr, sc + dot_idx) || allsum(sc + dot_idx, 1)) return 1;
+                dot_part_n = -1;
+                if (direct() && dot_idx == SC_SRN && op->dot_base < 0 && op->part_off == 0 && !op->part_dst &&
+                    op->form != FORM_STENCIL) {   // its partials wait for pcg_beta_kernel
+                    if (op_run_epi(op, EPI_JACOBI, o->omega, bufs[cur], bufs[nxt], rhs, 0, n0, 0, 0, false, true, stv))
+                        return 1;
+                    dot_part_n = op->last_partials;
+                    dot_part = op->ctx->scratch + dot_part_n;   // (where poms_op_run_reduce2 reads a dot's partials)
+                } else if (run(EPI_JACOBI, bufs[cur], bufs[nxt], rhs, nullptr, sc + dot_idx) || allsum(sc + dot_idx, 1)) {
+                    return 1;
+                }
             } else {
                 h = arm(H_JN + ring, 1);
                 if (jrun(EPI_JACOBI, bufs[cur], bufs[nxt], rhs, true, false, h)) return 1;
@@ -2450,7 +2477,10 @@ int poms_pcg_jacobi(poms_op* op, poms_comm* comm, const poms_pcg_opts* o, const 
             k -= 1;
             break;
         }
-        hipLaunchKernelGGL(pcg_scalars_kernel, dim3(1), dim3(64), 0, R.st, R.sc, 1);
+        if (dd && R.dot_part_n >= 0)   // x . rhs's partials from the last sweep, reduced here
+            hipLaunchKernelGGL(pcg_beta_kernel, dim3(1), dim3(256), 0, R.st, R.dot_part, (int)R.dot_part_n, R.sc);
+        else
+            hipLaunchKernelGGL(pcg_scalars_kernel, dim3(1), dim3(64), 0, R.st, R.sc, 1);
         if (poms_pcg_xp_update_dev(ctx, L, R.sc + SC_ALPHA2, x, p, sn, stream)) return 1;
     }
     if (k > o->maxiter) k = o->maxiter;
