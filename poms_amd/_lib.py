@@ -73,6 +73,7 @@ _SIGS = {
     "poms_op_set_chunk": [_vp, _i],
     "poms_op_set_tile_cols": [_vp, _i],
     "poms_op_set_variant": [_vp, _i],
+    "poms_variant_built": [_i],
     "poms_op_get_variant": [_vp, C.POINTER(_i)],
     "poms_op_kernel_variant": [_vp, _i, C.POINTER(_i)],
     "poms_op_last_variant": [_vp, C.POINTER(_i)],

@@ -44,18 +44,32 @@ def _needs(obj: Path, src: Path) -> bool:
     return any(d.stat().st_mtime > obj.stat().st_mtime for d in deps if d.exists())
 
 
+# v7 (kron_v7.hip, variant 11) is an experimental kernel, slower than v5: the product
+# library compiles only its stubs (variant 11 then runs v5); POMS_WITH_V7=1 builds it.
+WITH_V7 = os.environ.get("POMS_WITH_V7", "0") == "1"
+
+
+def _obj_name(s: str) -> str:
+    return s + (".o" if s != "kron_v7.hip" or not WITH_V7 else ".full.o")
+
+
+def _defines(s: str) -> list[str]:
+    return ["-DPOMS_V7_STUB"] if s == "kron_v7.hip" and not WITH_V7 else []
+
+
 def build(verbose: bool = False, force: bool = False, jobs: int = 4) -> Path:
     hipcc = _hipcc()
     OBJ.mkdir(exist_ok=True)
     todo = []
     for s in SOURCES:
-        src, obj = CSRC / s, OBJ / (s + ".o")
+        src, obj = CSRC / s, OBJ / _obj_name(s)
         if force or _needs(obj, src):
             todo.append((src, obj))
 
     def _compile(pair):
         src, obj = pair
-        cmd = [hipcc, *_flags(), "-I", str(HERE.parent / "include"), "-c", str(src), "-o", str(obj)]
+        cmd = [hipcc, *_flags(), *_defines(src.name), "-I", str(HERE.parent / "include"), "-c", str(src), "-o",
+               str(obj)]
         if verbose:
             print(" ".join(cmd), flush=True)
         r = subprocess.run(cmd, capture_output=True, text=True)
@@ -67,8 +81,10 @@ def build(verbose: bool = False, force: bool = False, jobs: int = 4) -> Path:
         for name in ex.map(_compile, todo):
             if verbose:
                 print(f"compiled {name}", flush=True)
-    objs = [str(OBJ / (s + ".o")) for s in SOURCES]
-    if force or todo or not LIB.exists():
+    objs = [str(OBJ / _obj_name(s)) for s in SOURCES]
+    stamp = OBJ / "link.cfg"   # relink when the set of objects changes (POMS_WITH_V7)
+    cfg = " ".join(objs)
+    if force or todo or not LIB.exists() or not stamp.exists() or stamp.read_text() != cfg:
         tmp = LIB.with_suffix(".so.tmp")
         # librccl.so.1: at run time the one torch already loaded (same SONAME)
         cmd = [hipcc, f"--offload-arch={ARCH}", "-shared", "-fPIC", "-o", str(tmp), *objs,
@@ -77,6 +93,7 @@ def build(verbose: bool = False, force: bool = False, jobs: int = 4) -> Path:
         if r.returncode != 0:
             raise RuntimeError(f"link failed:\n{r.stdout}\n{r.stderr}")
         os.replace(tmp, LIB)
+        stamp.write_text(cfg)
     return LIB
 
 

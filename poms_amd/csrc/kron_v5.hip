@@ -127,6 +127,7 @@ kron_v5_kernel(const double* __restrict__ x, double* __restrict__ y, const doubl
     constexpr bool J0 = (EPI == EPI_JACOBI0);
     constexpr bool HIST = APD || (JAC && XH) || J0;   // x (J0: x1) at the output point from a register history
     constexpr bool XIN = JAC && !XH;            // ... or DMA'd next to b (fewer VGPRs, 8 B/DOF more reads)
+    constexpr bool ZR = J0;                     // zeroed rings + every-lane sums (see below)
     // y stores: nt (bit 4), or sc1 (bit 16: written through, the line is dropped from
     // the XCD's L2 instead of kept -- leaves the L2 to the x halo rows the neighbouring
     // tiles re-read), or sc0 sc1 (bit 32)
@@ -326,11 +327,14 @@ kron_v5_kernel(const double* __restrict__ x, double* __restrict__ y, const doubl
     for (int i = 0; i < (HIST ? P : 1); ++i) { hist[i][0] = 0.0; hist[i][1] = 0.0; }
     double nrm = 0.0, dotp = 0.0;
 
-    // The rings start zeroed (builds with running sums): lane-columns and rows no DMA
-    // fills then hold zeros, every lane's epilogue terms are finite, and the sums can
-    // take every lane of the wave, the lanes that are not output points being zeroed
-    // once after the march (see the epilogues).
-    if constexpr ((JAC || APD || J0) && MODE == 0) {
+    // J0 (ZR): the rings start zeroed, so lane-columns and rows no DMA fills hold
+    // zeros, every lane's epilogue terms are finite, and the two running sums take
+    // every lane of the wave, the lanes that are not output points being zeroed once
+    // after the march (J0 829 -> 816 us, round 4).  The Jacobi sweep and apply + dot
+    // keep the round-3 masked sums: with the zeroed rings the Jacobi build issued 3 %
+    // more VALU and 10.6 % more wave cycles (SQ counters, r03 vs r04), 694.6 -> 709.5 us
+    // in the driver's bench line (round-4 verdict).
+    if constexpr (ZR && MODE == 0) {
         // (x ring, then b and x_in rings: contiguous from XS_OFF)
         static_assert(BS_OFF == XS_OFF + D * XR * TC && XI_OFF == BS_OFF + (HASB ? NB * T1 * TC : 0), "ring layout");
         constexpr int NZ = (XI_OFF + (XIN ? 2 * T1 * TC : 0) - XS_OFF) / 2;
@@ -594,10 +598,8 @@ kron_v5_kernel(const double* __restrict__ x, double* __restrict__ y, const doubl
                 } else if constexpr (APD) {
                     outv[0] = vo[0];
                     outv[1] = vo[1];
-                    if (en) {   // every lane (the rings start zeroed); see the J0 epilogue below
-                        dotp = fma(xin[0], outv[0], dotp);
-                        dotp = fma((cok & 2) ? xin[1] : 0.0, outv[1], dotp);
-                    }
+#pragma unroll
+                    for (int e = 0; e < 2; ++e) dotp = ok[e] ? fma(xin[e], outv[e], dotp) : dotp;
                 } else if constexpr (J0) {
                     // x1 = s b, x2 = x1 + s (b - A x1) = x1 + (x1 - s A x1), s = omega/diag;
                     // xin = x1 at the output point (the scaled centre tap)
@@ -675,12 +677,9 @@ kron_v5_kernel(const double* __restrict__ x, double* __restrict__ y, const doubl
                         for (int e = 0; e < 2; ++e) {
                             const double dr = (bv[e] - vo[e]) * rc[e];   // rc = omega / diag
                             outv[e] = xin[e] + dr;
-                            if (en) {   // every lane (the rings start zeroed); see the J0 epilogue
-                                const bool k = e == 0 || (cok & 2);
-                                const double drm = k ? dr : 0.0;   // (nrm >= 0: + 0 * 0 is exact)
-                                nrm = fma(drm, drm, nrm);
-                                if constexpr (JDOT) dotp = fma(k ? outv[e] : 0.0, bv[e], dotp);
-                            }
+                            const double drm = ok[e] ? dr : 0.0;   // (nrm >= 0: + 0 * 0 is exact)
+                            nrm = fma(drm, drm, nrm);
+                            if constexpr (JDOT) dotp = ok[e] ? fma(outv[e], bv[e], dotp) : dotp;
                         }
                     }
                 }
@@ -712,7 +711,7 @@ kron_v5_kernel(const double* __restrict__ x, double* __restrict__ y, const doubl
         nrm = js[0];
         dotp = js[1];
     }
-    if constexpr ((JAC || APD || J0) && !J0NS) {   // the lanes whose terms are not output points
+    if constexpr (ZR && !J0NS) {   // the lanes whose terms are not output points
         if (!(row_ok && (cok & 1))) {
             nrm = 0.0;
             dotp = 0.0;

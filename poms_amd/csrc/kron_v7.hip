@@ -41,6 +41,9 @@
 
 namespace poms {
 
+#ifndef POMS_V7_STUB   // (the product build compiles this file with POMS_V7_STUB: v7 is an
+                       // experimental variant, slower than v5; POMS_WITH_V7=1 builds it)
+
 typedef __attribute__((address_space(3))) void lds7_void_t;
 
 struct V7Geom {
@@ -798,20 +801,21 @@ int kron_v7_tiles(int pmax, int n1, int n2) {
     return vg.ntiles;
 }
 
+// dry: only check that the build exists and does not spill (0), else 2 -- the caller
+// then runs v5 instead (op_run), as for every other unmet v7 precondition
 template <int P, int EPI, int D, int CN, int CP, bool SAME12, bool JDOT>
 static int v7_launch_t(const KronPtrs& p, const KronGeom& g, const V7Geom& vg, const ToepConst& tc, double omega,
-                       hipStream_t st) {
+                       hipStream_t st, bool dry) {
     // hand-counted vmcnt waits: a build that spills to scratch would break them
     static int scratch = -1;
     if (scratch < 0) {
         hipFuncAttributes at{};
-        if (hipFuncGetAttributes(&at, reinterpret_cast<const void*>(&kron_v7_kernel<P, EPI, D, CN, CP, SAME12, JDOT>)) !=
-            hipSuccess) {
-            set_error("v7: hipFuncGetAttributes failed");
-            return 1;
-        }
-        scratch = (int)at.localSizeBytes;
+        scratch = hipFuncGetAttributes(&at, reinterpret_cast<const void*>(&kron_v7_kernel<P, EPI, D, CN, CP, SAME12, JDOT>)) ==
+                          hipSuccess
+                      ? (int)at.localSizeBytes
+                      : (1 << 30);
     }
+    if (dry) return scratch > 0 ? 2 : 0;
     if (scratch > 0) {
         set_error("v7: kernel build spills to scratch (vmcnt counting invalid)");
         return 1;
@@ -825,15 +829,15 @@ static int v7_launch_t(const KronPtrs& p, const KronGeom& g, const V7Geom& vg, c
 
 template <int P, int EPI, int D, int CP, bool SAME12, bool JDOT>
 static int v7_launch_cn(const KronPtrs& p, const KronGeom& g, const V7Geom& vg, const ToepConst& tc, double omega,
-                        hipStream_t st) {
+                        hipStream_t st, bool dry) {
     switch (vg.cn) {
-        case 0: return v7_launch_t<P, EPI, D, 0, CP, SAME12, JDOT>(p, g, vg, tc, omega, st);
-        case 16: return v7_launch_t<P, EPI, D, 16, CP, SAME12, JDOT>(p, g, vg, tc, omega, st);
-        case 32: return v7_launch_t<P, EPI, D, 32, CP, SAME12, JDOT>(p, g, vg, tc, omega, st);
-        case 48: return v7_launch_t<P, EPI, D, 48, CP, SAME12, JDOT>(p, g, vg, tc, omega, st);
-        case 64: return v7_launch_t<P, EPI, D, 64, CP, SAME12, JDOT>(p, g, vg, tc, omega, st);
-        case 80: return v7_launch_t<P, EPI, D, 80, CP, SAME12, JDOT>(p, g, vg, tc, omega, st);
-        case 96: return v7_launch_t<P, EPI, D, 96, CP, SAME12, JDOT>(p, g, vg, tc, omega, st);
+        case 0: return v7_launch_t<P, EPI, D, 0, CP, SAME12, JDOT>(p, g, vg, tc, omega, st, dry);
+        case 16: return v7_launch_t<P, EPI, D, 16, CP, SAME12, JDOT>(p, g, vg, tc, omega, st, dry);
+        case 32: return v7_launch_t<P, EPI, D, 32, CP, SAME12, JDOT>(p, g, vg, tc, omega, st, dry);
+        case 48: return v7_launch_t<P, EPI, D, 48, CP, SAME12, JDOT>(p, g, vg, tc, omega, st, dry);
+        case 64: return v7_launch_t<P, EPI, D, 64, CP, SAME12, JDOT>(p, g, vg, tc, omega, st, dry);
+        case 80: return v7_launch_t<P, EPI, D, 80, CP, SAME12, JDOT>(p, g, vg, tc, omega, st, dry);
+        case 96: return v7_launch_t<P, EPI, D, 96, CP, SAME12, JDOT>(p, g, vg, tc, omega, st, dry);
     }
     set_error("v7: bad narrow tile width");
     return 1;
@@ -841,16 +845,16 @@ static int v7_launch_cn(const KronPtrs& p, const KronGeom& g, const V7Geom& vg, 
 
 template <int EPI, int CP, bool JDOT>
 static int v7_launch_e(bool same, const KronPtrs& p, const KronGeom& g, const V7Geom& vg, const ToepConst& tc,
-                       double omega, hipStream_t st) {
-    return same ? v7_launch_cn<3, EPI, 4, CP, true, JDOT>(p, g, vg, tc, omega, st)
-                : v7_launch_cn<3, EPI, 4, CP, false, JDOT>(p, g, vg, tc, omega, st);
+                       double omega, hipStream_t st, bool dry) {
+    return same ? v7_launch_cn<3, EPI, 4, CP, true, JDOT>(p, g, vg, tc, omega, st, dry)
+                : v7_launch_cn<3, EPI, 4, CP, false, JDOT>(p, g, vg, tc, omega, st, dry);
 }
 
 // Epilogues built: APPLY, RESID, JACOBI (with / without the fused x_out . b), APPLYDOT.
 // Cache policy (CP): 4 = non-temporal y stores, 2 = non-temporal b loads (both streamed).
 int kron_v7_launch(int pmax, int epi, const KronPtrs& p, const KronGeom& g, const ToepConst& tc, double omega,
-                   hipStream_t st, int diag) {
-    if (pmax != 3) { set_error("v7: p = 3 only"); return 1; }
+                   hipStream_t st, int diag, bool dry) {
+    if (pmax != 3) { if (dry) return 2; set_error("v7: p = 3 only"); return 1; }
     V7Geom vg{};
     v7_plan_p<3>(g.n1, g.n2, &vg);
     if (vg.ntiles <= 0) return 0;
@@ -858,26 +862,43 @@ int kron_v7_launch(int pmax, int epi, const KronPtrs& p, const KronGeom& g, cons
     for (int k = 0; k <= 3; ++k) same = same && tc.t1a[k] == tc.t2a[k] && tc.t1b[k] == tc.t2b[k];
     if (diag) {   // diagnostic / tuning builds (apply): 1 memory only, 2 arithmetic only,
                   // 3 non-temporal x DMAs, 4 y stores with the default policy
-        if (epi != EPI_APPLY || diag > 4) { set_error("v7 diag: apply, modes 1-4"); return 1; }
+        if (epi != EPI_APPLY || diag > 4) { if (dry) return 2; set_error("v7 diag: apply, modes 1-4"); return 1; }
         switch (diag) {
-            case 1: return v7_launch_e<EPI_APPLY, 4 | 256, false>(same, p, g, vg, tc, omega, st);
-            case 2: return v7_launch_e<EPI_APPLY, 4 | 512, false>(same, p, g, vg, tc, omega, st);
-            case 3: return v7_launch_e<EPI_APPLY, 4 | 1, false>(same, p, g, vg, tc, omega, st);
-            default: return v7_launch_e<EPI_APPLY, 0, false>(same, p, g, vg, tc, omega, st);
+            case 1: return v7_launch_e<EPI_APPLY, 4 | 256, false>(same, p, g, vg, tc, omega, st, dry);
+            case 2: return v7_launch_e<EPI_APPLY, 4 | 512, false>(same, p, g, vg, tc, omega, st, dry);
+            case 3: return v7_launch_e<EPI_APPLY, 4 | 1, false>(same, p, g, vg, tc, omega, st, dry);
+            default: return v7_launch_e<EPI_APPLY, 0, false>(same, p, g, vg, tc, omega, st, dry);
         }
     }
     switch (epi) {
-        case EPI_APPLY: return v7_launch_e<EPI_APPLY, 4, false>(same, p, g, vg, tc, omega, st);
-        case EPI_RESID: return v7_launch_e<EPI_RESID, 6, false>(same, p, g, vg, tc, omega, st);
+        case EPI_APPLY: return v7_launch_e<EPI_APPLY, 4, false>(same, p, g, vg, tc, omega, st, dry);
+        case EPI_RESID: return v7_launch_e<EPI_RESID, 6, false>(same, p, g, vg, tc, omega, st, dry);
         case EPI_JACOBI:
             return p.partial2 ? v7_launch_e<EPI_JACOBI, 6, true>(same, p, g, vg, tc, omega, st)
-                              : v7_launch_e<EPI_JACOBI, 6, false>(same, p, g, vg, tc, omega, st);
-        case EPI_APPLYDOT: return v7_launch_e<EPI_APPLYDOT, 4, false>(same, p, g, vg, tc, omega, st);
+                              : v7_launch_e<EPI_JACOBI, 6, false>(same, p, g, vg, tc, omega, st, dry);
+        case EPI_APPLYDOT: return v7_launch_e<EPI_APPLYDOT, 4, false>(same, p, g, vg, tc, omega, st, dry);
         // (EPI_JACOBI0 compiles -- the body has it -- but spills a few VGPRs in the
         // epilogue of the P planes next to each global end; not built until it fits)
     }
+    if (dry) return 2;
     set_error("v7: epilogue not built");
     return 1;
 }
+
+int kron_v7_built() { return 1; }
+
+#else   // POMS_V7_STUB: the product library without the v7 kernels
+
+int kron_v7_tiles(int, int, int) { return 0; }
+
+int kron_v7_launch(int, int, const KronPtrs&, const KronGeom&, const ToepConst&, double, hipStream_t, int, bool dry) {
+    if (dry) return 2;
+    set_error("v7 (variant 11) is not in this build: rebuild with POMS_WITH_V7=1");
+    return 1;
+}
+
+int kron_v7_built() { return 0; }
+
+#endif
 
 }  // namespace poms

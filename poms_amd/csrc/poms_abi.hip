@@ -26,7 +26,8 @@ int kron_v5_launch(int pmax, int epi, const KronPtrs& p, const KronGeom& g, cons
 void kron_v5_tile(int pmax, bool aligned, int* H, int* TO);
 int kron_v5_rows(int pmax, int epi);
 int kron_v7_launch(int pmax, int epi, const KronPtrs& p, const KronGeom& g, const ToepConst& tc, double omega,
-                   hipStream_t st, int diag);
+                   hipStream_t st, int diag, bool dry = false);
+int kron_v7_built();
 int kron_v7_tiles(int pmax, int n1, int n2);
 int kron_tile_rows();
 int kron_tile_cols();
@@ -145,6 +146,8 @@ struct poms_op {
     double* spec_dev = nullptr;
     double* spec_host = nullptr;    // kSpecVals, pinned
     double* la_buf = nullptr;   // the two-sweep lookahead's fourth preconditioner buffer (zero ghosts)
+    double* la_raw = nullptr;   // its allocation: la_buf sits la_off doubles in, on the work vectors' 128-B phase
+    int64_t la_off = -1;
     int64_t la_n = 0;
     double* spec_bak = nullptr;
     int64_t spec_bak_n = 0;
@@ -159,6 +162,7 @@ struct poms_op {
     static constexpr int kSpecGraphs = 4;
     SpecGraph spec_graphs[kSpecGraphs];
     int64_t spec_graph_clock = 0;
+    uint64_t gen = 0;   // bumped by every setter that changes the launches a graph would capture
     int spec_graph_hits = 0, spec_graph_caps = 0;   // graphs stop when captures outnumber hits
     int spec_calls = 0, spec_repeats = 0;            // speculative calls, and those repeated step by step
     hipStream_t cap_stream = nullptr;                 // private non-blocking capture stream
@@ -562,7 +566,7 @@ int poms_op_stencil_data(poms_op* o, double* data_host) {
 int poms_op_destroy(poms_op* o) {
     if (!o) return 0;
     for (double* p : {o->a0t, o->b0t, o->a1, o->b1, o->a2, o->b2, o->dg2a, o->dg2b, o->rdiag0, o->coef, o->sv_dev,
-                      o->spec_dev, o->spec_bak, o->la_buf})
+                      o->spec_dev, o->spec_bak, o->la_raw})
         if (p) (void)hipFree(p);
     for (double* p : {o->sv_host, o->sv_part, o->spec_part, o->spec_host})
         if (p) (void)hipHostFree(p);
@@ -583,10 +587,19 @@ int poms_op_set_variant(poms_op* op, int variant) {
     // sweep streaming the x rows no other tile reads)
     const bool known = variant == 0 || variant == 4 || (variant >= 7 && variant <= 11) ||
                        (variant >= 90 && variant <= 113) || (variant >= 121 && variant <= 124);
-    if (!op || !known) { set_error("poms_op_set_variant: bad argument (0, 4, 7, 8, 9, 10, 11; 90-113 diagnostic)"); return 1; }
+    if (!op || !known) {
+        set_error("poms_op_set_variant: bad argument (0, 4, 7, 8, 9, 10, 11; 90-113 and 121-124 diagnostic)");
+        return 1;
+    }
     if (variant > 0 && !op->v2_ok) { set_error("poms_op_set_variant: variant needs pads == pmax"); return 1; }
     op->variant = variant;
+    ++op->gen;
     return 0;
+}
+
+int poms_variant_built(int variant) {
+    if (variant == 11 || (variant >= 121 && variant <= 124)) return kron_v7_built();
+    return (variant == 0 || variant == 4 || (variant >= 7 && variant <= 10) || (variant >= 90 && variant <= 113)) ? 1 : 0;
 }
 
 int poms_op_kernel_variant(poms_op* op, int epilogue, int* variant) {
@@ -622,12 +635,14 @@ int poms_op_get_variant(poms_op* op, int* variant) {
 int poms_op_set_tile_cols(poms_op* op, int cols) {
     if (!op || cols < 0 || cols > 64 - 2 * op->pmax) { set_error("poms_op_set_tile_cols: bad argument"); return 1; }
     op->tout = cols;
+    ++op->gen;
     return 0;
 }
 
 int poms_op_set_chunk(poms_op* op, int chunk) {
     if (!op || chunk < 0) { set_error("poms_op_set_chunk: bad argument"); return 1; }
     op->chunk = chunk;
+    ++op->gen;
     return 0;
 }
 
@@ -849,6 +864,19 @@ static int op_run(poms_op* o, int epi, double omega, const double* x, double* y,
     int v = resolve_variant(o, epi);
     if (v == 11 && !v7_ok(o, x, y))   // (as resolve_variant would pick for variant 10)
         v = (v5_ok(o) && !(epi == EPI_JACOBI0 && o->pmax == 3 && !same_toeplitz12(o))) ? 10 : 9;
+    if (v == 11 || (v >= 121 && v <= 124)) {
+        // v7 not in this build (the product library compiles it out), or this epilogue's
+        // build spills: run v5 instead, as for any other unmet v7 precondition (a
+        // diagnostic v7 build asked for by number fails loudly)
+        KronGeom g7;
+        if (op_geom(o, zb, ze, g7, 11, 0, zb2, ze2, epi)) return 1;
+        const KronPtrs p7{x, y, b, o->a0t, o->b0t, o->a1, o->b1, o->a2, o->b2, nullptr,
+                          want_dot ? o->ctx->scratch : nullptr, o->rdiag0};
+        if (kron_v7_launch(o->pmax, epi, p7, g7, o->tc, omega, nullptr, v >= 121 ? v - 120 : 0, true) != 0) {
+            if (v >= 121) { set_error("v7 diagnostic build unavailable (not built: POMS_WITH_V7=1, or it spills)"); return 1; }
+            v = (v5_ok(o) && !(epi == EPI_JACOBI0 && o->pmax == 3 && !same_toeplitz12(o))) ? 10 : 9;
+        }
+    }
     const int v5_diag = (v >= 101 && v <= 113) ? v - 100 : 0;   // v5 diagnostic / tuning builds
     if (v5_diag) v = 10;
     const int v7_diag = (v >= 121 && v <= 124) ? v - 120 : 0;   // v7 diagnostic / tuning builds
@@ -983,6 +1011,7 @@ int poms_op_diag_scale(poms_op* o, double scale, const double* b, double* x, int
 int poms_op_set_ghost_corners(poms_op* op, int yes) {
     if (!op) { set_error("poms_op_set_ghost_corners: null operator"); return 1; }
     op->ghost_corners = yes != 0;
+    ++op->gen;
     return 0;
 }
 
@@ -2294,6 +2323,15 @@ static int pcg_speculative(PcgRun& R, const double* b, double* x, int has_x0, do
     key[11] = (uint64_t)(uint32_t)op->variant | ((uint64_t)(uint32_t)op->chunk << 32);
     key[12] = (uint64_t)(op->timing ? 1 : 0) | ((uint64_t)(uint32_t)op->t_epi << 8) | ((uint64_t)(uint32_t)op->t_every << 32);
     key[13] = (uint64_t)(uintptr_t)R.comm | ((uint64_t)(uint32_t)(o->prev + 1) << 48) | ((uint64_t)(uint32_t)(o->next + 1) << 56);
+    {   // whatever else changes the captured launches: the setters' generation, the tile
+        // geometry and ghost corners, the partials layout, and the env knobs read per launch
+        const char* hp = getenv("POMS_HOST_PARTIALS");
+        const char* la = getenv("POMS_PCG_LOOKAHEAD");
+        key[14] = op->gen ^ ((uint64_t)(uint32_t)op->tout << 20) ^ ((uint64_t)(op->ghost_corners ? 1 : 0) << 52) ^
+                  ((uint64_t)(uint32_t)(hp ? atoi(hp) + 1 : 0) << 40);
+        key[15] = (uint64_t)(uint32_t)(op->dot_base + 1) ^ ((uint64_t)(uint32_t)op->part_off << 32) ^
+                  ((uint64_t)(la && la[0] ? la[0] : 0) << 56);
+    }
     poms_op::SpecGraph* hit = nullptr;
     for (auto& g : op->spec_graphs)
         if (g.exec && std::memcmp(g.key, key, sizeof(key)) == 0) hit = &g;
@@ -2320,15 +2358,26 @@ static int pcg_speculative(PcgRun& R, const double* b, double* x, int has_x0, do
         R.st = cst;
         R.stv = cstv;
         ++op->spec_graph_caps;
-        if (rc || ce != hipSuccess) {
-            if (gr) (void)hipGraphDestroy(gr);
-            if (!rc) set_error(std::string("pcg graph capture: ") + hipGetErrorString(ce));
-            return 1;
-        }
         hipGraphExec_t ex = nullptr;
-        const hipError_t ie = hipGraphInstantiate(&ex, gr, nullptr, nullptr, 0);
-        (void)hipGraphDestroy(gr);
-        if (ie != hipSuccess) { set_error(std::string("pcg graph instantiate: ") + hipGetErrorString(ie)); return 1; }
+        hipError_t ie = hipSuccess;
+        if (!rc && ce == hipSuccess) ie = hipGraphInstantiate(&ex, gr, nullptr, nullptr, 0);
+        if (gr) (void)hipGraphDestroy(gr);
+        if (rc || ce != hipSuccess || ie != hipSuccess) {
+            // Nothing captured ran.  Clear the sticky error and run the call uncaptured on
+            // the caller's stream (advisor, round 4: a capture or instantiate failure used
+            // to fail the whole poms_pcg_jacobi call); graphs are off for this operator
+            // from now on.
+            (void)hipGetLastError();
+            op->spec_graph_caps += 1 << 20;
+            R.sparts.clear();
+            R.schk.clear();
+            R.srr.clear();
+            R.scur = 0;
+            R.sn = 0;
+            int vrr0u = 0;
+            if (spec_issue(R, b, x, has_x0, work, &vrr0u)) return 1;
+            return spec_finish(R, vrr0u, info);
+        }
         std::memcpy(slot->key, key, sizeof(key));
         slot->exec = ex;
         slot->parts = R.sparts;
@@ -2349,9 +2398,6 @@ static int pcg_speculative(PcgRun& R, const double* b, double* x, int has_x0, do
     return spec_finish(R, hit->vrr0, info);
 }
 
-// Speculative mode: POMS_PCG_SPEC=1 always, 0 never; by default when a sweep is short
-// (< 32 M local DOF: the 2D grids, the 8-GPU slabs), where the host's turn-around per
-// sweep, not the GPU, set the pace of the step-by-step loop.
 // Speculative mode is opt-in (POMS_PCG_SPEC=1): on the 2D 1024^2 cycle, measured in one
 // process against the step-by-step loop, it costs 3.8 ms per cycle vs 3.1 (graph replay
 // included; profiles/r04/graph): the stream drain it needs at the end of every call
@@ -2435,14 +2481,24 @@ int poms_pcg_jacobi(poms_op* op, poms_comm* comm, const poms_pcg_opts* o, const 
         const char* le = getenv("POMS_PCG_LOOKAHEAD");
         const bool la = R.direct() && (le && le[0] ? le[0] == '1' : op->ndim == 2);
         if (la) {
+            // The buffer takes the work vectors' 16-B / 128-B phase (they start `shift`
+            // doubles into their allocation on the line-aligned layout): the flat vector
+            // kernels and v5's aligned tiles then run on it exactly as on the other three
+            // buffers, with the same block split of the sums (advisor, round 4).
             const int64_t nbuf = (int64_t)(op->L.n[0] + 2 * op->L.pads[0]) * row_geom(&op->L).s0;
+            const int64_t off = (int64_t)((reinterpret_cast<uintptr_t>(work[2]) & 127) / sizeof(double));
             if (op->la_n < nbuf) {
-                if (op->la_buf) POMS_HIP_CHECK(hipFree(op->la_buf));
-                op->la_buf = nullptr;
+                if (op->la_raw) POMS_HIP_CHECK(hipFree(op->la_raw));
+                op->la_raw = op->la_buf = nullptr;
                 op->la_n = 0;
-                POMS_HIP_CHECK(hipMalloc(reinterpret_cast<void**>(&op->la_buf), nbuf * sizeof(double)));
-                POMS_HIP_CHECK(hipMemsetAsync(op->la_buf, 0, nbuf * sizeof(double), R.st));   // zero ghosts
+                POMS_HIP_CHECK(hipMalloc(reinterpret_cast<void**>(&op->la_raw), (nbuf + 16) * sizeof(double)));
                 op->la_n = nbuf;
+                op->la_off = -1;
+            }
+            if (op->la_off != off) {   // (re-)placed: zero ghosts
+                POMS_HIP_CHECK(hipMemsetAsync(op->la_raw, 0, (nbuf + 16) * sizeof(double), R.st));
+                op->la_off = off;
+                op->la_buf = op->la_raw + off;
             }
             e4 = op->la_buf;
         }

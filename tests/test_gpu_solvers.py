@@ -364,6 +364,41 @@ def test_native_pcg_matches_python_loop(gpu, monkeypatch, lookahead, ndim, N, p,
     assert out["1"][1]["res_norm"] == out["0"][1]["res_norm"]
 
 
+@pytest.mark.parametrize("ndim,N,p,scale,x0,tol,maxiter", [
+    (2, 64, 3, 1.0, False, 1e-6, 10),      # the 2D default (lookahead on)
+    (3, 20, 3, 1.0, True, 1e-6, 10),       # v5 on aligned tiles
+    (3, 16, 2, 1e-5, False, 1e-6, 10),     # damped Jacobi stops early
+    (2, 40, 1, 1e-9, True, 1e-6, 10),
+])
+@pytest.mark.parametrize("lookahead", ["0", "1"])
+def test_native_pcg_matches_python_loop_aligned_layout(gpu, monkeypatch, lookahead, ndim, N, p, scale, x0, tol,
+                                                       maxiter):
+    """The same bitwise check on the V-cycle's line-aligned layout (align=True: the
+    work vectors start `shift` doubles into their buffers).  The lookahead's fourth
+    buffer takes their 128-B phase, so the flat vector kernels and v5's aligned
+    tiles run on it as on the others (advisor, round 4: a raw hipMalloc sent its
+    updates to the per-row fall-back and v5 to its unaligned tiles)."""
+    monkeypatch.setenv("POMS_PCG_LOOKAHEAD", lookahead)
+    from poms_amd import solvers
+    from poms_amd.stencil import KronOperator, StencilVectorSpace
+    M, K = assemble_1d(uniform_knots(p, N), p)
+    n = N + p
+    V = StencilVectorSpace([n] * ndim, [p] * ndim, align=True)
+    A = KronOperator.laplace(V, [M] * ndim, [K] * ndim)
+    rng = np.random.default_rng(N + p + 1)
+    b = V.zeros().from_numpy(scale * rng.standard_normal((n,) * ndim))
+    xi = V.zeros().from_numpy(rng.standard_normal((n,) * ndim)) if x0 else None
+    assert solvers._native_ok(A, V)
+    out = {}
+    for native in ("0", "1"):
+        monkeypatch.setenv("POMS_NATIVE_PCG", native)
+        x, info = solvers.pcg(A, solvers.damped_jacobi, b, x0=xi, tol=tol, maxiter=maxiter)
+        out[native] = (x.to_local_numpy(), info)
+    np.testing.assert_array_equal(out["1"][0], out["0"][0])
+    for k in ("niter", "success", "res_norm"):
+        assert out["1"][1][k] == out["0"][1][k], k
+
+
 @pytest.mark.parametrize("cap", ["0", "16"])
 @pytest.mark.parametrize("ndim,N,p,scale", [(3, 20, 3, 1.0), (2, 64, 3, 1.0), (3, 16, 2, 1e-5)])
 def test_native_pcg_device_reduction_fallback(gpu, monkeypatch, cap, ndim, N, p, scale):

@@ -13,9 +13,15 @@ import numpy as np
 import pytest
 
 from oracle import poms_oracle as orc
+from poms_amd import _lib
 from poms_amd.splines import assemble_1d, uniform_knots
 
 pytestmark = pytest.mark.gpu
+
+# v7 is compiled only with POMS_WITH_V7=1 (experimental, slower than v5); without it
+# variant 11 runs v5 (test_v7_absent_runs_v5)
+V7_BUILT = bool(_lib.lib.poms_variant_built(11))
+needs_v7 = pytest.mark.skipif(not V7_BUILT, reason="v7 not in this build (POMS_WITH_V7=1 builds it)")
 
 TOL = 1e-13
 
@@ -46,6 +52,7 @@ def _op(n0, N1, N2, align=True):
     return V, KronOperator.laplace(V, Ms, Ks), Ms, Ks, npts
 
 
+@needs_v7
 @pytest.mark.parametrize("n0,N1,N2", [
     (20, 221, 221),    # 224 x 224: two wide tiles, no narrow column
     (17, 208, 208),    # 211: the remainder (99) takes a whole wide tile
@@ -78,6 +85,7 @@ def test_v7_apply_matches_v5_bitwise_and_oracle(gpu, n0, N1, N2):
     assert not bool(rest.any())
 
 
+@needs_v7
 @pytest.mark.parametrize("n0,N1,N2", [(20, 221, 221), (12, 224, 224), (9, 300, 512), (25, 77, 150), (30, 37, 37)])
 def test_v7_epilogues_match_v5(gpu, n0, N1, N2):
     """Residual, Jacobi sweep (norm, and the fused x_out . b), apply + x.Ax: the
@@ -125,6 +133,7 @@ def test_v7_unaligned_layout_falls_back(gpu):
     assert rel(y, orc.kron_sum_apply(x, Ms, Ks)) <= TOL
 
 
+@needs_v7
 def test_v7_headline_grid_matches_v5(gpu):
     """515^3 (the bench grid, 5 tile columns: 4 x 112 + 80): v7 == v5 bitwise on a
     random input, with several axis-0 chunk lengths (chunk boundaries move)."""
@@ -148,3 +157,19 @@ def test_v7_headline_grid_matches_v5(gpu):
         assert A.last_variant == 11
         assert bool(torch.equal(V.interior(y7._data), V.interior(y5._data))), f"chunk {ch}"
     A.set_chunk(0)
+
+
+@pytest.mark.skipif(V7_BUILT, reason="v7 is built")
+def test_v7_absent_runs_v5(gpu):
+    """Without v7 in the library, asking for variant 11 runs v5 (last_variant 10) with
+    v5's results; a v7 diagnostic build asked for by number fails loudly."""
+    V, A, _, _, npts = _op(20, 40, 131)
+    x = V.zeros().from_numpy(np.random.default_rng(5).uniform(-1, 1, npts))
+    y5 = A.dot(x).to_local_numpy()
+    A.set_variant(11)
+    y = A.dot(x).to_local_numpy()
+    assert A.last_variant == 10
+    assert np.array_equal(y, y5)
+    A.set_variant(121)
+    with pytest.raises(_lib.PomsError):
+        A.dot(x)
