@@ -147,14 +147,20 @@ int poms_op_set_tile_cols(poms_op* op, int cols);
  *       elsewhere it runs v5 -- poms_op_last_variant tells which ran).  v7 is
  *       experimental (slower than v5) and compiled only with POMS_WITH_V7=1;
  *       without it variant 11 runs v5 (poms_variant_built(11) == 0);
- *  90-113 = diagnostic / tuning builds (memory-only, compute-only, cache policies;
- *  110-112: two sweeps from zero without sums / x1 scaling, timing only);
+ *  90-114 = diagnostic / tuning builds (memory-only, compute-only, cache policies;
+ *  110-112: two sweeps from zero without sums / x1 scaling, timing only; 114:
+ *  clock-stamped apply / Jacobi sweep, poms_diag_v5_stamps);
  *  121-124 = v7 memory only / arithmetic only (timing only) / non-temporal x
  *  DMAs / y stores with the default cache policy.
  * Variants 4-11 need storage pads == pmax on every used axis.                  */
 int poms_op_set_variant(poms_op* op, int variant);
 /* 1 if the kernels of `variant` are compiled into this library, else 0 (11: v7). */
 int poms_variant_built(int variant);
+/* Diagnostic: the per-wave clock stamps of the last v5 stamped launches (variant
+ * 114, p = 3 apply / Jacobi sweep): n u64, 8 per wave in launch order (block x
+ * waves + wave): cycles waiting for the wave's DMAs, in the plane barrier, the
+ * rest; planes; start / end (100 MHz); XCC; CU.  The buffer is cleared after.   */
+int poms_diag_v5_stamps(uint64_t* host_out, int64_t n);
 /* Declare that the ghost edges / corners of axes 1 and 2 may hold non-zero data:
  * the vector is a block of a decomposition of axes 1 and 2 (spl Cart,
  * `sources/tests/test_kron_dot.py:51-55`), not an axis-0 slab whose ghosts off

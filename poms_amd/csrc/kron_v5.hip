@@ -39,10 +39,20 @@
 #include "common.hpp"
 
 #include <cstdlib>
+#include <vector>
 
 namespace poms {
 
 typedef __attribute__((address_space(3))) void lds5_void_t;
+
+// MODE 6 (diagnostic, apply / Jacobi): per-wave clock stamps of the march.  Per wave,
+// 8 u64: [0] cycles waiting for its own DMAs (s_waitcnt vmcnt), [1] in the plane
+// barrier, [2] the rest (DMA issue, arithmetic, store), [3] planes, [4] start and
+// [5] end (s_memrealtime, 100 MHz), [6] XCC id, [7] CU id.  s_memtime reads the
+// shader clock (a scalar READ; nothing is stored through the scalar cache); the
+// stamps go out by vector stores.
+constexpr int kV5Stamps = 1 << 19;   // u64 entries: 65536 waves
+__device__ unsigned long long g_v5_stamps[kV5Stamps];
 
 template <int AUX = 0>   // cache policy (gfx950: bit 1 = nt, streaming)
 __device__ __forceinline__ void dma16s(__amdgpu_buffer_rsrc_t r, double* lds_dst, int voff, unsigned soff) {
@@ -326,6 +336,12 @@ kron_v5_kernel(const double* __restrict__ x, double* __restrict__ y, const doubl
 #pragma unroll
     for (int i = 0; i < (HIST ? P : 1); ++i) { hist[i][0] = 0.0; hist[i][1] = 0.0; }
     double nrm = 0.0, dotp = 0.0;
+    constexpr bool STAMP = MODE == 6;
+    unsigned long long st_wait = 0, st_bar = 0, st_rest = 0, st_prev = 0, st_t0 = 0;
+    if constexpr (STAMP) {
+        st_t0 = __builtin_amdgcn_s_memrealtime();
+        st_prev = __builtin_amdgcn_s_memtime();
+    }
 
     // J0 (ZR): the rings start zeroed, so lane-columns and rows no DMA fills hold
     // zeros, every lane's epilogue terms are finite, and the two running sums take
@@ -380,6 +396,11 @@ kron_v5_kernel(const double* __restrict__ x, double* __restrict__ y, const doubl
         for (int q = 0; q < NS; ++q) {
             const int t = tb + q;
             if (t < nplanes) {
+                unsigned long long st_a = 0;
+                if constexpr (STAMP) {
+                    st_a = __builtin_amdgcn_s_memtime();
+                    st_rest += st_a - st_prev;
+                }
                 // ---- x(t) (and b(t)) landed: own DMAs by vmcnt, everyone's by the barrier.
                 // Per iteration each wave issues, in order: b(t+1) [x_in(t+1)], x(t+PFX) (1 or
                 // 2), 1 store.  Loads return in order, but a store may be acknowledged
@@ -401,7 +422,16 @@ kron_v5_kernel(const double* __restrict__ x, double* __restrict__ y, const doubl
                     else if (xtra) v5_wait_vm<(PFX - 1) * NXM>();
                     else v5_wait_vm<(PFX - 1) * (NXM - 1)>();
                 }
+                unsigned long long st_b = 0;
+                if constexpr (STAMP) {
+                    st_b = __builtin_amdgcn_s_memtime();
+                    st_wait += st_b - st_a;
+                }
                 v5_barrier();
+                if constexpr (STAMP) {
+                    st_prev = __builtin_amdgcn_s_memtime();
+                    st_bar += st_prev - st_b;
+                }
                 if constexpr (B3) {
                     dma_x(t + PFX < nplanes ? z0 - P + t + PFX : -(1 << 20), (t + PFX) % D);
                     dma_b(min(zo_of(t + 2), z1), (t + 2) % 3);   // (clamped: the plane past the chunk is a dummy)
@@ -706,6 +736,22 @@ kron_v5_kernel(const double* __restrict__ x, double* __restrict__ y, const doubl
         }
     }
     v5_wait_vm<0>();  // no LDS-DMA may outlive the workgroup
+    if constexpr (STAMP) {
+        st_rest += __builtin_amdgcn_s_memtime() - st_prev;
+        const unsigned long long t1 = __builtin_amdgcn_s_memrealtime();
+        const int slot = (blockIdx.x * NW + wv) * 8;
+        if (lane < 8 && slot + 8 <= kV5Stamps) {
+            unsigned hw;
+            __asm__ volatile("s_getreg_b32 %0, hwreg(HW_REG_HW_ID)" : "=s"(hw));
+            unsigned xcc;
+            __asm__ volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(xcc));
+            const unsigned long long v = lane == 0 ? st_wait : lane == 1 ? st_bar : lane == 2 ? st_rest
+                                       : lane == 3 ? (unsigned long long)nplanes : lane == 4 ? st_t0
+                                       : lane == 5 ? t1 : lane == 6 ? (unsigned long long)(xcc & 15)
+                                       : (unsigned long long)(((hw >> 8) & 15) | (((hw >> 13) & 7) << 4));
+            g_v5_stamps[slot + lane] = v;
+        }
+    }
     if constexpr (JSL) {
         const d2 js = *(const d2*)(lds + JS_OFF + 2 * tid);
         nrm = js[0];
@@ -887,6 +933,12 @@ int kron_v5_launch(int pmax, int epi, const KronPtrs& p, const KronGeom& g, cons
                  : diag_mode == 11 ? v5_launch_t<3, EPI_JACOBI0, 4, 4, 14>(p, g, tc, H, omega, st)
                                    : v5_launch_t<3, EPI_JACOBI0, 4, 5, 14>(p, g, tc, H, omega, st);
         }
+        if (diag_mode == 14) {   // stamped march (MODE 6): apply, or the Jacobi sweep's production build
+            if (epi == EPI_APPLY) return v5_launch_t<3, EPI_APPLY, 4, 6, 6>(p, g, tc, H, omega, st);
+            if (epi == EPI_JACOBI) return v5_launch_t<3, EPI_JACOBI, 4, 6, 6 | 64, true>(p, g, tc, H, omega, st);
+            set_error("v5 diag mode 14: apply / Jacobi only");
+            return 1;
+        }
         if (diag_mode <= 2) {   // 1 = memory only, 2 = arithmetic only (apply)
             if (epi != EPI_APPLY) { set_error("v5 diag mode 1/2: apply only"); return 1; }
             return diag_mode == 1 ? v5_launch_t<3, EPI_APPLY, 4, 1>(p, g, tc, H, omega, st)
@@ -928,5 +980,20 @@ int kron_v5_launch(int pmax, int epi, const KronPtrs& p, const KronGeom& g, cons
 }
 
 int kron_v5_rows(int pmax, int epi) { return v5_waves(pmax, epi); }
+
+// MODE 6 stamps: copy n u64 (<= kV5Stamps) to host (zeroed after the copy)
+int kron_v5_stamps(unsigned long long* host, int64_t n) {
+    if (n < 0 || n > kV5Stamps) { set_error("v5 stamps: bad count"); return 1; }
+    if (hipMemcpyFromSymbol(host, HIP_SYMBOL(g_v5_stamps), n * sizeof(unsigned long long)) != hipSuccess) {
+        set_error("v5 stamps: copy failed");
+        return 1;
+    }
+    std::vector<unsigned long long> z((size_t)n, 0ull);
+    if (hipMemcpyToSymbol(HIP_SYMBOL(g_v5_stamps), z.data(), n * sizeof(unsigned long long)) != hipSuccess) {
+        set_error("v5 stamps: clear failed");
+        return 1;
+    }
+    return 0;
+}
 
 }  // namespace poms

@@ -28,6 +28,7 @@ int kron_v5_rows(int pmax, int epi);
 int kron_v7_launch(int pmax, int epi, const KronPtrs& p, const KronGeom& g, const ToepConst& tc, double omega,
                    hipStream_t st, int diag, bool dry = false);
 int kron_v7_built();
+int kron_v5_stamps(unsigned long long* host, int64_t n);
 int kron_v7_tiles(int pmax, int n1, int n2);
 int kron_tile_rows();
 int kron_tile_cols();
@@ -586,7 +587,7 @@ int poms_op_set_variant(poms_op* op, int variant) {
     // two sweeps from zero without sums / x1 scaling, timing only; 113: the Jacobi
     // sweep streaming the x rows no other tile reads)
     const bool known = variant == 0 || variant == 4 || (variant >= 7 && variant <= 11) ||
-                       (variant >= 90 && variant <= 113) || (variant >= 121 && variant <= 124);
+                       (variant >= 90 && variant <= 114) || (variant >= 121 && variant <= 124);
     if (!op || !known) {
         set_error("poms_op_set_variant: bad argument (0, 4, 7, 8, 9, 10, 11; 90-113 and 121-124 diagnostic)");
         return 1;
@@ -597,9 +598,14 @@ int poms_op_set_variant(poms_op* op, int variant) {
     return 0;
 }
 
+int poms_diag_v5_stamps(uint64_t* host_out, int64_t n) {
+    if (!host_out) { set_error("poms_diag_v5_stamps: null argument"); return 1; }
+    return kron_v5_stamps(reinterpret_cast<unsigned long long*>(host_out), n);
+}
+
 int poms_variant_built(int variant) {
     if (variant == 11 || (variant >= 121 && variant <= 124)) return kron_v7_built();
-    return (variant == 0 || variant == 4 || (variant >= 7 && variant <= 10) || (variant >= 90 && variant <= 113)) ? 1 : 0;
+    return (variant == 0 || variant == 4 || (variant >= 7 && variant <= 10) || (variant >= 90 && variant <= 114)) ? 1 : 0;
 }
 
 int poms_op_kernel_variant(poms_op* op, int epilogue, int* variant) {
@@ -877,7 +883,7 @@ static int op_run(poms_op* o, int epi, double omega, const double* x, double* y,
             v = (v5_ok(o) && !(epi == EPI_JACOBI0 && o->pmax == 3 && !same_toeplitz12(o))) ? 10 : 9;
         }
     }
-    const int v5_diag = (v >= 101 && v <= 113) ? v - 100 : 0;   // v5 diagnostic / tuning builds
+    const int v5_diag = (v >= 101 && v <= 114) ? v - 100 : 0;   // v5 diagnostic / tuning builds
     if (v5_diag) v = 10;
     const int v7_diag = (v >= 121 && v <= 124) ? v - 120 : 0;   // v7 diagnostic / tuning builds
     if (v7_diag) v = v7_ok(o, x, y) && epi == EPI_APPLY ? 11 : -1;

@@ -16,6 +16,8 @@ for rnd in 1 2; do
     grep -o '"kind": "[a-z_]*", "median_us": [0-9.]*' $O/kb_${tag}_$rnd.log | sed "s/^/$tag r$rnd /"
   done
 done
+timeout -k 10 200 python tools/v5_stamps.py --kinds apply,jacobi --reps 4 --json $O/stamps.json > $O/stamps.log 2>&1; rc=$?
+echo "stamps rc=$rc"; cut -c1-400 $O/stamps.log | tail -8; [ $rc -eq 0 ] || stop stamps $rc
 (cd /tmp && timeout -s KILL 120 rocprofv3 --pmc GRBM_GUI_ACTIVE --kernel-trace --output-format csv -d $R/$O/clock -o clk -- \
     python3 $R/tools/kernel_bench.py --rounds 1 --reps 20 --kinds apply,jacobi,from_zero) > $O/clock.log 2>&1
 rc=$?; echo "clock rc=$rc"; [ $rc -eq 0 ] || stop clock $rc

@@ -1,0 +1,102 @@
+#!/usr/bin/env python3
+"""Where the v5 march spends its time: the clock-stamped diagnostic build (variant 114).
+
+Runs the 515^3 p = 3 apply (and the Jacobi sweep) a few times with variant 114 and
+reads the per-wave stamps (poms_diag_v5_stamps): cycles waiting for the wave's own
+DMAs, in the plane barrier, and the rest (DMA issue, arithmetic, store); each wave's
+start / end on the 100 MHz clock, its XCC and CU.  Prints the split, the spread of
+workgroup durations, the per-CU busy time against the launch span, and the tail.
+
+    python tools/v5_stamps.py --cells 512 --kinds apply,jacobi
+"""
+from __future__ import annotations
+
+import argparse
+import ctypes as C
+import json
+import statistics
+import sys
+from pathlib import Path
+
+ROOT = Path(__file__).resolve().parents[1]
+sys.path.insert(0, str(ROOT))
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--cells", type=int, default=512)
+    ap.add_argument("--kinds", default="apply,jacobi")
+    ap.add_argument("--reps", type=int, default=5)
+    ap.add_argument("--json", default="")
+    a = ap.parse_args()
+    import numpy as np
+    import torch
+    from poms_amd import _lib
+    from poms_amd.splines import assemble_1d, uniform_knots
+    from poms_amd.stencil import KronOperator, StencilVectorSpace
+
+    p, N = 3, a.cells
+    M, K = assemble_1d(uniform_knots(p, N), p)
+    n = N + p
+    V = StencilVectorSpace([n] * 3, [p] * 3, align=True)
+    A = KronOperator.laplace(V, [M] * 3, [K] * 3)
+    x, b, y = V.zeros(), V.zeros(), V.zeros()
+    V.interior(x._data).uniform_(-1, 1)
+    V.interior(b._data).uniform_(-1, 1)
+    out = {}
+    for kind in a.kinds.split(","):
+        fn = {"apply": lambda: A.dot(x, out=y),
+              "jacobi": lambda: A.jacobi_sweep(b, x, y, 2.0 / 3.0, want_norm=False)}[kind]
+        A.set_variant(10)
+        for _ in range(3):
+            fn()
+        A.set_variant(114)
+        res = []
+        for r in range(a.reps):
+            torch.cuda.synchronize()
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record()
+            fn()
+            e1.record()
+            torch.cuda.synchronize()
+            assert A.last_variant == 114
+            nw = 1 << 16
+            buf = (C.c_uint64 * (nw * 8))()
+            _lib.call("poms_diag_v5_stamps", C.cast(buf, C.c_void_p), nw * 8)
+            s = np.frombuffer(buf, dtype=np.uint64).reshape(nw, 8).astype(np.float64)
+            s = s[s[:, 3] > 0]   # waves that ran
+            wait, bar, rest, planes, t0, t1, xcc, cu = s.T
+            tot = wait + bar + rest
+            wall_us = e0.elapsed_time(e1) * 1e3
+            # workgroups: 16 waves each, consecutive rows
+            nwg = len(s) // 16
+            wg_t0 = t0[: nwg * 16].reshape(nwg, 16).min(1)
+            wg_t1 = t1[: nwg * 16].reshape(nwg, 16).max(1)
+            span = (wg_t1.max() - wg_t0.min()) / 100.0   # us
+            wg_dur = (wg_t1 - wg_t0) / 100.0
+            cuid = (xcc * 1000 + cu)[: nwg * 16].reshape(nwg, 16)[:, 0]
+            busy = {}
+            for c, d in zip(cuid, wg_dur):
+                busy[c] = busy.get(c, 0.0) + d
+            busyv = np.array(list(busy.values()))
+            row = {"kind": kind, "rep": r, "event_us": wall_us, "span_us": span, "waves": int(len(s)), "wgs": nwg,
+                   "cus_used": len(busy), "frac_wait": float(wait.sum() / tot.sum()),
+                   "frac_barrier": float(bar.sum() / tot.sum()), "frac_rest": float(rest.sum() / tot.sum()),
+                   "cycles_per_plane": float(tot.sum() / planes.sum()),
+                   "wait_per_plane": float(wait.sum() / planes.sum()), "bar_per_plane": float(bar.sum() / planes.sum()),
+                   "rest_per_plane": float(rest.sum() / planes.sum()),
+                   "clock_ghz": float(tot.sum() / ((t1 - t0).sum() / 100.0) / 1e3),
+                   "wg_us_median": float(np.median(wg_dur)), "wg_us_min": float(wg_dur.min()), "wg_us_max": float(wg_dur.max()),
+                   "cu_busy_us_median": float(np.median(busyv)), "cu_busy_us_max": float(busyv.max()),
+                   "cu_busy_us_min": float(busyv.min()), "util": float(busyv.sum() / (len(busy) * span)),
+                   "tail_us": float((wg_t1.max() - np.sort(wg_t1)[int(0.9 * nwg)]) / 100.0)}
+            res.append(row)
+            print(json.dumps({k: (round(v, 4) if isinstance(v, float) else v) for k, v in row.items()}), flush=True)
+        out[kind] = res
+    A.set_variant(8)
+    if a.json:
+        Path(a.json).write_text(json.dumps(out, indent=1))
+
+
+if __name__ == "__main__":
+    main()
