@@ -87,6 +87,21 @@ struct poms_comm {
 
 static hipStream_t cstream(void* s) { return reinterpret_cast<hipStream_t>(s); }
 
+// A call that waits on the host (event / stream synchronisation, a host callback)
+// must not run while `s` is being captured into a graph: nothing captured has run,
+// so it would wait for work that never starts or read values never written.  Such a
+// call fails loudly instead (round-4 verdict: capture of a smoother call with a
+// communicator had crashed with no diagnosis).
+static int refuse_in_capture(hipStream_t s, const char* what) {
+    hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
+    if (hipStreamIsCapturing(s, &cs) != hipSuccess) return 0;
+    if (cs != hipStreamCaptureStatusNone) {
+        ::poms::set_error(std::string(what) + ": host-synchronising call during stream capture");
+        return 1;
+    }
+    return 0;
+}
+
 namespace poms {
 int op_run_split(poms_op* op, int epilogue, double omega, const double* x, double* y, const double* b,
                  int64_t ib, int64_t ie, int64_t b1s, int64_t b1e, int64_t b2s, int64_t b2e, double* norm_out,
@@ -307,6 +322,7 @@ int poms_comm_is_host(poms_comm* c, int* yes) {
 
 // host transport: in-place sum of `count` device doubles through the callback
 static int host_allreduce(poms_comm* c, double* buf, int64_t count, hipStream_t st) {
+    if (refuse_in_capture(st, "host transport all-reduce")) return 1;
     POMS_HIP_CHECK(hipStreamSynchronize(st));
     if (c->stage.size() < (size_t)count) c->stage.resize((size_t)count);
     POMS_HIP_CHECK(hipMemcpy(c->stage.data(), buf, count * sizeof(double), hipMemcpyDeviceToHost));
@@ -351,6 +367,7 @@ int poms_halo_start(poms_comm* c, double* data, int64_t plane_elems, int64_t n_l
     if (width == 0 || (prev < 0 && next < 0)) return 0;
     if (c->host) {   // stage the boundary planes, exchange through the callback, copy back
         hipStream_t st = cstream(stream);
+        if (refuse_in_capture(st, "host transport exchange")) return 1;
         POMS_HIP_CHECK(hipStreamSynchronize(st));
         const size_t cnt = (size_t)width * (size_t)plane_elems;
         if (c->stage.size() < 4 * cnt) c->stage.resize(4 * cnt);
@@ -425,6 +442,7 @@ int poms_allreduce_sum(poms_comm* c, double* buf, int64_t count, void* stream, i
 int poms_comm_slot(poms_comm* c, double** dev_slot, int* ticket) {
     if (!c || !dev_slot || !ticket) { set_error("poms_comm_slot: null argument"); return 1; }
     const int t = c->ring_next;
+    if (refuse_in_capture(c->cs, "poms_comm_slot")) return 1;
     c->ring_next = (t + 1) % poms_comm::kRing;
     POMS_HIP_CHECK(hipEventSynchronize(c->ring_ev[t]));
     slot_arm(c->ring + 2 * t);
@@ -479,6 +497,7 @@ static int shm_allsum(poms_comm* c, double* v, int cnt) {
 int poms_comm_wait(poms_comm* c, int ticket) {
     if (!c || ticket < 0 || ticket >= poms_comm::kRing) { set_error("poms_comm_wait: bad argument"); return 1; }
     if (c->ring_done[ticket]) return 0;
+    if (refuse_in_capture(c->cs, "poms_comm_wait")) return 1;
     const int cnt = c->ring_cnt[ticket];
     if (cnt < 1 || !c->ring_dst[ticket]) { set_error("poms_comm_wait: ticket has no pending sum"); return 1; }
     double* slot = c->ring + 2 * ticket;
@@ -527,6 +546,7 @@ int poms_op_run_dist(poms_op* op, poms_comm* c, int epilogue, double omega, cons
     double *nout = want_norm ? norm_dev : nullptr, *dout = want_dot ? dot_dev : nullptr;
     int t = -1;
     if (lazy_count > 0) {
+        if (refuse_in_capture(cstream(stream), "poms_op_run_dist (lazy host-read sums)")) return 1;
         if (!host_dst || !ticket || lazy_count != (want_norm ? 1 : 0) + (want_dot ? 1 : 0)) {
             set_error("poms_op_run_dist: bad lazy request");
             return 1;
