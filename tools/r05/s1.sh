@@ -9,7 +9,7 @@ O=gpurun_out/${1:-r05s1}; mkdir -p $O
 export TMPDIR=/tmp
 stop() { echo "STOP: $1 (rc=$2)"; exit "$2"; }
 for rnd in 1 2; do
-  for L in main poms_amd/exp/lib_r04.so; do
+  for L in main poms_amd/exp/lib_zr.so poms_amd/exp/lib_r04.so; do
     tag=$(basename $L .so); lib=$R/poms_amd/libpoms_hip.so; [ "$L" = main ] || lib=$R/$L
     POMS_HIP_LIB=$lib timeout -k 10 200 python tools/kernel_bench.py --reps 40 --rounds 2 --kinds apply,jacobi,from_zero \
         > $O/kb_${tag}_$rnd.log 2>&1; rc=$?; echo "kb $tag $rnd rc=$rc"; [ $rc -eq 0 ] || stop kb $rc
