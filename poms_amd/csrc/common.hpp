@@ -30,8 +30,6 @@ struct KronGeom {
     int z2_begin, z2_end;  // optional second plane range of the same launch (the other slab boundary)
     int tout;            // output columns per 64-column tile (v3 / v4 kernels; <= 64 - 2P)
     int order = 0;       // v5 / v6 tile order within an XCD: 0 = axis-2 tiles fastest, 1 = axis-1 tiles fastest
-    int skew = 0;        // v5 (tuning): odd tile rows start ~skew us late (POMS_V5_SKEW), so that two
-                         // vertically adjacent tiles do not fetch their shared halo rows at the same time
 };
 
 // Output planes [z0, z1) of axis-0 chunk `ch` (3D launches may cover two ranges).

@@ -389,9 +389,6 @@ kron_v5_kernel(const double* __restrict__ x, double* __restrict__ y, const doubl
         }
     }
 
-    if (g.skew > 0 && (t1 & 1)) {   // tuning (POMS_V5_SKEW): ~1 us per unit
-        for (int i = 0; i < g.skew; ++i) __builtin_amdgcn_s_sleep(32);
-    }
 #pragma unroll
     for (int i = 0; i < PFX; ++i) dma_x(i < nplanes ? z0 - P + i : -(1 << 20), i);
     if constexpr (HASB) dma_b(zo_of(0), 0);

@@ -25,9 +25,6 @@ int kron_v5_launch(int pmax, int epi, const KronPtrs& p, const KronGeom& g, cons
                    double omega, hipStream_t st, int diag_mode);
 void kron_v5_tile(int pmax, bool aligned, int* H, int* TO);
 int kron_v5_rows(int pmax, int epi);
-int kron_m2_launch(int pmax, int epi, const KronPtrs& p, const KronGeom& g, const ToepConst& tc, int H, double omega,
-                   hipStream_t st);
-bool kron_m2_aligned(const double* x, const double* y, const double* b, int pd2, int H, int64_t s1);
 int kron_v7_launch(int pmax, int epi, const KronPtrs& p, const KronGeom& g, const ToepConst& tc, double omega,
                    hipStream_t st, int diag, bool dry = false);
 int kron_v7_built();
@@ -589,10 +586,10 @@ int poms_op_set_variant(poms_op* op, int variant) {
     // 90/91, 92-100, 101-113: diagnostic / tuning builds of v3, v4, v5 (110-112: v5
     // two sweeps from zero without sums / x1 scaling, timing only; 113: the Jacobi
     // sweep streaming the x rows no other tile reads)
-    const bool known = variant == 0 || variant == 4 || (variant >= 7 && variant <= 12) ||
+    const bool known = variant == 0 || variant == 4 || (variant >= 7 && variant <= 11) ||
                        (variant >= 90 && variant <= 114) || (variant >= 121 && variant <= 124);
     if (!op || !known) {
-        set_error("poms_op_set_variant: bad argument (0, 4, 7, 8, 9, 10, 11, 12; 90-114 and 121-124 diagnostic)");
+        set_error("poms_op_set_variant: bad argument (0, 4, 7, 8, 9, 10, 11; 90-114 and 121-124 diagnostic)");
         return 1;
     }
     if (variant > 0 && !op->v2_ok) { set_error("poms_op_set_variant: variant needs pads == pmax"); return 1; }
@@ -608,8 +605,7 @@ int poms_diag_v5_stamps(uint64_t* host_out, int64_t n) {
 
 int poms_variant_built(int variant) {
     if (variant == 11 || (variant >= 121 && variant <= 124)) return kron_v7_built();
-    return (variant == 0 || variant == 4 || (variant >= 7 && variant <= 10) || variant == 12 ||
-            (variant >= 90 && variant <= 114)) ? 1 : 0;
+    return (variant == 0 || variant == 4 || (variant >= 7 && variant <= 10) || (variant >= 90 && variant <= 114)) ? 1 : 0;
 }
 
 int poms_op_kernel_variant(poms_op* op, int epilogue, int* variant) {
@@ -725,7 +721,7 @@ static int op_geom(poms_op* o, int64_t zb, int64_t ze, KronGeom& g, int v = -1, 
     g.tiles2 = (int)((o->L.n[2] + kron_tile_cols() - 1) / kron_tile_cols());
     const int trows = v == 10 ? kron_v5_rows(o->pmax, epi) : kron_tile_rows();
     g.tiles1 = (int)((o->L.n[1] + trows - 1) / trows);
-    g.tout = (v == 10 || v == 12) ? v5_to : (o->tout > 0 ? o->tout : 64 - 2 * o->pmax);
+    g.tout = v == 10 ? v5_to : (o->tout > 0 ? o->tout : 64 - 2 * o->pmax);
     if (v >= 4) g.tiles2 = (int)((o->L.n[2] + g.tout - 1) / g.tout);
     if (v == 11) {   // v7: the kernel maps its tiles itself; one flat tile index
         g.tiles2 = 1;
@@ -733,14 +729,6 @@ static int op_geom(poms_op* o, int64_t zb, int64_t ze, KronGeom& g, int v = -1, 
     }
     if (!is3d) {
         g.z_begin = 0; g.z_end = 1; g.chunk = 1; g.nchunks = 1; g.nch1 = 1; g.z2_begin = g.z2_end = 0;
-        if (v == 12) {   // m2: column tiles x row chunks, one wave each
-            const int n1 = (int)o->L.n[1];
-            int ch = o->chunk;
-            if (ch <= 0) ch = 16;   // rows per wave (tuning: poms_op_set_chunk)
-            g.chunk = std::max(1, std::min(ch, n1));
-            g.nchunks = (n1 + g.chunk - 1) / g.chunk;
-            g.tiles1 = 1;
-        }
         return 0;
     }
     if (zb < 0 || ze > o->L.n[0] || zb > ze) { set_error("plane range outside the slab"); return 1; }
@@ -755,12 +743,6 @@ static int op_geom(poms_op* o, int64_t zb, int64_t ze, KronGeom& g, int v = -1, 
             ord = e ? (atoi(e) ? 1 : 0) : 0;
         }
         g.order = ord;
-        static int skew = -1;   // (tuning: POMS_V5_SKEW, v5 only)
-        if (skew < 0) {
-            const char* e = getenv("POMS_V5_SKEW");
-            skew = e ? std::max(0, atoi(e)) : 0;
-        }
-        g.skew = v == 10 ? skew : 0;
     }
     g.z_begin = (int)zb;
     g.z_end = (int)ze;
@@ -786,23 +768,9 @@ static int op_geom(poms_op* o, int64_t zb, int64_t ze, KronGeom& g, int v = -1, 
 
 // variants whose Jacobi epilogue also accumulates x_out . b (v3 and v4 kernels)
 static bool fused_dot_ok(const poms_op* o) {
-    return o->form == FORM_STENCIL || (o->variant >= 4 && o->variant <= 12);
+    return o->form == FORM_STENCIL || (o->variant >= 4 && o->variant <= 11);
 }
 
-// m2 (variant 12, kron_m2.hip) runs 2D FORM_SUM operators at p <= 3 with storage pads
-// == pmax (its tiles are v5's, the corner-ghost rule too) and arrays < 2 GiB; its
-// 16-B loads and stores need 16-B aligned rows (checked per call).  POMS_M2=0 keeps
-// the round-4 2D kernels (v3 / v4) for A/B runs.
-static bool m2_ok(const poms_op* o) {
-    static int on = -1;
-    if (on < 0) {
-        const char* e = getenv("POMS_M2");
-        on = (e && e[0] == '0') ? 0 : 1;
-    }
-    const int64_t bytes = (int64_t)(o->L.n[1] + 2 * o->L.pads[1]) * row_geom(&o->L).s1 * 8;
-    return on && o->ndim == 2 && o->form == FORM_SUM && o->v2_ok && o->pmax <= 3 && bytes < 0x7ffffff0LL &&
-           !(o->ghost_corners && (o->pmax & 1));
-}
 
 // General-stencil launch (FORM_STENCIL): the epilogues of op_run plus EPI_DIAG.
 static int stencil_run(poms_op* o, int epi, double omega, const double* x, double* y, const double* b,
@@ -860,8 +828,6 @@ static int resolve_variant(const poms_op* o, int epi) {
                       // axes 1 and 2 share their rows (the other build spills)
         else if (o->ndim == 3)
             v = ((epi == EPI_APPLY && o->pmax >= 3) || (plain && o->pmax >= 4)) ? 7 : 9;
-        else if (epi != EPI_JACOBI0 && m2_ok(o))
-            v = 12;   // (op_run falls back to v3 / v4 on rows that are not 16-B aligned)
         else if (epi == EPI_JACOBI && o->pmax <= 3)
             v = jacobi2d_variant();
         else
@@ -903,17 +869,6 @@ static int op_run(poms_op* o, int epi, double omega, const double* x, double* y,
     // Variant 10 (v5) runs apply / residual / Jacobi / apply+dot of 3D p <= 3
     // operators, and is what 8 picks for them; 9 otherwise.
     int v = resolve_variant(o, epi);
-    if (v == 12) {   // m2: 2D FORM_SUM p <= 3 (resolve_variant), 16-B aligned rows (here)
-        int h = 0, to = 0;
-        kron_v5_tile(o->pmax, v5_aligned(o, x), &h, &to);
-        if (!m2_ok(o) || epi == EPI_JACOBI0 ||
-            !kron_m2_aligned(x, y, epi == EPI_APPLY || epi == EPI_APPLYDOT ? nullptr : b, (int)o->L.pads[2], h,
-                             row_geom(&o->L).s1)) {
-            const bool plain = epi == EPI_APPLY || epi == EPI_RESID;
-            v = o->ndim == 2 && epi == EPI_JACOBI && o->pmax <= 3 ? jacobi2d_variant()
-                : (plain && o->pmax <= 3) ? 7 : 9;
-        }
-    }
     if (v == 11 && !v7_ok(o, x, y))   // (as resolve_variant would pick for variant 10)
         v = (v5_ok(o) && !(epi == EPI_JACOBI0 && o->pmax == 3 && !same_toeplitz12(o))) ? 10 : 9;
     if (v == 11 || (v >= 121 && v <= 124)) {
@@ -936,7 +891,7 @@ static int op_run(poms_op* o, int epi, double omega, const double* x, double* y,
     if (v < 0) { set_error("v7 diagnostic build: aligned p = 3 apply only"); return 1; }
     o->last_variant = v7_diag ? 120 + v7_diag : v5_diag ? 100 + v5_diag : v;
     int v5_h = 0, v5_to = 0;
-    if (v == 10 || v == 12) kron_v5_tile(o->pmax, v5_aligned(o, x), &v5_h, &v5_to);
+    if (v == 10) kron_v5_tile(o->pmax, v5_aligned(o, x), &v5_h, &v5_to);
     KronGeom g;
     if (op_geom(o, zb, ze, g, v, v5_to, zb2, ze2, epi)) return 1;
     const int64_t nblk = (int64_t)g.tiles2 * g.tiles1 * g.nchunks;
@@ -971,9 +926,7 @@ static int op_run(poms_op* o, int epi, double omega, const double* x, double* y,
         tlh->ndof = (int64_t)((ze - zb) + (ze2 - zb2)) * g.n1 * g.n2;
         POMS_HIP_CHECK(timing_record(tlh->e0, as_stream(stream)));
     }
-    const int rc = v == 12
-        ? kron_m2_launch(o->pmax, epi, p, g, o->tc, v5_h, omega, as_stream(stream))
-        : v == 11
+    const int rc = v == 11
         ? kron_v7_launch(o->pmax, epi, p, g, o->tc, omega, as_stream(stream), v7_diag)
         : v == 10
         ? kron_v5_launch(o->pmax, epi, p, g, o->tc, v5_h, omega, as_stream(stream), v5_diag)

@@ -4,7 +4,7 @@ item 2: `POMS_PCG_GRAPH=2 tools/slab_proxy.py --loopback-rank 1` dumped core.)
 
 Each stage runs in a child process with faulthandler on, so a crash names its stage
 and the Python frame that made the native call; the parent prints every stage's exit
-status and stderr tail and stops at the first failure:
+status and stderr tail:
 
   halo      one ghost exchange (grouped ncclSend/ncclRecv on the communication
             stream, ordered by events) captured with torch.cuda.graph, replayed 3x,
@@ -139,7 +139,7 @@ STAGES = {"halo": stage_halo, "allreduce": stage_allreduce, "split": stage_split
 
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--stages", default="halo,allreduce,split,pcg")
+    ap.add_argument("--stages", default="allreduce,halo,split,pcg")
     ap.add_argument("--child", default="")
     a = ap.parse_args()
     if a.child:
@@ -147,14 +147,14 @@ def main():
         faulthandler.enable()
         STAGES[a.child]()
         return 0
-    for s in a.stages.split(","):
+    bad = False
+    for s in a.stages.split(","):   # every stage, each in its own process
         r = subprocess.run([sys.executable, "-X", "faulthandler", __file__, "--child", s], capture_output=True, text=True,
                            timeout=240)
         tail = "\n".join((r.stdout + r.stderr).strip().splitlines()[-25:])
         print(f"=== stage {s}: exit {r.returncode}\n{tail}\n", flush=True)
-        if r.returncode != 0:
-            return 1
-    return 0
+        bad = bad or r.returncode != 0
+    return 1 if bad else 0
 
 
 if __name__ == "__main__":

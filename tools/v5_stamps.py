@@ -28,6 +28,8 @@ def main():
     ap.add_argument("--kinds", default="apply,jacobi")
     ap.add_argument("--reps", type=int, default=5)
     ap.add_argument("--json", default="")
+    ap.add_argument("--stamp-variant", type=int, default=114,
+                    help="114: the production march stamped; 116: the software-pipelined apply stamped")
     a = ap.parse_args()
     import numpy as np
     import torch
@@ -50,7 +52,7 @@ def main():
         A.set_variant(10)
         for _ in range(3):
             fn()
-        A.set_variant(114)
+        A.set_variant(a.stamp_variant)
         res = []
         for r in range(a.reps):
             torch.cuda.synchronize()
@@ -59,7 +61,7 @@ def main():
             fn()
             e1.record()
             torch.cuda.synchronize()
-            assert A.last_variant == 114
+            assert A.last_variant == a.stamp_variant
             nw = 1 << 16
             buf = (C.c_uint64 * (nw * 8))()
             _lib.call("poms_diag_v5_stamps", C.cast(buf, C.c_void_p), nw * 8)
