@@ -423,6 +423,20 @@ int poms_comm_uses_shm(poms_comm* comm, int* yes);
 int poms_halo_start(poms_comm* comm, double* data, int64_t plane_elems, int64_t n_local, int pad,
                     int width, int prev, int next, void* stream);
 int poms_halo_finish(poms_comm* comm, void* stream);
+/* Peer transport for poms_halo_start (every rank the same enable / wgs): the
+ * exchange becomes ONE kernel of `wgs` workgroups (1..256) on the communication
+ * stream that stores the boundary planes straight into the neighbours' mailboxes
+ * (IPC-mapped device memory; xGMI peer stores between GPUs) and copies its own
+ * mailboxes into the ghost planes, ordered by per-workgroup flag slots -- no RCCL
+ * call and no host step, so it can be captured into a graph.  The mailboxes are
+ * (re)built, collectively with the two neighbours, at the first exchange of a
+ * larger size or poms_comm_peer_reserve (never inside a capture).  A wait that
+ * exceeds 20 s gives up and sets the timed-out flag (poms_comm_peer_status)
+ * instead of hanging the GPU.  Replaces the same `_update_ghost_regions_parallel`
+ * (`pyccel/kron_product.py:21-41`).                                            */
+int poms_comm_set_peer(poms_comm* comm, int enable, int wgs);
+int poms_comm_peer_reserve(poms_comm* comm, int64_t cnt, int prev, int next);
+int poms_comm_peer_status(poms_comm* comm, int* active, int* fine_grained, int* timed_out);
 /* In-place global sum of `count` doubles after the work queued on `stream`;
  * wait_back: `stream` waits for the result, else it is ready on the
  * communication stream only.                                                  */

@@ -13,6 +13,7 @@
 // solver scalars (`sources/solvers.py:87-124`, `sources/mg_jac.py:95`).
 #include "common.hpp"
 #include "split_hooks.hpp"
+#include "peer.hpp"
 #include "../../include/poms_hip.h"
 
 #include <rccl/rccl.h>
@@ -21,6 +22,7 @@
 #include <sys/mman.h>
 #include <unistd.h>
 
+#include <algorithm>
 #include <atomic>
 #include <chrono>
 #include <cmath>
@@ -74,6 +76,20 @@ struct poms_comm {
     poms_host_allreduce_fn ar = nullptr;
     void* user = nullptr;
     std::vector<double> stage;      // 4 x width x plane_elems (send lo / recv lo / send hi / recv hi)
+    // peer transport (poms_comm_set_peer): the ghost exchange as ONE kernel on the
+    // communication stream that writes the boundary planes straight into the
+    // neighbours' mailboxes (IPC-mapped device memory, xGMI peer stores) and copies
+    // its own mailboxes into the ghost planes, synchronised by per-workgroup flag
+    // slots -- no RCCL call, no host step, capturable into a graph
+    bool peer_on = false;
+    int peer_wgs = 32;                // exchange workgroups (the same on every rank)
+    int peer_prev = -2, peer_next = -2;   // the neighbours the blocks were exchanged with
+    int64_t peer_cap = 0;             // doubles per mailbox side
+    char* pblk = nullptr;             // own block: flag slots + 2 mailbox sides
+    char* pprev = nullptr;            // the neighbours' blocks (IPC-opened; own on a loopback)
+    char* pnext = nullptr;
+    bool pprev_ipc = false, pnext_ipc = false;
+    bool peer_fine = false;           // own block is fine-grained (coherent) device memory
 };
 
 #define POMS_NCCL_CHECK(expr)                                                    \
@@ -144,6 +160,182 @@ static void shm_open_block(poms_comm* c, const char* id, size_t id_len) {
     // the last slot's seq counts the ranks present (zero-filled by the first ftruncate)
     reinterpret_cast<std::atomic<uint64_t>*>(&c->shm[2 * c->nranks].seq)->fetch_add(1);
     snprintf(c->shm_name, sizeof(c->shm_name), "%s", name);
+}
+
+// ---- peer transport (csrc/peer.hpp) -------------------------------------------
+namespace {
+__global__ void __launch_bounds__(256) peer_exchange_kernel(const PeerArgs a) { peer_exchange_body(a, blockIdx.x, gridDim.x); }
+
+double* peer_side_host(uint64_t* blk, int side, int64_t cap) {
+    return reinterpret_cast<double*>(reinterpret_cast<char*>(blk) + kPeerHdr) + (int64_t)side * cap;
+}
+}  // namespace
+
+static void peer_release(poms_comm* c) {
+    if (c->pprev_ipc && c->pprev) (void)hipIpcCloseMemHandle(c->pprev);
+    if (c->pnext_ipc && c->pnext && c->pnext != c->pprev) (void)hipIpcCloseMemHandle(c->pnext);
+    if (c->pblk) (void)hipFree(c->pblk);
+    c->pblk = c->pprev = c->pnext = nullptr;
+    c->pprev_ipc = c->pnext_ipc = false;
+    c->peer_cap = 0;
+    c->peer_prev = c->peer_next = -2;
+}
+
+// Pass `bytes` of host data to prev / next and take theirs (blocking): the host
+// callback, or RCCL send/recv on the communication stream.  prev == next (a
+// one-rank loopback): nothing to exchange, the caller uses its own block.
+static int peer_swap_bytes(poms_comm* c, const void* mine, void* from_prev, void* from_next, int bytes, int prev,
+                           int next) {
+    const int nd = (bytes + 7) / 8;
+    std::vector<double> st(4 * (size_t)nd, 0.0);
+    std::memcpy(st.data(), mine, bytes);
+    std::memcpy(st.data() + 2 * nd, mine, bytes);
+    if (c->host) {
+        if (c->xchg(c->user, st.data(), st.data() + nd, st.data() + 2 * nd, st.data() + 3 * nd, nd, prev, next)) {
+            set_error("peer transport: handle exchange callback failed");
+            return 1;
+        }
+    } else {
+        double* d = nullptr;
+        POMS_HIP_CHECK(hipMalloc(reinterpret_cast<void**>(&d), 4 * (size_t)nd * sizeof(double)));
+        bool ok = hipMemcpy(d, st.data(), 4 * (size_t)nd * sizeof(double), hipMemcpyHostToDevice) == hipSuccess;
+        ok = ok && ncclGroupStart() == ncclSuccess;
+        if (ok && prev >= 0)
+            ok = ncclSend(d, nd, ncclDouble, prev, c->comm, c->cs) == ncclSuccess &&
+                 ncclRecv(d + nd, nd, ncclDouble, prev, c->comm, c->cs) == ncclSuccess;
+        if (ok && next >= 0)
+            ok = ncclSend(d + 2 * nd, nd, ncclDouble, next, c->comm, c->cs) == ncclSuccess &&
+                 ncclRecv(d + 3 * nd, nd, ncclDouble, next, c->comm, c->cs) == ncclSuccess;
+        ok = (ncclGroupEnd() == ncclSuccess) && ok;
+        ok = ok && hipStreamSynchronize(c->cs) == hipSuccess &&
+             hipMemcpy(st.data(), d, 4 * (size_t)nd * sizeof(double), hipMemcpyDeviceToHost) == hipSuccess;
+        (void)hipFree(d);
+        if (!ok) { set_error("peer transport: handle exchange over RCCL failed"); return 1; }
+    }
+    if (prev >= 0) std::memcpy(from_prev, st.data() + nd, bytes);
+    if (next >= 0) std::memcpy(from_next, st.data() + 3 * nd, bytes);
+    return 0;
+}
+
+// Blocks of `cnt` doubles per side with the neighbours prev / next, (re)built when
+// missing, too small or exchanged with other neighbours.  Collective over the two
+// neighbours (every rank issues the same exchanges in the same order, so all of
+// them rebuild at the same call); never inside a capture.
+static int peer_ensure(poms_comm* c, int64_t cnt, int prev, int next, hipStream_t st) {
+    if (c->pblk && cnt <= c->peer_cap && prev == c->peer_prev && next == c->peer_next) return 0;
+    if (refuse_in_capture(st, "peer transport setup (first exchange of this size)")) return 1;
+    // every earlier exchange of this rank is complete, hence every neighbour's store
+    // into the old block (the neighbours, in turn, finish theirs before answering the
+    // handle exchange below)
+    POMS_HIP_CHECK(hipStreamSynchronize(c->cs));
+    POMS_HIP_CHECK(hipStreamSynchronize(st));
+    const bool loop = c->nranks == 1;   // a one-rank loopback: the neighbours are this rank
+    char* old = c->pblk;
+    char* old_prev = c->pprev;
+    char* old_next = c->pnext;
+    const bool old_prev_ipc = c->pprev_ipc, old_next_ipc = c->pnext_ipc;
+    const int64_t cap = (std::max<int64_t>(cnt, 1 << 16) + 31) & ~(int64_t)31;   // (keeps side 1 16-B aligned)
+    const size_t bytes = kPeerHdr + 2 * (size_t)cap * sizeof(double);
+    char* blk = nullptr;
+    // fine-grained (coherent between devices and XCDs) unless POMS_PEER_FINE=0 (tuning)
+    const char* fe = getenv("POMS_PEER_FINE");
+    const bool want_fine = fe ? fe[0] != '0' : true;
+    bool fine = want_fine &&
+                hipExtMallocWithFlags(reinterpret_cast<void**>(&blk), bytes, hipDeviceMallocFinegrained) == hipSuccess;
+    hipIpcMemHandle_t mine{};
+    if (fine && !loop && hipIpcGetMemHandle(&mine, blk) != hipSuccess) {   // not exportable: plain device memory
+        (void)hipFree(blk);
+        blk = nullptr;
+        fine = false;
+    }
+    (void)hipGetLastError();
+    if (!blk) {
+        POMS_HIP_CHECK(hipMalloc(reinterpret_cast<void**>(&blk), bytes));
+        if (!loop) POMS_HIP_CHECK(hipIpcGetMemHandle(&mine, blk));
+    }
+    POMS_HIP_CHECK(hipMemset(blk, 0, kPeerHdr));
+    POMS_HIP_CHECK(hipDeviceSynchronize());
+    char* np = nullptr;
+    char* nn = nullptr;
+    bool pi = false, ni = false;
+    if (loop) {
+        np = prev >= 0 ? blk : nullptr;
+        nn = next >= 0 ? blk : nullptr;
+    } else {
+        // each rank sends its handle and the capacity, so that a mismatch fails loudly
+        struct Msg { hipIpcMemHandle_t h; int64_t cap; } m{mine, cap}, fp{}, fn{};
+        if (peer_swap_bytes(c, &m, &fp, &fn, (int)sizeof(Msg), prev, next)) return 1;
+        if ((prev >= 0 && fp.cap != cap) || (next >= 0 && fn.cap != cap)) {
+            set_error("peer transport: neighbours disagree on the mailbox size");
+            return 1;
+        }
+        if (prev >= 0) {
+            POMS_HIP_CHECK(hipIpcOpenMemHandle(reinterpret_cast<void**>(&np), fp.h, hipIpcMemLazyEnablePeerAccess));
+            pi = true;
+        }
+        if (next >= 0) {
+            POMS_HIP_CHECK(hipIpcOpenMemHandle(reinterpret_cast<void**>(&nn), fn.h, hipIpcMemLazyEnablePeerAccess));
+            ni = true;
+        }
+    }
+    if (old_prev_ipc && old_prev) (void)hipIpcCloseMemHandle(old_prev);
+    if (old_next_ipc && old_next && old_next != old_prev) (void)hipIpcCloseMemHandle(old_next);
+    if (old) (void)hipFree(old);
+    c->pblk = blk;
+    c->pprev = np;
+    c->pnext = nn;
+    c->pprev_ipc = pi;
+    c->pnext_ipc = ni;
+    c->peer_cap = cap;
+    c->peer_prev = prev;
+    c->peer_next = next;
+    c->peer_fine = fine;
+    return 0;
+}
+
+// The argument block of one exchange of `data` (mailboxes built if needed).
+static int peer_fill(poms_comm* c, double* data, int64_t plane_elems, int64_t n_local, int pad, int width, int prev,
+                     int next, hipStream_t st, PeerArgs& a) {
+    const int64_t cnt = (int64_t)width * plane_elems;
+    if (peer_ensure(c, cnt, prev, next, st)) return 1;
+    a.send_lo = data + (int64_t)pad * plane_elems;
+    a.send_hi = data + (int64_t)(pad + n_local - width) * plane_elems;
+    a.ghost_lo = data + (int64_t)(pad - width) * plane_elems;
+    a.ghost_hi = data + (int64_t)(pad + n_local) * plane_elems;
+    a.cnt = cnt;
+    a.cap = c->peer_cap;
+    auto* own = reinterpret_cast<uint64_t*>(c->pblk);
+    a.own = own;
+    a.out_lo = a.out_hi = nullptr;
+    a.arr_lo = a.arr_hi = a.ack_lo = a.ack_hi = nullptr;
+    const bool loop = c->nranks == 1;
+    if (prev >= 0) {
+        auto* pb = loop ? own : reinterpret_cast<uint64_t*>(c->pprev);
+        a.out_lo = peer_side_host(pb, loop ? 0 : 1, a.cap);
+        a.arr_lo = pb + (loop ? kArrPrev : kArrNext);
+        a.ack_lo = pb + (loop ? kAckPrev : kAckNext);
+    }
+    if (next >= 0) {
+        auto* nb = loop ? own : reinterpret_cast<uint64_t*>(c->pnext);
+        a.out_hi = peer_side_host(nb, loop ? 1 : 0, a.cap);
+        a.arr_hi = nb + (loop ? kArrNext : kArrPrev);
+        a.ack_hi = nb + (loop ? kAckNext : kAckPrev);
+    }
+    a.G = c->peer_wgs;
+    return 0;
+}
+
+// The exchange as its own kernel on the communication stream
+static int peer_exchange(poms_comm* c, double* data, int64_t plane_elems, int64_t n_local, int pad, int width,
+                         int prev, int next, hipStream_t st) {
+    PeerArgs a;
+    if (peer_fill(c, data, plane_elems, n_local, pad, width, prev, next, st, a)) return 1;
+    POMS_HIP_CHECK(hipEventRecord(c->ev_in, st));
+    POMS_HIP_CHECK(hipStreamWaitEvent(c->cs, c->ev_in, 0));
+    hipLaunchKernelGGL(peer_exchange_kernel, dim3(a.G), dim3(256), 0, c->cs, a);
+    POMS_HIP_CHECK(hipGetLastError());
+    POMS_HIP_CHECK(hipEventRecord(c->ev_halo, c->cs));
+    return 0;
 }
 
 extern "C" {
@@ -334,6 +526,7 @@ static int host_allreduce(poms_comm* c, double* buf, int64_t count, hipStream_t 
 int poms_comm_destroy(poms_comm* c) {
     if (!c) return 0;
     if (c->cs) (void)hipStreamSynchronize(c->cs);
+    peer_release(c);
     if (c->comm) ncclCommDestroy(c->comm);
     for (hipEvent_t e : {c->ev_in, c->ev_halo, c->ev_red, c->ev_bnd})
         if (e) (void)hipEventDestroy(e);
@@ -353,6 +546,38 @@ int poms_comm_stream(poms_comm* c, void** stream) {
     return 0;
 }
 
+int poms_comm_set_peer(poms_comm* c, int enable, int wgs) {
+    if (!c || wgs < 1 || wgs > kPeerMaxWgs) { set_error("poms_comm_set_peer: bad argument (wgs in 1..256)"); return 1; }
+    if (c->peer_on && (!enable || wgs != c->peer_wgs)) {   // blocks are rebuilt at the next exchange
+        (void)hipStreamSynchronize(c->cs);
+        peer_release(c);
+    }
+    c->peer_on = enable != 0;
+    c->peer_wgs = wgs;
+    return 0;
+}
+
+int poms_comm_peer_reserve(poms_comm* c, int64_t cnt, int prev, int next) {
+    if (!c || cnt < 1) { set_error("poms_comm_peer_reserve: bad argument"); return 1; }
+    if (!c->peer_on || (prev < 0 && next < 0)) return 0;
+    return peer_ensure(c, cnt, prev, next, c->cs);
+}
+
+int poms_comm_peer_status(poms_comm* c, int* active, int* fine_grained, int* timed_out) {
+    if (!c || !active || !fine_grained || !timed_out) { set_error("poms_comm_peer_status: null argument"); return 1; }
+    *active = c->peer_on ? 1 : 0;
+    *fine_grained = c->peer_fine ? 1 : 0;
+    *timed_out = 0;
+    if (c->pblk) {
+        if (refuse_in_capture(c->cs, "poms_comm_peer_status")) return 1;
+        uint64_t st = 0;
+        POMS_HIP_CHECK(hipStreamSynchronize(c->cs));
+        POMS_HIP_CHECK(hipMemcpy(&st, c->pblk + 8 * kStatus, sizeof(st), hipMemcpyDeviceToHost));
+        *timed_out = st != 0 ? 1 : 0;
+    }
+    return 0;
+}
+
 // Ghost exchange of an axis-0 slab: `data` points at plane 0 of the padded local
 // array (the first ghost plane), planes are `plane_elems` doubles apart; the
 // first / last `width` owned planes go to `prev` / `next` (-1: none) and their
@@ -365,7 +590,7 @@ int poms_halo_start(poms_comm* c, double* data, int64_t plane_elems, int64_t n_l
         return 1;
     }
     if (width == 0 || (prev < 0 && next < 0)) return 0;
-    if (c->host) {   // stage the boundary planes, exchange through the callback, copy back
+    if (c->host && !c->peer_on) {   // stage the boundary planes, exchange through the callback, copy back
         hipStream_t st = cstream(stream);
         if (refuse_in_capture(st, "host transport exchange")) return 1;
         POMS_HIP_CHECK(hipStreamSynchronize(st));
@@ -389,6 +614,7 @@ int poms_halo_start(poms_comm* c, double* data, int64_t plane_elems, int64_t n_l
         POMS_HIP_CHECK(hipEventRecord(c->ev_halo, st));
         return 0;
     }
+    if (c->peer_on) return peer_exchange(c, data, plane_elems, n_local, pad, width, prev, next, cstream(stream));
     POMS_HIP_CHECK(hipEventRecord(c->ev_in, cstream(stream)));
     POMS_HIP_CHECK(hipStreamWaitEvent(c->cs, c->ev_in, 0));
     const size_t cnt = (size_t)width * (size_t)plane_elems;

@@ -2311,8 +2311,9 @@ static int pcg_speculative(PcgRun& R, const double* b, double* x, int has_x0, do
     // loopback call crashed in the attempt, r04graph logs).  A caller whose buffers
     // never repeat would capture every call: after 8 more captures than hits the
     // operator stops using graphs.
-    // POMS_PCG_GRAPH=2 (diagnostic, tools/graph_rccl_probe.py): graphs with an RCCL
-    // communicator too -- every exchange and all-reduce of the call captured
+    // POMS_PCG_GRAPH=2 (opt-in, tools/graph_rccl_probe.py): graphs with a communicator
+    // too -- every exchange and all-reduce of the call captured; RCCL's point-to-point
+    // exchange does not survive capture, the peer transport's does (POMS_COMM_PEER=1)
     const char* ge = getenv("POMS_PCG_GRAPH");
     int host_comm = 0;
     if (R.comm && poms_comm_is_host(R.comm, &host_comm)) return 1;

@@ -341,7 +341,12 @@ class NativeComm:
     :meth:`create` runs a self-test (an all-reduce and a ghost exchange checked
     against their known results, both run on every rank before either is judged)
     and RAISES if it fails on any rank; ``POMS_NATIVE_COMM=0`` selects the
-    torch.distributed transport explicitly."""
+    torch.distributed transport explicitly.
+
+    ``POMS_COMM_PEER=1`` (the same on every rank) moves the ghost exchange to the
+    peer transport (``poms_comm_set_peer``): one kernel of ``POMS_PEER_WGS``
+    (default 32) workgroups that stores the boundary planes into the neighbours'
+    IPC-mapped mailboxes -- no RCCL call, capturable.  The self-test then runs it."""
 
     def __init__(self, handle, device: int, callbacks=None):
         import ctypes as C
@@ -356,6 +361,31 @@ class NativeComm:
         yes = C.c_int()
         _lib.call("poms_comm_is_host", self.h, C.byref(yes))
         self.is_host = bool(yes.value)
+        self.peer = False
+        if os.environ.get("POMS_COMM_PEER", "0") == "1":
+            self.set_peer(True, int(os.environ.get("POMS_PEER_WGS", "32")))
+
+    def set_peer(self, enable: bool, wgs: int = 64) -> None:
+        """Peer transport for the ghost exchange on (every rank alike) or off."""
+        from . import _lib
+        _lib.call("poms_comm_set_peer", self.h, 1 if enable else 0, int(wgs))
+        self.peer = bool(enable)
+
+    def peer_reserve(self, cnt: int, prev: int, nxt: int) -> None:
+        """Build the peer mailboxes for exchanges of up to ``cnt`` doubles per side now
+        (collective with the two neighbours), not at the first such exchange -- which
+        may be inside a graph capture."""
+        from . import _lib
+        _lib.call("poms_comm_peer_reserve", self.h, int(cnt), int(prev), int(nxt))
+
+    def peer_status(self) -> dict:
+        """{"active", "fine_grained", "timed_out"} of the peer transport (synchronises
+        the communication stream)."""
+        import ctypes as C
+        from . import _lib
+        a, f, t = C.c_int(), C.c_int(), C.c_int()
+        _lib.call("poms_comm_peer_status", self.h, C.byref(a), C.byref(f), C.byref(t))
+        return {"active": bool(a.value), "fine_grained": bool(f.value), "timed_out": bool(t.value)}
 
     @property
     def uses_shm(self) -> bool:
@@ -513,6 +543,8 @@ class NativeComm:
         s0, s1 = lz.value(0), lz.value(1)
         ok = ok and s0 == world * (world + 1) / 2.0 and s1 == float(world * world)
         h = data.cpu()
+        if self.peer and self.peer_status()["timed_out"]:
+            return False
         for j in range(width):
             lo = h[pad - width + j]   # planes n_loc-width+j of rank-1
             hi = h[pad + n_loc + j]   # planes j of rank+1

@@ -578,6 +578,12 @@ class KronOperator:
         n0g = V.npts[0] if nd == 3 else 1
         _lib.call("poms_op_create", V.ctx, 3 if nd == 3 else 2, C.byref(V.layout), cform, self.pmax,
                   farr, g0, n0g, C.byref(self._h))
+        d = V.dist if V.is_distributed else None
+        if d is not None and getattr(d, "native", None) is not None and d.native.peer and nd == 3:
+            # peer transport: the mailboxes for this operator's exchanges now, on every
+            # rank (operators are built in the same order everywhere), not inside a capture
+            d.native.peer_reserve(self.pmax * V.plane_elems, -1 if d.prev is None else d.prev,
+                                  -1 if d.next is None else d.next)
         self.timer = None  # list -> (kind, start_event, end_event, call) per kernel launch
         self._calls = 0    # operator calls (one call = 1 launch, or 2 when a halo exchange is overlapped)
 

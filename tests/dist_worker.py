@@ -202,6 +202,21 @@ def run_gpu():
     err = rel(got.numpy().reshape(xr.shape), xr)
     check(err <= tol, f"distributed V-cycle {err} > {tol}")
     check(ipre["niter"] == ipre_r["niter"] and ipos["niter"] == ipos_r["niter"], "iteration counts")
+    _check_peer(d)
+    _check_peer(mg.space.dist)
+
+
+def _check_peer(d):
+    """With POMS_COMM_PEER=1 every exchange went through the peer transport, and no
+    wait of its kernel timed out."""
+    want = os.environ.get("POMS_COMM_PEER") == "1"
+    nc = getattr(d, "native", None)
+    if nc is None or dist.get_world_size() == 1:
+        return
+    check(nc.peer == want, f"peer transport {nc.peer}, asked {want}")
+    if want:
+        st = nc.peer_status()
+        check(st["active"] and not st["timed_out"], f"peer transport status {st}")
 
 
 def run_gpu_fullsize_slabs():
@@ -268,6 +283,7 @@ def run_gpu_fullsize_slabs():
     xl3, il = solvers.pcg(Al, solvers.damped_jacobi, bl, tol=1e-6, maxiter=10)
     xg3, ig = solvers.pcg(Ag, solvers.damped_jacobi, bg, tol=1e-6, maxiter=10)
     check(il["niter"] == ig["niter"] and il["success"] == ig["success"], f"pcg stop {il} vs {ig}")
+    _check_peer(d)
     print(f"rank {dist.get_rank()} slab [{d.start}, {d.end}) errors {errs}", flush=True)
 
 

@@ -83,9 +83,10 @@ def test_two_rank_distributed_operator_and_vcycle_gpu(device_reductions):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("world,boundary_on_cs,shm", [(2, "1", "0"), (3, "1", "0"), (2, "0", "0"),
-                                                      (2, "1", "1"), (3, "1", "1"), (1, "1", "0")])
-def test_two_rank_native_schedule_with_peers_gpu(world, boundary_on_cs, shm):
+@pytest.mark.parametrize("world,boundary_on_cs,shm,peer", [(2, "1", "0", "0"), (3, "1", "0", "0"), (2, "0", "0", "0"),
+                                                           (2, "1", "1", "0"), (3, "1", "1", "0"), (1, "1", "0", "0"),
+                                                           (2, "1", "1", "1"), (3, "1", "1", "1"), (3, "0", "1", "1")])
+def test_two_rank_native_schedule_with_peers_gpu(world, boundary_on_cs, shm, peer):
     """The production slab schedule (poms_op_run_dist: exchange, interior planes,
     both boundaries in one launch -- on the communication stream behind the
     exchange, or with POMS_BOUNDARY_ON_CS=0 on the compute stream; lazy ring-slot
@@ -96,21 +97,28 @@ def test_two_rank_native_schedule_with_peers_gpu(world, boundary_on_cs, shm):
     (shm_allsum, poms_comm_wait's shared-memory branch) as in a one-node RCCL run.
     world=1: a communicator with no neighbour takes the single-launch path (no
     exchange is queued, so no split launch may run unordered on the communication
-    stream; advisor, round 3)."""
+    stream; advisor, round 3).  peer=1: the ghost planes move through the peer
+    transport instead (POMS_COMM_PEER: one kernel on the communication stream storing
+    into the neighbours' IPC-mapped mailboxes -- here processes sharing the GPU)."""
     import torch
     assert torch.cuda.device_count() >= 1, "GPU test selected but no GPU visible"
     _launch("gpu", world=world, extra_env={"POMS_TEST_DEVRED": "1", "POMS_TEST_HOST_TRANSPORT": "1",
-                                           "POMS_BOUNDARY_ON_CS": boundary_on_cs, "POMS_TEST_HOST_SHM": shm})
+                                           "POMS_BOUNDARY_ON_CS": boundary_on_cs, "POMS_TEST_HOST_SHM": shm,
+                                           "POMS_COMM_PEER": peer})
 
 
 @pytest.mark.gpu
-def test_eight_rank_fullsize_slabs_host_transport_gpu():
+@pytest.mark.parametrize("peer", ["0", "1"])
+def test_eight_rank_fullsize_slabs_host_transport_gpu(peer):
     """The 8-GPU run's split of the headline grid (515^3 over 8 ranks: 65/64-plane
     slabs) on one GPU: the production schedule and the shared-memory sums against
-    the single-GPU result at 1e-13 with identical iteration counts."""
+    the single-GPU result at 1e-13 with identical iteration counts.  peer=1: the
+    ghost exchange through the peer transport (POMS_COMM_PEER)."""
     import torch
     assert torch.cuda.device_count() >= 1, "GPU test selected but no GPU visible"
-    _launch("gpu_fullsize_slabs", world=8, timeout=900)
+    # (8 exchange workgroups per rank: each holds a CU slot while it waits for its
+    # neighbours, and here 8 ranks share one GPU)
+    _launch("gpu_fullsize_slabs", world=8, timeout=900, extra_env={"POMS_COMM_PEER": peer, "POMS_PEER_WGS": "8"})
 
 
 @pytest.mark.gpu

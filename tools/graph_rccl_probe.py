@@ -130,7 +130,7 @@ def stage_pcg():
         out[mode] = (x._data.clone(), dict(info))
     assert out["step"][1] == out["graph"][1], (out["step"][1], out["graph"][1])
     assert torch.equal(out["step"][0], out["graph"][0]), "graph replay != step-by-step loop"
-    st = A.spec_stats() if hasattr(A, "spec_stats") else None
+    st = A.spec_stats if hasattr(A, "spec_stats") else None
     print("pcg ok", out["graph"][1], "spec stats", st, flush=True)
 
 

@@ -74,6 +74,7 @@ def main():
     ap.add_argument("--warmup", type=int, default=1)
     ap.add_argument("--loopback-rank", type=int, default=None)
     ap.add_argument("--world", type=int, default=8)
+    ap.add_argument("--chunk", type=int, default=0, help="axis-0 chunk of every operator launch (0: auto)")
     a = ap.parse_args()
     import torch
     torch.cuda.set_device(0)
@@ -82,13 +83,15 @@ def main():
         from poms_amd.mg import TwoLevelVCycle
         n = a.cells + a.p
         d = SlabDistribution.loopback(n, a.loopback_rank, a.world)
-        mg = TwoLevelVCycle(a.p, a.cells, a.coarse, ndim=3, dist=d)
+        mg = TwoLevelVCycle(a.p, a.cells, a.coarse, ndim=3, dist=d, chunk=a.chunk)
         npts = [d.n_local, n, n]
         label = (f"rank {a.loopback_rank} of {a.world}: {npts[0]}x{n}x{n} owned DOF of the {n}^3 problem, "
                  f"exchanges with {(d.prev is not None) + (d.next is not None)} neighbour side(s) "
                  f"looped back through a one-rank RCCL communicator ({d.transport})")
     else:
         mg, npts = build(a.planes - a.p, a.cells, a.p, a.coarse)
+        if a.chunk:
+            mg.A.set_chunk(a.chunk)
         label = f"{npts[0]}x{npts[1]}x{npts[2]} DOF (one slab of the 8-GPU bench, no halo)"
     bf = mg.rhs_ones()
     for _ in range(a.warmup):
