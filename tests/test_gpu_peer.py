@@ -98,20 +98,23 @@ def test_peer_exchange_capture_and_replay():
     assert not c.peer_status()["timed_out"]
 
 
-def test_peer_loopback_operator_matches_rccl_loopback():
+@pytest.mark.parametrize("cells,rank", [(40, 1), (120, 1), (120, 0), (200, 2)])
+def test_peer_loopback_operator_matches_rccl_loopback(cells, rank):
     """The distributed operator calls (interior planes beside the exchange, both
     boundaries after it) with the peer transport equal the RCCL transport's bitwise
-    on the same loopback slab (both put the slab's own planes in its ghosts)."""
+    on the same loopback slab (both put the slab's own planes in its ghosts): apply,
+    Jacobi sweep and its norm, residual, two sweeps from zero and their norms, apply
+    + dot -- each call exchanging, twice over."""
     from poms_amd.dist import SlabDistribution
     from poms_amd.splines import assemble_1d, uniform_knots
     from poms_amd.stencil import KronOperator, StencilVectorSpace
     torch.cuda.set_device(0)
-    p, cells = 3, 40
+    p = 3
     n = cells + p
     M, K = assemble_1d(uniform_knots(p, cells), p)
     outs = []
     for peer in (False, True):
-        d = SlabDistribution.loopback(n, 1, 4)
+        d = SlabDistribution.loopback(n, rank, 4)
         if peer:
             d.native.set_peer(True, 64)
         V = StencilVectorSpace([n] * 3, [p] * 3, align=True, dist=d)
@@ -120,19 +123,28 @@ def test_peer_loopback_operator_matches_rccl_loopback():
         x, b = V.zeros(), V.zeros()
         V.interior(x._data).uniform_(-1, 1, generator=gen)
         V.interior(b._data).uniform_(-1, 1, generator=gen)
-        y = A.dot(x)
-        xo = V.zeros()
-        nrm = A.jacobi_sweep(b, x, xo, 2.0 / 3.0, want_norm=True)
-        r = A.residual(b, xo)
-        torch.cuda.synchronize()
-        outs.append((y._data.clone(), xo._data.clone(), nrm, r._data.clone()))
+        res = []
+        for _ in range(2):
+            x._ghost_valid = False
+            y = A.dot(x)
+            xo = V.zeros()
+            x._ghost_valid = False
+            nrm = A.jacobi_sweep(b, x, xo, 2.0 / 3.0, want_norm=True)
+            r = A.residual(b, xo)
+            j0 = V.zeros()
+            b._ghost_valid = False
+            n0 = A.jacobi_from_zero(b, j0, 2.0 / 3.0, want_norm=True)
+            x._ghost_valid = False
+            ad = float(A.dot_inner(x, V.zeros(), device=True))
+            torch.cuda.synchronize()
+            res.append([V.interior(t._data).clone() for t in (y, xo, r, j0)] + [nrm, n0, ad])
+        outs.append(res)
         if peer:
-            assert not d.native.peer_status()["timed_out"]
-    (y0, x0, n0, r0), (y1, x1, n1, r1) = outs
-    assert torch.equal(V.interior(y0), V.interior(y1))
-    assert torch.equal(V.interior(x0), V.interior(x1))
-    assert torch.equal(V.interior(r0), V.interior(r1))
-    assert n0 == n1
+            st = d.native.peer_status()
+            assert st["active"] and not st["timed_out"], st
+    for a, b_ in zip(outs[0], outs[1]):
+        for u, v in zip(a, b_):
+            assert torch.equal(u, v) if isinstance(u, torch.Tensor) else u == v, (u, v)
 
 
 def _loopback_op(cells=40, p=3, rank=1, world=4):
