@@ -354,7 +354,7 @@ kron_v5_kernel(const double* __restrict__ x, double* __restrict__ y, const doubl
     // keep the round-3 masked sums: with the zeroed rings the Jacobi build issued 3 %
     // more VALU and 10.6 % more wave cycles (SQ counters, r03 vs r04), 694.6 -> 709.5 us
     // in the driver's bench line (round-4 verdict).
-    if constexpr (ZR && MODE == 0) {
+    if constexpr (ZR && (MODE == 0 || MODE == 6)) {
         // (x ring, then b and x_in rings: contiguous from XS_OFF)
         static_assert(BS_OFF == XS_OFF + D * XR * TC && XI_OFF == BS_OFF + (HASB ? NB * T1 * TC : 0), "ring layout");
         constexpr int NZ = (XI_OFF + (XIN ? 2 * T1 * TC : 0) - XS_OFF) / 2;
@@ -947,10 +947,11 @@ int kron_v5_launch(int pmax, int epi, const KronPtrs& p, const KronGeom& g, cons
                  : diag_mode == 11 ? v5_launch_t<3, EPI_JACOBI0, 4, 4, 14>(p, g, tc, H, omega, st)
                                    : v5_launch_t<3, EPI_JACOBI0, 4, 5, 14>(p, g, tc, H, omega, st);
         }
-        if (diag_mode == 14) {   // stamped march (MODE 6): apply, or the Jacobi sweep's production build
+        if (diag_mode == 14) {   // stamped march (MODE 6): apply, or the Jacobi sweep's / J0's production build
             if (epi == EPI_APPLY) return v5_launch_t<3, EPI_APPLY, 4, 6, 6>(p, g, tc, H, omega, st);
             if (epi == EPI_JACOBI) return v5_launch_t<3, EPI_JACOBI, 4, 6, 6 | 64, true>(p, g, tc, H, omega, st);
-            set_error("v5 diag mode 14: apply / Jacobi only");
+            if (epi == EPI_JACOBI0) return v5_launch_t<3, EPI_JACOBI0, 4, 6, 14>(p, g, tc, H, omega, st);
+            set_error("v5 diag mode 14: apply / Jacobi / two sweeps from zero only");
             return 1;
         }
         if (diag_mode <= 2) {   // 1 = memory only, 2 = arithmetic only (apply)

@@ -768,7 +768,7 @@ static int op_geom(poms_op* o, int64_t zb, int64_t ze, KronGeom& g, int v = -1, 
 
 // variants whose Jacobi epilogue also accumulates x_out . b (v3 and v4 kernels)
 static bool fused_dot_ok(const poms_op* o) {
-    return o->form == FORM_STENCIL || (o->variant >= 4 && o->variant <= 11);
+    return o->form == FORM_STENCIL || (o->variant >= 4 && o->variant <= 11) || o->variant == 114;
 }
 
 
@@ -857,7 +857,7 @@ static int op_run(poms_op* o, int epi, double omega, const double* x, double* y,
         return 1;
     }
     if (epi == EPI_JACOBI0 && !(o->variant == 8 || o->variant == 9 || o->variant == 10 || o->variant == 11 ||
-                                (o->variant >= 110 && o->variant <= 112))) {
+                                (o->variant >= 110 && o->variant <= 112) || o->variant == 114)) {
         set_error("two sweeps from zero: kernel variant 8, 9 or 10 only");
         return 1;
     }
@@ -989,7 +989,7 @@ int poms_op_from_zero_supported(poms_op* op, int* yes) {
     const int64_t bytes = (int64_t)(op->L.n[0] + 2 * op->L.pads[0]) * row_geom(&op->L).s0 * 8;
     *yes = (op->ndim == 3 && op->form != FORM_STENCIL &&
             (op->variant == 8 || op->variant == 9 || op->variant == 10 || op->variant == 11 ||
-             (op->variant >= 110 && op->variant <= 112)) &&
+             (op->variant >= 110 && op->variant <= 112) || op->variant == 114) &&
             bytes < 0x7ffffff0LL) ? 1 : 0;
     return 0;
 }

@@ -48,7 +48,8 @@ def main():
     out = {}
     for kind in a.kinds.split(","):
         fn = {"apply": lambda: A.dot(x, out=y),
-              "jacobi": lambda: A.jacobi_sweep(b, x, y, 2.0 / 3.0, want_norm=False)}[kind]
+              "jacobi": lambda: A.jacobi_sweep(b, x, y, 2.0 / 3.0, want_norm=False),
+              "from_zero": lambda: A.jacobi_from_zero(b, y, 2.0 / 3.0, want_norm=True)}[kind]
         A.set_variant(10)
         for _ in range(3):
             fn()
