@@ -251,30 +251,46 @@ static int peer_ensure(poms_comm* c, int64_t cnt, int prev, int next, hipStream_
     (void)hipGetLastError();
     if (!blk) {
         POMS_HIP_CHECK(hipMalloc(reinterpret_cast<void**>(&blk), bytes));
-        if (!loop) POMS_HIP_CHECK(hipIpcGetMemHandle(&mine, blk));
+        if (!loop && hipIpcGetMemHandle(&mine, blk) != hipSuccess) {
+            (void)hipFree(blk);
+            set_error("peer transport: hipIpcGetMemHandle of the mailboxes failed");
+            return 1;
+        }
     }
-    POMS_HIP_CHECK(hipMemset(blk, 0, kPeerHdr));
-    POMS_HIP_CHECK(hipDeviceSynchronize());
+    if (hipMemset(blk, 0, kPeerHdr) != hipSuccess || hipDeviceSynchronize() != hipSuccess) {
+        (void)hipFree(blk);
+        set_error("peer transport: clearing the flag slots failed");
+        return 1;
+    }
     char* np = nullptr;
     char* nn = nullptr;
     bool pi = false, ni = false;
+    // on any failure below: nothing of the new block stays mapped or allocated (the old
+    // one, if any, stays in use)
+    auto fail = [&](const std::string& msg) {
+        if (pi && np) (void)hipIpcCloseMemHandle(np);
+        if (ni && nn) (void)hipIpcCloseMemHandle(nn);
+        (void)hipFree(blk);
+        if (!msg.empty()) set_error(msg);
+        return 1;
+    };
     if (loop) {
         np = prev >= 0 ? blk : nullptr;
         nn = next >= 0 ? blk : nullptr;
     } else {
         // each rank sends its handle and the capacity, so that a mismatch fails loudly
         struct Msg { hipIpcMemHandle_t h; int64_t cap; } m{mine, cap}, fp{}, fn{};
-        if (peer_swap_bytes(c, &m, &fp, &fn, (int)sizeof(Msg), prev, next)) return 1;
-        if ((prev >= 0 && fp.cap != cap) || (next >= 0 && fn.cap != cap)) {
-            set_error("peer transport: neighbours disagree on the mailbox size");
-            return 1;
-        }
+        if (peer_swap_bytes(c, &m, &fp, &fn, (int)sizeof(Msg), prev, next)) return fail("");
+        if ((prev >= 0 && fp.cap != cap) || (next >= 0 && fn.cap != cap))
+            return fail("peer transport: neighbours disagree on the mailbox size");
         if (prev >= 0) {
-            POMS_HIP_CHECK(hipIpcOpenMemHandle(reinterpret_cast<void**>(&np), fp.h, hipIpcMemLazyEnablePeerAccess));
+            if (hipIpcOpenMemHandle(reinterpret_cast<void**>(&np), fp.h, hipIpcMemLazyEnablePeerAccess) != hipSuccess)
+                return fail("peer transport: hipIpcOpenMemHandle of the previous rank's mailboxes failed");
             pi = true;
         }
         if (next >= 0) {
-            POMS_HIP_CHECK(hipIpcOpenMemHandle(reinterpret_cast<void**>(&nn), fn.h, hipIpcMemLazyEnablePeerAccess));
+            if (hipIpcOpenMemHandle(reinterpret_cast<void**>(&nn), fn.h, hipIpcMemLazyEnablePeerAccess) != hipSuccess)
+                return fail("peer transport: hipIpcOpenMemHandle of the next rank's mailboxes failed");
             ni = true;
         }
     }
