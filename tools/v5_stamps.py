@@ -28,6 +28,8 @@ def main():
     ap.add_argument("--kinds", default="apply,jacobi")
     ap.add_argument("--reps", type=int, default=5)
     ap.add_argument("--json", default="")
+    ap.add_argument("--chunk", type=int, default=0, help="axis-0 chunk (0: auto)")
+    ap.add_argument("--per-tile", action="store_true", help="mean workgroup duration per tile row / column / chunk")
     ap.add_argument("--stamp-variant", type=int, default=114,
                     help="114: the production march stamped; 116: the software-pipelined apply stamped")
     a = ap.parse_args()
@@ -42,6 +44,8 @@ def main():
     n = N + p
     V = StencilVectorSpace([n] * 3, [p] * 3, align=True)
     A = KronOperator.laplace(V, [M] * 3, [K] * 3)
+    if a.chunk:
+        A.set_chunk(a.chunk)
     x, b, y = V.zeros(), V.zeros(), V.zeros()
     V.interior(x._data).uniform_(-1, 1)
     V.interior(b._data).uniform_(-1, 1)
@@ -93,6 +97,21 @@ def main():
                    "cu_busy_us_median": float(np.median(busyv)), "cu_busy_us_max": float(busyv.max()),
                    "cu_busy_us_min": float(busyv.min()), "util": float(busyv.sum() / (len(busy) * span)),
                    "tail_us": float((wg_t1.max() - np.sort(wg_t1)[int(0.9 * nwg)]) / 100.0)}
+            # per tile row / column / chunk: mean workgroup duration (the default
+            # dispatch order: blockIdx -> XCD-contiguous bid -> t2 fastest, then t1, chunk)
+            if a.per_tile:
+                T2n, T1n = -(-(n) // 112), -(-(n) // 16)
+                nch = nwg // (T1n * T2n)
+                q, rr = nwg >> 3, nwg & 7
+                bids = []
+                for bx in range(nwg):
+                    xc, k = bx & 7, bx >> 3
+                    bids.append((xc * (q + 1) if xc < rr else rr * (q + 1) + (xc - rr) * q) + k)
+                bids = np.array(bids)
+                t2s, t1s, chs = bids % T2n, (bids // T2n) % T1n, bids // (T1n * T2n)
+                row["by_t1"] = {int(t): round(float(wg_dur[t1s == t].mean()), 1) for t in np.unique(t1s)}
+                row["by_t2"] = {int(t): round(float(wg_dur[t2s == t].mean()), 1) for t in np.unique(t2s)}
+                row["by_ch"] = {int(t): round(float(wg_dur[chs == t].mean()), 1) for t in np.unique(chs)}
             res.append(row)
             print(json.dumps({k: (round(v, 4) if isinstance(v, float) else v) for k, v in row.items()}), flush=True)
         out[kind] = res
