@@ -159,8 +159,15 @@ int poms_variant_built(int variant);
 /* Diagnostic: the per-wave clock stamps of the last v5 stamped launches (variant
  * 114, p = 3 apply / Jacobi sweep): n u64, 8 per wave in launch order (block x
  * waves + wave): cycles waiting for the wave's DMAs, in the plane barrier, the
- * rest; planes; start / end (100 MHz); XCC; CU.  The buffer is cleared after.   */
+ * rest; planes; start / end (100 MHz); XCC | tile << 8 (the tile's index in the
+ * default order); CU.  The buffer is cleared after.                            */
 int poms_diag_v5_stamps(uint64_t* host_out, int64_t n);
+/* Tuning: the order in which v5 launches start their tiles within each XCD's
+ * range -- 1 longest estimated first (default; POMS_V5_SCHED=0 in the environment
+ * starts with 0), 0 the default order.  Results are bitwise the same either way
+ * (the partial sums keep their slots).  mode < 0 only queries.  Returns the
+ * previous mode.                                                                */
+int poms_diag_v5_sched(int mode);
 /* Declare that the ghost edges / corners of axes 1 and 2 may hold non-zero data:
  * the vector is a block of a decomposition of axes 1 and 2 (spl Cart,
  * `sources/tests/test_kron_dot.py:51-55`), not an axis-0 slab whose ghosts off

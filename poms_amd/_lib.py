@@ -75,6 +75,7 @@ _SIGS = {
     "poms_op_set_variant": [_vp, _i],
     "poms_variant_built": [_i],
     "poms_diag_v5_stamps": [_vp, _i64],
+    "poms_diag_v5_sched": [_i],
     "poms_op_get_variant": [_vp, C.POINTER(_i)],
     "poms_op_kernel_variant": [_vp, _i, C.POINTER(_i)],
     "poms_op_last_variant": [_vp, C.POINTER(_i)],

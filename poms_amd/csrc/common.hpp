@@ -30,6 +30,7 @@ struct KronGeom {
     int z2_begin, z2_end;  // optional second plane range of the same launch (the other slab boundary)
     int tout;            // output columns per 64-column tile (v3 / v4 kernels; <= 64 - 2P)
     int order = 0;       // v5 / v6 tile order within an XCD: 0 = axis-2 tiles fastest, 1 = axis-1 tiles fastest
+    const int* sched = nullptr;   // v5: tile of each workgroup (kron_v5_sched), or null: the XCD-contiguous order
 };
 
 // Output planes [z0, z1) of axis-0 chunk `ch` (3D launches may cover two ranges).

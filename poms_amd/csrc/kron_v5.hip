@@ -38,7 +38,11 @@
 // DMA pair holding storage column 0 of storage row 0 fails the range check there).
 #include "common.hpp"
 
+#include <algorithm>
+#include <atomic>
 #include <cstdlib>
+#include <map>
+#include <mutex>
 #include <vector>
 
 namespace poms {
@@ -87,6 +91,16 @@ __device__ __forceinline__ void v5_wait_vm() {  // s_waitcnt vmcnt(N) (gfx9 enco
 
 __device__ __forceinline__ void v5_barrier() {
     __asm__ volatile("" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    __asm__ volatile("" ::: "memory");
+}
+
+// A barrier after this wave's own LDS stores (s_waitcnt lgkmcnt(0), then s_barrier).
+// __syncthreads() here would also wait vmcnt(0): every DMA in flight, the prefetched
+// planes included, drained at each plane.
+__device__ __forceinline__ void v5_lds_barrier() {
+    __asm__ volatile("" ::: "memory");
+    __builtin_amdgcn_s_waitcnt(15 | (7 << 4) | (0 << 8) | (3 << 14));
     __builtin_amdgcn_s_barrier();
     __asm__ volatile("" ::: "memory");
 }
@@ -195,11 +209,22 @@ kron_v5_kernel(const double* __restrict__ x, double* __restrict__ y, const doubl
     const int wv = __builtin_amdgcn_readfirstlane(tid >> 6);
 
     const int nblk = gridDim.x;
-    int bid;
-    {   // consecutive tiles on one XCD (round-robin dispatch over the 8 XCDs)
-        const int b = blockIdx.x, q = nblk >> 3, rr = nblk & 7, xcd = b & 7, k = b >> 3;
-        bid = (xcd < rr ? xcd * (q + 1) : rr * (q + 1) + (xcd - rr) * q) + k;
-    }
+    // tile of this workgroup: consecutive tiles on one XCD (round-robin dispatch over
+    // the 8 XCDs), taken in the host's order within each XCD's range when g.sched is
+    // set (longest tiles first, kron_v5_sched)
+    // (g.sched holds the tile of each workgroup, then the tile's slot in the default
+    // order: the partial sums keep that slot, so the reductions add in the same order
+    // whatever the dispatch order.  Both are scalar loads where they are used, not
+    // SGPRs held through the march.)
+    auto tile_of = [&]() -> int {
+        const int b = blockIdx.x, q = nblk >> 3, rr = nblk & 7, x = b & 7;
+        return g.sched != nullptr ? __builtin_amdgcn_readfirstlane(g.sched[b])
+                                  : (x < rr ? x * (q + 1) : rr * (q + 1) + (x - rr) * q) + (b >> 3);
+    };
+    auto slot_of = [&]() -> int {
+        return g.sched != nullptr ? __builtin_amdgcn_readfirstlane(g.sched[gridDim.x + blockIdx.x]) : (int)blockIdx.x;
+    };
+    int bid = tile_of();
     const int TO = g.tout;
     // tile order within an XCD's contiguous range: t1 fastest (g.order = 1: the
     // tiles above and below, which read each other's halo rows, run together on one
@@ -480,7 +505,7 @@ kron_v5_kernel(const double* __restrict__ x, double* __restrict__ y, const doubl
                                 *(d2*)(xsl + q * TC + 2 * lane) = v;
                             }
                         }
-                        __syncthreads();
+                        v5_lds_barrier();   // (not __syncthreads: that drained the DMAs in flight)
                     }
                 }
                 // ---- axis 1: u = F1a x, v = F1b x on this wave's row, 2 columns per lane
@@ -761,7 +786,7 @@ kron_v5_kernel(const double* __restrict__ x, double* __restrict__ y, const doubl
             __asm__ volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(xcc));
             const unsigned long long v = lane == 0 ? st_wait : lane == 1 ? st_bar : lane == 2 ? st_rest
                                        : lane == 3 ? (unsigned long long)nplanes : lane == 4 ? st_t0
-                                       : lane == 5 ? t1 : lane == 6 ? (unsigned long long)(xcc & 15)
+                                       : lane == 5 ? t1 : lane == 6 ? ((unsigned long long)(xcc & 15) | ((unsigned long long)tile_of() << 8))
                                        : (unsigned long long)(((hw >> 8) & 15) | (((hw >> 13) & 7) << 4));
             g_v5_stamps[slot + lane] = v;
         }
@@ -788,7 +813,7 @@ kron_v5_kernel(const double* __restrict__ x, double* __restrict__ y, const doubl
             if (tid == 0) {
                 double s = 0.0;
                 for (int w = 0; w < NW; ++w) s += lds[RED_OFF + w];
-                partial[blockIdx.x] = s;
+                partial[slot_of()] = s;
             }
         }
         if (partial2 != nullptr) {
@@ -800,7 +825,7 @@ kron_v5_kernel(const double* __restrict__ x, double* __restrict__ y, const doubl
             if (tid == 0) {
                 double s = 0.0;
                 for (int w = 0; w < NW; ++w) s += lds[RED_OFF + w];
-                partial2[blockIdx.x] = s;
+                partial2[slot_of()] = s;
             }
         }
     }
@@ -928,8 +953,95 @@ void kron_v5_tile(int pmax, bool aligned, int* H, int* TO) {
     }
 }
 
-int kron_v5_launch(int pmax, int epi, const KronPtrs& p, const KronGeom& g, const ToepConst& tc, int H,
+// Dispatch order of a launch's tiles (KronGeom::sched).  The hardware hands
+// workgroup b to XCD b % 8, and each XCD starts its workgroups in order, one per CU
+// as CUs free up (round-robin over its 4 shader engines; r05 stamps,
+// tools/v5_stamps.py --raw).  The default order gives each XCD a contiguous range
+// of tiles; a range that ends on its slowest tiles -- at 515^3 the two-sweeps-from-
+// zero tile rows off the axis-1 Toeplitz interior, 1.2-1.5x the others -- runs them
+// in the grid's last round and stretches its tail.  This table keeps each XCD's
+// range and starts its tiles in order of decreasing estimated duration (stable:
+// equal tiles keep the default order, neighbours together on the XCD's L2).  The
+// estimate is the tile's planes (halo included) times the measured factors of its
+// slow paths.  Built once per geometry and device, outside any graph capture (a
+// launch during a capture that has no table yet keeps the default order).
+// POMS_V5_SCHED=0 turns it off.
+static std::atomic<int> g_v5_sched{-1};
+
+int kron_v5_set_sched(int mode) {   // poms_diag_v5_sched
+    if (g_v5_sched.load() < 0) {
+        const char* e = getenv("POMS_V5_SCHED");
+        g_v5_sched = e ? (atoi(e) ? 1 : 0) : 1;
+    }
+    const int prev = g_v5_sched.load();
+    if (mode >= 0) g_v5_sched = mode ? 1 : 0;
+    return prev;
+}
+
+static const int* v5_sched(int P, int epi, const KronGeom& g, const ToepConst& tc, hipStream_t st) {
+    const int mode = kron_v5_set_sched(-1);
+    const int nblk = g.tiles2 * g.tiles1 * g.nchunks;
+    if (mode == 0 || nblk < 16) return nullptr;
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess) return nullptr;
+    const std::vector<int> key = {dev, P, epi, g.n0, g.n1, g.n2, g.g0, g.z_begin, g.z_end, g.z2_begin, g.z2_end,
+                                  g.chunk, g.nch1, g.nchunks, g.tiles1, g.tiles2, g.tout, g.order,
+                                  tc.lo0, tc.hi0, tc.lo1, tc.hi1, tc.lo2, tc.hi2};
+    static std::mutex mu;
+    static std::map<std::vector<int>, int*> cache;
+    std::lock_guard<std::mutex> lk(mu);
+    auto it = cache.find(key);
+    if (it != cache.end()) return it->second;
+    hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
+    if (hipStreamIsCapturing(st, &cs) != hipSuccess || cs != hipStreamCaptureStatusNone) return nullptr;
+    const int T1 = v5_waves(P, epi), TO = g.tout;
+    const bool j0 = epi == EPI_JACOBI0;
+    std::vector<double> w(nblk);
+    for (int b = 0; b < nblk; ++b) {
+        int r = b, t1, t2;
+        if (g.order) { t1 = r % g.tiles1; r /= g.tiles1; t2 = r % g.tiles2; r /= g.tiles2; }
+        else { t2 = r % g.tiles2; r /= g.tiles2; t1 = r % g.tiles1; r /= g.tiles1; }
+        const int ch = r;
+        int z0, z1;   // (chunk_planes)
+        if (ch < g.nch1) { z0 = g.z_begin + ch * g.chunk; z1 = std::min(z0 + g.chunk, g.z_end); }
+        else { z0 = g.z2_begin + (ch - g.nch1) * g.chunk; z1 = std::min(z0 + g.chunk, g.z2_end); }
+        const int r0 = t1 * T1, c0 = t2 * TO;
+        double f = 1.0;
+        // measured (r05 stamps, 515^3 p = 3): general axis-2 column tiles +11 % (J0) / +5 %;
+        // J0 tiles that scale the ring in place +20 %, the partial last tile row +50 %
+        if (!(c0 >= tc.lo2 && std::min(c0 + TO, g.n2) <= tc.hi2)) f += j0 ? 0.11 : 0.05;
+        if (j0 && !(r0 - P >= tc.lo1 && r0 + T1 + P <= tc.hi1)) f += 0.2;
+        if (j0 && r0 + T1 > g.n1) f += 0.3;
+        w[b] = (double)(z1 - z0 + 2 * P) * f;
+    }
+    // [0, nblk): the tile of workgroup b; [nblk, 2 nblk): that tile's slot in the
+    // default order (workgroup k * 8 + x runs tile lo(x) + k)
+    std::vector<int> h(2 * (size_t)nblk);
+    const int q = nblk >> 3, rr = nblk & 7;
+    for (int x = 0; x < 8; ++x) {
+        const int lo = x < rr ? x * (q + 1) : rr * (q + 1) + (x - rr) * q, cnt = x < rr ? q + 1 : q;
+        std::vector<int> idx(cnt);
+        for (int k = 0; k < cnt; ++k) idx[k] = lo + k;
+        std::stable_sort(idx.begin(), idx.end(), [&](int a, int b) { return w[a] > w[b]; });
+        for (int k = 0; k < cnt; ++k) {
+            h[k * 8 + x] = idx[k];
+            h[nblk + k * 8 + x] = (idx[k] - lo) * 8 + x;
+        }
+    }
+    int* d = nullptr;
+    if (hipMalloc(&d, h.size() * sizeof(int)) != hipSuccess) return nullptr;
+    if (hipMemcpy(d, h.data(), h.size() * sizeof(int), hipMemcpyHostToDevice) != hipSuccess) {
+        (void)hipFree(d);
+        return nullptr;
+    }
+    cache[key] = d;
+    return d;
+}
+
+int kron_v5_launch(int pmax, int epi, const KronPtrs& p, const KronGeom& g_in, const ToepConst& tc, int H,
                    double omega, hipStream_t st, int diag_mode) {
+    KronGeom g = g_in;
+    g.sched = v5_sched(pmax, epi, g_in, tc, st);
     if (H < pmax || (H & 1) || (g.tout & 1) || H + g.tout + pmax > 128) {
         set_error("v5: bad tile geometry");
         return 1;

@@ -29,6 +29,7 @@ int kron_v7_launch(int pmax, int epi, const KronPtrs& p, const KronGeom& g, cons
                    hipStream_t st, int diag, bool dry = false);
 int kron_v7_built();
 int kron_v5_stamps(unsigned long long* host, int64_t n);
+int kron_v5_set_sched(int mode);
 int kron_v7_tiles(int pmax, int n1, int n2);
 int kron_tile_rows();
 int kron_tile_cols();
@@ -602,6 +603,8 @@ int poms_diag_v5_stamps(uint64_t* host_out, int64_t n) {
     if (!host_out) { set_error("poms_diag_v5_stamps: null argument"); return 1; }
     return kron_v5_stamps(reinterpret_cast<unsigned long long*>(host_out), n);
 }
+
+int poms_diag_v5_sched(int mode) { return kron_v5_set_sched(mode); }
 
 int poms_variant_built(int variant) {
     if (variant == 11 || (variant >= 121 && variant <= 124)) return kron_v7_built();

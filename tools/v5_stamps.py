@@ -30,6 +30,7 @@ def main():
     ap.add_argument("--json", default="")
     ap.add_argument("--chunk", type=int, default=0, help="axis-0 chunk (0: auto)")
     ap.add_argument("--per-tile", action="store_true", help="mean workgroup duration per tile row / column / chunk")
+    ap.add_argument("--raw", default="", help="save per-workgroup start/end/XCD/CU of each rep to this .npz")
     ap.add_argument("--stamp-variant", type=int, default=114,
                     help="114: the production march stamped; 116: the software-pipelined apply stamped")
     a = ap.parse_args()
@@ -49,7 +50,7 @@ def main():
     x, b, y = V.zeros(), V.zeros(), V.zeros()
     V.interior(x._data).uniform_(-1, 1)
     V.interior(b._data).uniform_(-1, 1)
-    out = {}
+    out, raws = {}, {}
     for kind in a.kinds.split(","):
         fn = {"apply": lambda: A.dot(x, out=y),
               "jacobi": lambda: A.jacobi_sweep(b, x, y, 2.0 / 3.0, want_norm=False),
@@ -73,6 +74,8 @@ def main():
             s = np.frombuffer(buf, dtype=np.uint64).reshape(nw, 8).astype(np.float64)
             s = s[s[:, 3] > 0]   # waves that ran
             wait, bar, rest, planes, t0, t1, xcc, cu = s.T
+            tile = np.floor(xcc / 256.0)   # the workgroup's tile (default-order index), stamped above the XCD id
+            xcc = xcc - 256.0 * tile
             tot = wait + bar + rest
             wall_us = e0.elapsed_time(e1) * 1e3
             # workgroups: 16 waves each, consecutive rows
@@ -97,25 +100,24 @@ def main():
                    "cu_busy_us_median": float(np.median(busyv)), "cu_busy_us_max": float(busyv.max()),
                    "cu_busy_us_min": float(busyv.min()), "util": float(busyv.sum() / (len(busy) * span)),
                    "tail_us": float((wg_t1.max() - np.sort(wg_t1)[int(0.9 * nwg)]) / 100.0)}
-            # per tile row / column / chunk: mean workgroup duration (the default
-            # dispatch order: blockIdx -> XCD-contiguous bid -> t2 fastest, then t1, chunk)
+            # per tile row / column / chunk: mean workgroup duration (the stamped tile
+            # index: t2 fastest, then t1, chunk -- the default POMS_TILE_ORDER)
             if a.per_tile:
                 T2n, T1n = -(-(n) // 112), -(-(n) // 16)
-                nch = nwg // (T1n * T2n)
-                q, rr = nwg >> 3, nwg & 7
-                bids = []
-                for bx in range(nwg):
-                    xc, k = bx & 7, bx >> 3
-                    bids.append((xc * (q + 1) if xc < rr else rr * (q + 1) + (xc - rr) * q) + k)
-                bids = np.array(bids)
+                bids = tile[: nwg * 16].reshape(nwg, 16)[:, 0].astype(np.int64)
                 t2s, t1s, chs = bids % T2n, (bids // T2n) % T1n, bids // (T1n * T2n)
                 row["by_t1"] = {int(t): round(float(wg_dur[t1s == t].mean()), 1) for t in np.unique(t1s)}
                 row["by_t2"] = {int(t): round(float(wg_dur[t2s == t].mean()), 1) for t in np.unique(t2s)}
                 row["by_ch"] = {int(t): round(float(wg_dur[chs == t].mean()), 1) for t in np.unique(chs)}
+            if a.raw:
+                cus = (xcc + 0)[: nwg * 16].reshape(nwg, 16)[:, 0], cu[: nwg * 16].reshape(nwg, 16)[:, 0]
+                raws[f"{kind}_{r}"] = np.stack([wg_t0, wg_t1, cus[0], cus[1], tile[: nwg * 16].reshape(nwg, 16)[:, 0]])
             res.append(row)
             print(json.dumps({k: (round(v, 4) if isinstance(v, float) else v) for k, v in row.items()}), flush=True)
         out[kind] = res
     A.set_variant(8)
+    if a.raw:
+        np.savez(a.raw, **raws)
     if a.json:
         Path(a.json).write_text(json.dumps(out, indent=1))
 
