@@ -508,6 +508,10 @@ kron_v5_kernel(const double* __restrict__ x, double* __restrict__ y, const doubl
                         v5_lds_barrier();   // (not __syncthreads: that drained the DMAs in flight)
                     }
                 }
+                // A wave whose output row lies past the slab's last row (13 of the 16 in
+                // the partial last tile row at 515^3) only issues its DMAs and takes the
+                // barriers: its points are never stored, and its sums are not kept.
+                if (MODE != 2 && !row_ok) continue;
                 // ---- axis 1: u = F1a x, v = F1b x on this wave's row, 2 columns per lane
                 const double* xs = lds + XS_OFF + (t % D) * XR * TC + 2 * lane;
                 d2 xv[W];
