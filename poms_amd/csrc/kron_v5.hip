@@ -38,6 +38,8 @@
 // DMA pair holding storage column 0 of storage row 0 fails the range check there).
 #include "common.hpp"
 
+#include <hip/hip_ext.h>
+
 #include <algorithm>
 #include <atomic>
 #include <cstdlib>
@@ -838,6 +840,19 @@ kron_v5_kernel(const double* __restrict__ x, double* __restrict__ y, const doubl
 #undef T2A
 #undef T2B
 
+// Timing events for the next v5 launch of this thread (op_run's sampled timing):
+// passed to hipExtLaunchKernel, which stamps the dispatch's own start and end.
+static thread_local hipEvent_t t_v5_ev0 = nullptr, t_v5_ev1 = nullptr;
+static thread_local bool t_v5_ev_used = false;
+
+void kron_v5_set_launch_events(hipEvent_t e0, hipEvent_t e1) {
+    t_v5_ev0 = e0;
+    t_v5_ev1 = e1;
+    t_v5_ev_used = false;
+}
+
+bool kron_v5_launch_events_used() { return t_v5_ev_used; }
+
 template <int P, int EPI, int D, int MODE, int CP, bool XH, bool ST16, bool JDOT, bool SAME12>
 static int v5_launch_t2(const KronPtrs& p, const KronGeom& g, const ToepConst& tc, int H, double omega,
                         hipStream_t st) {
@@ -857,6 +872,14 @@ static int v5_launch_t2(const KronPtrs& p, const KronGeom& g, const ToepConst& t
         return 1;
     }
     const int nblk = g.tiles2 * g.tiles1 * g.nchunks;
+    if (t_v5_ev0 != nullptr) {   // a timed launch: the events on the dispatch itself
+        hipExtLaunchKernelGGL((kron_v5_kernel<P, EPI, D, MODE, CP, XH, ST16, JDOT, SAME12>), dim3(nblk),
+                              dim3(64 * v5_waves(P, EPI)), 0, st, t_v5_ev0, t_v5_ev1, 0, p.x, p.y, p.b, p.a0t,
+                              p.b0t, p.a1, p.b1, p.a2, p.b2, p.partial, p.partial2, p.rdiag0, g, tc, H, omega);
+        t_v5_ev0 = t_v5_ev1 = nullptr;
+        t_v5_ev_used = true;
+        return 0;
+    }
     hipLaunchKernelGGL((kron_v5_kernel<P, EPI, D, MODE, CP, XH, ST16, JDOT, SAME12>), dim3(nblk), dim3(64 * v5_waves(P, EPI)), 0, st, p.x,
                        p.y, p.b, p.a0t, p.b0t, p.a1, p.b1, p.a2, p.b2, p.partial, p.partial2, p.rdiag0, g, tc, H, omega);
     return 0;

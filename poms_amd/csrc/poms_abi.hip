@@ -30,6 +30,8 @@ int kron_v7_launch(int pmax, int epi, const KronPtrs& p, const KronGeom& g, cons
 int kron_v7_built();
 int kron_v5_stamps(unsigned long long* host, int64_t n);
 int kron_v5_set_sched(int mode);
+void kron_v5_set_launch_events(hipEvent_t e0, hipEvent_t e1);
+bool kron_v5_launch_events_used();
 int kron_v7_tiles(int pmax, int n1, int n2);
 int kron_tile_rows();
 int kron_tile_cols();
@@ -916,6 +918,7 @@ static int op_run(poms_op* o, int epi, double omega, const double* x, double* y,
     KronPtrs p{x, y, b, o->a0t, o->b0t, o->a1, o->b1, o->a2, o->b2, want_norm ? pn : nullptr,
                want_dot ? pd : nullptr, o->rdiag0};
     poms_op::TimedLaunch* tlh = nullptr;
+    bool tl_ext = false;
     if (o->timing && (o->t_epi < 0 || o->t_epi == epi) && (o->t_seen++ % o->t_every) == 0) {
         // events on the launch stream around this launch (a sample: every t_every-th)
         if (o->tl_used == o->tl.size()) {
@@ -927,7 +930,17 @@ static int op_run(poms_op* o, int epi, double omega, const double* x, double* y,
         tlh = &o->tl[o->tl_used++];
         tlh->epi = epi;
         tlh->ndof = (int64_t)((ze - zb) + (ze2 - zb2)) * g.n1 * g.n2;
-        POMS_HIP_CHECK(timing_record(tlh->e0, as_stream(stream)));
+        // v5 outside a capture: the events ride on the kernel's own dispatch
+        // (hipExtLaunchKernel start / stop), i.e. the kernel's execution time as
+        // rocprofv3 reports it; otherwise event records before and after the launch
+        hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
+        POMS_HIP_CHECK(hipStreamIsCapturing(as_stream(stream), &cs));
+        if (v == 10 && cs == hipStreamCaptureStatusNone) {
+            kron_v5_set_launch_events(tlh->e0, tlh->e1);
+            tl_ext = true;
+        } else {
+            POMS_HIP_CHECK(timing_record(tlh->e0, as_stream(stream)));
+        }
     }
     const int rc = v == 11
         ? kron_v7_launch(o->pmax, epi, p, g, o->tc, omega, as_stream(stream), v7_diag)
@@ -939,7 +952,11 @@ static int op_run(poms_op* o, int epi, double omega, const double* x, double* y,
         ? kron_v4_launch(o->pmax, o->ndim == 3, o->form, epi, p, g, o->tc, omega, as_stream(stream),
                          v == 7 ? 0 : v - 91)
         : kron_v3_launch(v, o->pmax, o->ndim == 3, o->form, epi, p, g, o->tc, omega, as_stream(stream));
-    if (tlh) POMS_HIP_CHECK(timing_record(tlh->e1, as_stream(stream)));
+    if (tl_ext && !kron_v5_launch_events_used()) {   // (the v5 launch failed before its dispatch)
+        kron_v5_set_launch_events(nullptr, nullptr);
+        if (!rc) { set_error("v5: timed launch did not take its events"); return 1; }
+    }
+    if (tlh && !tl_ext) POMS_HIP_CHECK(timing_record(tlh->e1, as_stream(stream)));
     if (rc) return 1;
     POMS_HIP_CHECK(hipGetLastError());
     o->last_partials = (want_norm || want_dot) ? nblk : 0;
