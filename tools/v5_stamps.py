@@ -112,6 +112,9 @@ def main():
             if a.raw:
                 cus = (xcc + 0)[: nwg * 16].reshape(nwg, 16)[:, 0], cu[: nwg * 16].reshape(nwg, 16)[:, 0]
                 raws[f"{kind}_{r}"] = np.stack([wg_t0, wg_t1, cus[0], cus[1], tile[: nwg * 16].reshape(nwg, 16)[:, 0]])
+                # per wave (workgroup x wave): cycles waiting for own DMAs, in the barrier, the rest
+                raws[f"{kind}_{r}_waves"] = np.stack([wait[: nwg * 16].reshape(nwg, 16), bar[: nwg * 16].reshape(nwg, 16),
+                                                      rest[: nwg * 16].reshape(nwg, 16)])
             res.append(row)
             print(json.dumps({k: (round(v, 4) if isinstance(v, float) else v) for k, v in row.items()}), flush=True)
         out[kind] = res
