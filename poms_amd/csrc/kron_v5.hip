@@ -459,6 +459,12 @@ kron_v5_kernel(const double* __restrict__ x, double* __restrict__ y, const doubl
                     st_wait += st_b - st_a;
                 }
                 v5_barrier();
+                // Every wave starts the plane at a high issue priority and drops it for
+                // the plane's axis-0 scatter and epilogue.  A SIMD's four waves otherwise
+                // run in age order: the oldest finishes each plane first and then waits
+                // ~41 % of its cycles in the barrier, the youngest ~5 % (stamps), and the
+                // end of every plane runs on one wave, its latencies exposed.
+                __builtin_amdgcn_s_setprio(3);
                 if constexpr (STAMP) {
                     st_prev = __builtin_amdgcn_s_memtime();
                     st_bar += st_prev - st_b;
@@ -624,6 +630,7 @@ kron_v5_kernel(const double* __restrict__ x, double* __restrict__ y, const doubl
                     dd[0] = d[0]; dd[1] = d[1];
                 }
 
+                __builtin_amdgcn_s_setprio(0);
                 // ---- axis 0: scatter into the rotating slots (column gm of the factors;
                 // scalar loads -- taking the Toeplitz constants from the kernel arguments
                 // instead ran slower: they no longer fit the SGPRs and are re-loaded)
