@@ -1,3 +1,8 @@
+#!/bin/bash
+# Round-5 experiment record: the three POMS_V5_PRIO runtime modes of a one-off build
+# (0 none, 1 priority dropped after the axis-1 pass, 2 dropped before the axis-0
+# scatter), interleaved in alternating processes.  Mode 2 is now compiled in
+# unconditionally and the variable is gone (profiles/r05/prio/runtime_modes.log).
 set -u
 O=gpurun_out/s33; mkdir -p $O
 for r in 1 2; do
