@@ -1062,10 +1062,21 @@ static const int* v5_sched(int P, int epi, const KronGeom& g, const ToepConst& t
             h[nblk + k * 8 + x] = (idx[k] - lo) * 8 + x;
         }
     }
+    // stream-ordered allocation and upload on the launch's stream (no device-wide
+    // synchronisation: another stream may hold a peer exchange waiting on a
+    // neighbour); the host copy stays alive with the table
+    static std::map<std::vector<int>, std::vector<int>> host;
     int* d = nullptr;
-    if (hipMalloc(&d, h.size() * sizeof(int)) != hipSuccess) return nullptr;
-    if (hipMemcpy(d, h.data(), h.size() * sizeof(int), hipMemcpyHostToDevice) != hipSuccess) {
-        (void)hipFree(d);
+    if (hipMallocAsync(reinterpret_cast<void**>(&d), h.size() * sizeof(int), st) != hipSuccess) {
+        (void)hipGetLastError();
+        return nullptr;
+    }
+    std::vector<int>& hk = host[key];
+    hk = std::move(h);
+    if (hipMemcpyAsync(d, hk.data(), hk.size() * sizeof(int), hipMemcpyHostToDevice, st) != hipSuccess) {
+        (void)hipGetLastError();
+        (void)hipFreeAsync(d, st);
+        host.erase(key);
         return nullptr;
     }
     cache[key] = d;
