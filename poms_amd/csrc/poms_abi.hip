@@ -825,12 +825,14 @@ static int resolve_variant(const poms_op* o, int epi) {
     if (v == 8) {
         const bool plain = epi == EPI_APPLY || epi == EPI_RESID || epi == EPI_JACOBI;
         if (o->ndim == 3 && v5_ok(o) &&
-            (epi != EPI_JACOBI0 || o->pmax <= 2 || (o->pmax == 3 && same_toeplitz12(o))))
+            (epi != EPI_JACOBI0 || o->pmax != 3 || same_toeplitz12(o)))
             v = 10;   // v5: kernel_bench at 515^3 p = 3; 8-wave tiles at 256^3 p = 4, 5
                       // (profiles/r02/configs/kb_p5_waves8.log: apply 231 -> 185 us at p = 5);
-                      // sweeps from zero at p <= 2 (8-wave tiles) and at p = 3 (16-wave
-                      // tiles, 930 vs 945 us for v3 at 515^3, profiles/r02/j0_16wave/) where
-                      // axes 1 and 2 share their rows (the other build spills)
+                      // sweeps from zero at p <= 2 and p = 4, 5 (8-wave tiles; at 256^3
+                      // p = 4 208 vs 291 us for v3, p = 5 261 vs 428 us,
+                      // profiles/r05/late/kb_p45_j0.log) and at p = 3 (16-wave tiles, 930 vs
+                      // 945 us for v3 at 515^3, profiles/r02/j0_16wave/) where axes 1 and 2
+                      // share their rows (the other build spills)
         else if (o->ndim == 3)
             v = ((epi == EPI_APPLY && o->pmax >= 3) || (plain && o->pmax >= 4)) ? 7 : 9;
         else if (epi == EPI_JACOBI && o->pmax <= 3)
