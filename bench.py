@@ -37,7 +37,7 @@ sys.path.insert(0, str(ROOT))
 
 METRIC = "V-cycle DOF/s + Kron-SpMV GB/s vs HBM roofline, 3D Poisson p=3"
 HBM_PEAK_GBPS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md)
-KERNEL_NAMES = {11: "kron_v7_kernel", 10: "kron_v5_kernel", 9: "kron_v3_kernel(flat)", 7: "kron_v4_kernel", 4: "kron_v3_kernel"}
+KERNEL_NAMES = {10: "kron_v5_kernel", 9: "kron_v3_kernel(flat)", 7: "kron_v4_kernel", 4: "kron_v3_kernel"}
 
 
 def parse():

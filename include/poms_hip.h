@@ -141,20 +141,13 @@ int poms_op_set_tile_cols(poms_op* op, int cols);
  *       (3D FORM_SUM, arrays < 2 GiB, not at odd p with ghost corners; other
  *       operators, and two-sweeps-from-zero at p = 3 with distinct axis-1 /
  *       axis-2 Toeplitz rows, run variant 9);
- *  11 = v7: flat lane mapping (lane -> row, column pair of an R x 112 tile),
- *       axis-2 windows read from LDS instead of lane shifts, one barrier per
- *       plane (p = 3 apply on the line-aligned layout with uniform-knot factors;
- *       elsewhere it runs v5 -- poms_op_last_variant tells which ran).  v7 is
- *       experimental (slower than v5) and compiled only with POMS_WITH_V7=1;
- *       without it variant 11 runs v5 (poms_variant_built(11) == 0);
  *  90-114 = diagnostic / tuning builds (memory-only, compute-only, cache policies;
  *  110-112: two sweeps from zero without sums / x1 scaling, timing only; 114:
- *  clock-stamped apply / Jacobi sweep, poms_diag_v5_stamps);
- *  121-124 = v7 memory only / arithmetic only (timing only) / non-temporal x
- *  DMAs / y stores with the default cache policy.
- * Variants 4-11 need storage pads == pmax on every used axis.                  */
+ *  clock-stamped apply / Jacobi sweep, poms_diag_v5_stamps).
+ * (11, the experimental v7 kernel, was removed in round 6.)
+ * Variants 4-10 need storage pads == pmax on every used axis.                  */
 int poms_op_set_variant(poms_op* op, int variant);
-/* 1 if the kernels of `variant` are compiled into this library, else 0 (11: v7). */
+/* 1 if the kernels of `variant` are compiled into this library, else 0. */
 int poms_variant_built(int variant);
 /* Diagnostic: the per-wave clock stamps of the last v5 stamped launches (variant
  * 114, p = 3 apply / Jacobi sweep): n u64, 8 per wave in launch order (block x
@@ -444,6 +437,14 @@ int poms_halo_finish(poms_comm* comm, void* stream);
 int poms_comm_set_peer(poms_comm* comm, int enable, int wgs);
 int poms_comm_peer_reserve(poms_comm* comm, int64_t cnt, int prev, int next);
 int poms_comm_peer_status(poms_comm* comm, int* active, int* fine_grained, int* timed_out);
+/* Fails (returns 1, poms_last_error says why) if a peer exchange of this
+ * communicator has timed out: its ghost planes, and every result computed from
+ * them, are invalid.  No synchronisation (reads a host-mapped flag the exchange
+ * kernel sets); poms_comm_wait and poms_pcg_jacobi run it themselves.  The peer
+ * mailboxes cannot be rebuilt (a larger exchange, other neighbours, set_peer off or
+ * another wgs) once an exchange was captured into a graph: that call fails too.
+ * Neighbours must use the same wgs (checked when the mailboxes are built).      */
+int poms_comm_check(poms_comm* comm);
 /* In-place global sum of `count` doubles after the work queued on `stream`;
  * wait_back: `stream` waits for the result, else it is ready on the
  * communication stream only.                                                  */

@@ -97,6 +97,7 @@ _SIGS = {
     "poms_comm_set_peer": [_vp, _i, _i],
     "poms_comm_peer_reserve": [_vp, _i64, _i, _i],
     "poms_comm_peer_status": [_vp, C.POINTER(_i), C.POINTER(_i), C.POINTER(_i)],
+    "poms_comm_check": [_vp],
     "poms_allreduce_sum": [_vp, _vp, _i64, _vp, _i],
     "poms_comm_slot": [_vp, _pp, C.POINTER(_i)],
     "poms_allreduce_to_host": [_vp, _i, _i, _vp, _vp],

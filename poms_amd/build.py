@@ -16,7 +16,7 @@ HERE = Path(__file__).resolve().parent
 CSRC = HERE / "csrc"
 LIB = HERE / "libpoms_hip.so"
 OBJ = HERE / "_obj"
-SOURCES = ["kron_fused.hip", "kron_dpp.hip", "kron_v4.hip", "kron_v5.hip", "kron_v7.hip", "vec_ops.hip", "transfer.hip", "kron_solve.hip", "stencil_general.hip", "comm.hip", "poms_abi.hip"]
+SOURCES = ["kron_fused.hip", "kron_dpp.hip", "kron_v4.hip", "kron_v5.hip", "vec_ops.hip", "transfer.hip", "kron_solve.hip", "stencil_general.hip", "comm.hip", "poms_abi.hip"]
 ARCH = os.environ.get("POMS_OFFLOAD_ARCH", "gfx950")
 
 
@@ -44,17 +44,8 @@ def _needs(obj: Path, src: Path) -> bool:
     return any(d.stat().st_mtime > obj.stat().st_mtime for d in deps if d.exists())
 
 
-# v7 (kron_v7.hip, variant 11) is an experimental kernel, slower than v5: the product
-# library compiles only its stubs (variant 11 then runs v5); POMS_WITH_V7=1 builds it.
-WITH_V7 = os.environ.get("POMS_WITH_V7", "0") == "1"
-
-
 def _obj_name(s: str) -> str:
-    return s + (".o" if s != "kron_v7.hip" or not WITH_V7 else ".full.o")
-
-
-def _defines(s: str) -> list[str]:
-    return ["-DPOMS_V7_STUB"] if s == "kron_v7.hip" and not WITH_V7 else []
+    return s + ".o"
 
 
 def build(verbose: bool = False, force: bool = False, jobs: int = 4) -> Path:
@@ -68,7 +59,7 @@ def build(verbose: bool = False, force: bool = False, jobs: int = 4) -> Path:
 
     def _compile(pair):
         src, obj = pair
-        cmd = [hipcc, *_flags(), *_defines(src.name), "-I", str(HERE.parent / "include"), "-c", str(src), "-o",
+        cmd = [hipcc, *_flags(), "-I", str(HERE.parent / "include"), "-c", str(src), "-o",
                str(obj)]
         if verbose:
             print(" ".join(cmd), flush=True)
@@ -82,7 +73,7 @@ def build(verbose: bool = False, force: bool = False, jobs: int = 4) -> Path:
             if verbose:
                 print(f"compiled {name}", flush=True)
     objs = [str(OBJ / _obj_name(s)) for s in SOURCES]
-    stamp = OBJ / "link.cfg"   # relink when the set of objects changes (POMS_WITH_V7)
+    stamp = OBJ / "link.cfg"   # relink when the set of objects changes
     cfg = " ".join(objs)
     if force or todo or not LIB.exists() or not stamp.exists() or stamp.read_text() != cfg:
         tmp = LIB.with_suffix(".so.tmp")

@@ -90,6 +90,11 @@ struct poms_comm {
     char* pnext = nullptr;
     bool pprev_ipc = false, pnext_ipc = false;
     bool peer_fine = false;           // own block is fine-grained (coherent) device memory
+    uint64_t* peer_status = nullptr;  // timeout flag of the exchange kernel (pinned, device-mapped host memory)
+    // an exchange was queued while a stream was being captured: graphs now hold raw
+    // pointers into the mailbox block and its flag slots, so the block may no longer be
+    // rebuilt or released (advisor, round 5)
+    bool peer_captured = false;
 };
 
 #define POMS_NCCL_CHECK(expr)                                                    \
@@ -221,9 +226,32 @@ static int peer_swap_bytes(poms_comm* c, const void* mine, void* from_prev, void
 // missing, too small or exchanged with other neighbours.  Collective over the two
 // neighbours (every rank issues the same exchanges in the same order, so all of
 // them rebuild at the same call); never inside a capture.
+// A timed-out exchange (a neighbour lagged by more than 20 s) left stale or partly
+// written mailbox contents in the ghost planes: every later result is invalid.
+static int peer_check(poms_comm* c) {
+    if (c->peer_status && __atomic_load_n(c->peer_status, __ATOMIC_ACQUIRE) != 0) {
+        set_error("peer transport: a ghost exchange timed out waiting for a neighbour (> 20 s); "
+                  "its ghost planes, and every result computed from them, are invalid");
+        return 1;
+    }
+    return 0;
+}
+
 static int peer_ensure(poms_comm* c, int64_t cnt, int prev, int next, hipStream_t st) {
     if (c->pblk && cnt <= c->peer_cap && prev == c->peer_prev && next == c->peer_next) return 0;
     if (refuse_in_capture(st, "peer transport setup (first exchange of this size)")) return 1;
+    if (c->pblk && c->peer_captured) {
+        set_error("peer transport: the mailboxes would be rebuilt (a larger exchange or other neighbours) after "
+                  "an exchange was captured into a graph, whose replays would then write freed memory; "
+                  "reserve the largest exchange (poms_comm_peer_reserve) before capturing");
+        return 1;
+    }
+    if (!c->peer_status) {
+        void* h = nullptr;
+        POMS_HIP_CHECK(hipHostMalloc(&h, 64, hipHostMallocMapped | hipHostMallocCoherent));
+        c->peer_status = static_cast<uint64_t*>(h);
+        *c->peer_status = 0;
+    }
     // every earlier exchange of this rank is complete, hence every neighbour's store
     // into the old block (the neighbours, in turn, finish theirs before answering the
     // handle exchange below)
@@ -279,10 +307,15 @@ static int peer_ensure(poms_comm* c, int64_t cnt, int prev, int next, hipStream_
         nn = next >= 0 ? blk : nullptr;
     } else {
         // each rank sends its handle and the capacity, so that a mismatch fails loudly
-        struct Msg { hipIpcMemHandle_t h; int64_t cap; } m{mine, cap}, fp{}, fn{};
+        // ... and its exchange workgroup count: each workgroup waits for the slots of
+        // the neighbour's G workgroups, so unequal counts could only end in the timeout
+        struct Msg { hipIpcMemHandle_t h; int64_t cap; int64_t wgs; } m{mine, cap, c->peer_wgs}, fp{}, fn{};
         if (peer_swap_bytes(c, &m, &fp, &fn, (int)sizeof(Msg), prev, next)) return fail("");
         if ((prev >= 0 && fp.cap != cap) || (next >= 0 && fn.cap != cap))
             return fail("peer transport: neighbours disagree on the mailbox size");
+        if ((prev >= 0 && fp.wgs != c->peer_wgs) || (next >= 0 && fn.wgs != c->peer_wgs))
+            return fail("peer transport: neighbours use different exchange workgroup counts "
+                        "(poms_comm_set_peer wgs / POMS_PEER_WGS must be equal on every rank)");
         if (prev >= 0) {
             if (hipIpcOpenMemHandle(reinterpret_cast<void**>(&np), fp.h, hipIpcMemLazyEnablePeerAccess) != hipSuccess)
                 return fail("peer transport: hipIpcOpenMemHandle of the previous rank's mailboxes failed");
@@ -338,6 +371,9 @@ static int peer_fill(poms_comm* c, double* data, int64_t plane_elems, int64_t n_
         a.ack_hi = nb + (loop ? kAckNext : kAckPrev);
     }
     a.G = c->peer_wgs;
+    void* sd = nullptr;
+    POMS_HIP_CHECK(hipHostGetDevicePointer(&sd, c->peer_status, 0));
+    a.status = static_cast<uint64_t*>(sd);
     return 0;
 }
 
@@ -346,6 +382,9 @@ static int peer_exchange(poms_comm* c, double* data, int64_t plane_elems, int64_
                          int prev, int next, hipStream_t st) {
     PeerArgs a;
     if (peer_fill(c, data, plane_elems, n_local, pad, width, prev, next, st, a)) return 1;
+    hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
+    POMS_HIP_CHECK(hipStreamIsCapturing(st, &cs));
+    if (cs != hipStreamCaptureStatusNone) c->peer_captured = true;
     POMS_HIP_CHECK(hipEventRecord(c->ev_in, st));
     POMS_HIP_CHECK(hipStreamWaitEvent(c->cs, c->ev_in, 0));
     hipLaunchKernelGGL(peer_exchange_kernel, dim3(a.G), dim3(256), 0, c->cs, a);
@@ -543,6 +582,7 @@ int poms_comm_destroy(poms_comm* c) {
     if (!c) return 0;
     if (c->cs) (void)hipStreamSynchronize(c->cs);
     peer_release(c);
+    if (c->peer_status) (void)hipHostFree(c->peer_status);
     if (c->comm) ncclCommDestroy(c->comm);
     for (hipEvent_t e : {c->ev_in, c->ev_halo, c->ev_red, c->ev_bnd})
         if (e) (void)hipEventDestroy(e);
@@ -565,6 +605,10 @@ int poms_comm_stream(poms_comm* c, void** stream) {
 int poms_comm_set_peer(poms_comm* c, int enable, int wgs) {
     if (!c || wgs < 1 || wgs > kPeerMaxWgs) { set_error("poms_comm_set_peer: bad argument (wgs in 1..256)"); return 1; }
     if (c->peer_on && (!enable || wgs != c->peer_wgs)) {   // blocks are rebuilt at the next exchange
+        if (c->pblk && c->peer_captured) {
+            set_error("poms_comm_set_peer: an exchange was captured into a graph; its mailboxes cannot be released");
+            return 1;
+        }
         (void)hipStreamSynchronize(c->cs);
         peer_release(c);
     }
@@ -579,17 +623,20 @@ int poms_comm_peer_reserve(poms_comm* c, int64_t cnt, int prev, int next) {
     return peer_ensure(c, cnt, prev, next, c->cs);
 }
 
+int poms_comm_check(poms_comm* c) {
+    if (!c) { set_error("poms_comm_check: null communicator"); return 1; }
+    return peer_check(c);
+}
+
 int poms_comm_peer_status(poms_comm* c, int* active, int* fine_grained, int* timed_out) {
     if (!c || !active || !fine_grained || !timed_out) { set_error("poms_comm_peer_status: null argument"); return 1; }
     *active = c->peer_on ? 1 : 0;
     *fine_grained = c->peer_fine ? 1 : 0;
     *timed_out = 0;
-    if (c->pblk) {
+    if (c->pblk && c->peer_status) {
         if (refuse_in_capture(c->cs, "poms_comm_peer_status")) return 1;
-        uint64_t st = 0;
         POMS_HIP_CHECK(hipStreamSynchronize(c->cs));
-        POMS_HIP_CHECK(hipMemcpy(&st, c->pblk + 8 * kStatus, sizeof(st), hipMemcpyDeviceToHost));
-        *timed_out = st != 0 ? 1 : 0;
+        *timed_out = __atomic_load_n(c->peer_status, __ATOMIC_ACQUIRE) != 0 ? 1 : 0;
     }
     return 0;
 }
@@ -755,6 +802,8 @@ int poms_comm_wait(poms_comm* c, int ticket) {
         }
     }
     std::atomic_thread_fence(std::memory_order_acquire);
+    // (the launch that wrote the slot read ghost planes of an exchange queued before it)
+    if (peer_check(c)) return 1;
     double v[2] = {slot[0], cnt > 1 ? slot[1] : 0.0};
     if (c->nranks > 1) {
         if (c->shm) {   // one node (RCCL ranks, or a host transport with the block attached)

@@ -331,8 +331,17 @@ kron_v5_kernel(const double* __restrict__ x, double* __restrict__ y, const doubl
     // the output columns H .. H+TO-1: on the aligned layout that drops the two
     // half-lines of halo each b row fetched (8 of 64 lanes) and a quarter-line at
     // each end of every x row.
-    const uint32_t colbx = (uint32_t)colb + ((2 * lane + 1 >= H - P && 2 * lane < H + TO + P) ? 0u : 0x80000000u);
-    const uint32_t colbb = (uint32_t)colb + ((2 * lane + 1 >= H && 2 * lane < H + TO) ? 0u : 0x80000000u);
+    // Past the last interior column the same holds (round 6): the last tile column's
+    // lanes beyond n2 - 1 + P (x) or n2 - 1 (b) read only pitch padding and the next
+    // row's first columns -- 25 of 64 lanes at 515^3 -- so they are not fetched either.
+    // Their LDS slots keep an older plane's values; only lanes that are never stored
+    // (and whose sums are masked) read them.
+    const uint32_t colbx = (uint32_t)colb + ((2 * lane + 1 >= H - P && 2 * lane < H + TO + P && cg0 < g.n2 + P)
+                                                 ? 0u : 0x80000000u);
+    const uint32_t colbb = (uint32_t)colb + ((2 * lane + 1 >= H && 2 * lane < H + TO && cg0 < g.n2) ? 0u : 0x80000000u);
+    // x-tile rows past the last storage row any output reads (n1 - 1 + 2P; the partial
+    // last tile row at 515^3: 9 of its 22 rows) are not fetched either
+    const int xrows_ok = g.n1 + 2 * P - r0;
 
     // ---- LDS-DMA issue (per wave per plane: x NXM - 1 or NXM rows, b 1 row) ----
     auto dma_x = [&](int m, int slot) {
@@ -342,20 +351,22 @@ kron_v5_kernel(const double* __restrict__ x, double* __restrict__ y, const doubl
         // voffset: the soffset field is not covered by the buffer range check
         const bool ok = sp >= 0 && sp < nsp;
         const uint32_t so = ok ? (uint32_t)sp * plane8 : 0u;
-        // x-tile row q = storage row r0 + q
+        // x-tile row q = storage row r0 + q (rows q >= xrows_ok: out of range by voffset)
+        const bool ok0 = ok && wv < xrows_ok;
         if ((CP & 8) && wv >= 2 * P)   // a row only this tile reads: stream it
-            dma16s<2>(rx, lds + XS_OFF + (slot * XR + wv) * TC, ok ? (int)((uint32_t)((r0 + wv) * s1 * 8) + colbx) : 0x7ffffff0, so);
+            dma16s<2>(rx, lds + XS_OFF + (slot * XR + wv) * TC, ok0 ? (int)((uint32_t)((r0 + wv) * s1 * 8) + colbx) : 0x7ffffff0, so);
         else
-            dma16s<XAUX>(rx, lds + XS_OFF + (slot * XR + wv) * TC, ok ? (int)((uint32_t)((r0 + wv) * s1 * 8) + colbx) : 0x7ffffff0, so);
+            dma16s<XAUX>(rx, lds + XS_OFF + (slot * XR + wv) * TC, ok0 ? (int)((uint32_t)((r0 + wv) * s1 * 8) + colbx) : 0x7ffffff0, so);
 #pragma unroll
         for (int i = 1; i < NXM; ++i)   // rows wv + i NW: every wave but the last on the tile's x rows
             if (i < NXM - 1 || wv < XR - (NXM - 1) * NW)
                 dma16s<XAUX>(rx, lds + XS_OFF + (slot * XR + i * NW + wv) * TC,
-                             ok ? (int)((uint32_t)((r0 + i * NW + wv) * s1 * 8) + colbx) : 0x7ffffff0, so);
+                             (ok && i * NW + wv < xrows_ok) ? (int)((uint32_t)((r0 + i * NW + wv) * s1 * 8) + colbx)
+                                                            : 0x7ffffff0, so);
     };
     auto dma_b = [&](int zo, int slot) {
         const uint32_t so = (uint32_t)(zo + g.pd0) * plane8;
-        const int vob = (int)((uint32_t)((orow + P) * s1 * 8) + colbb);
+        const int vob = row_ok ? (int)((uint32_t)((orow + P) * s1 * 8) + colbb) : 0x7ffffff0;   // (no output row: no b)
         dma16s<BAUX>(rbv, lds + BS_OFF + (slot * T1 + wv) * TC, vob, so);
         if constexpr (XIN) dma16s<BAUX>(rx, lds + XI_OFF + (slot * T1 + wv) * TC, vob, so);
     };
@@ -527,8 +538,8 @@ kron_v5_kernel(const double* __restrict__ x, double* __restrict__ y, const doubl
                 for (int k = 0; k < W; ++k) xv[k] = *(const d2*)(xs + (wv + k) * TC);
                 if constexpr (MODE == 1) {
                     const bool ok0 = t >= 2 * P && row_ok && (cok & 1);
-                    bstore2_s(ry, ok0 ? (orow + P) * s1 * 8 + colb + (zo_of(t) + g.pd0) * (int)plane8 : 0x7ffffff0,
-                              0u, xv[P][0] + xv[0][0], xv[P][1] + xv[W - 1][1]);
+                    bstore2_sp<YAUX>(ry, ok0 ? (orow + P) * s1 * 8 + colb + (zo_of(t) + g.pd0) * (int)plane8 : 0x7ffffff0,
+                                     0u, xv[P][0] + xv[0][0], xv[P][1] + xv[W - 1][1]);
                     continue;
                 }
                 double u[2], v[2];
@@ -1113,7 +1124,7 @@ int kron_v5_launch(int pmax, int epi, const KronPtrs& p, const KronGeom& g_in, c
         }
         if (diag_mode <= 2) {   // 1 = memory only, 2 = arithmetic only (apply)
             if (epi != EPI_APPLY) { set_error("v5 diag mode 1/2: apply only"); return 1; }
-            return diag_mode == 1 ? v5_launch_t<3, EPI_APPLY, 4, 1>(p, g, tc, H, omega, st)
+            return diag_mode == 1 ? v5_launch_t<3, EPI_APPLY, 4, 1, 6>(p, g, tc, H, omega, st)   // (the apply's cache policy)
                                   : v5_launch_t<3, EPI_APPLY, 4, 2>(p, g, tc, H, omega, st);
         }
 #define V5CP(CP, XH)                                                                               \

@@ -45,6 +45,10 @@ struct PeerArgs {
     uint64_t* ack_hi;
     int64_t cap;             // doubles per mailbox side
     int G;                   // exchange workgroups (0: no exchange in this launch)
+    // set to 1 (system scope) when a wait times out: pinned, device-mapped HOST memory,
+    // which every host-synchronising communicator call reads (poms_comm_wait fails
+    // loudly on it, so a timed-out exchange is never consumed silently)
+    uint64_t* status;
 };
 
 #ifdef __HIPCC__
@@ -114,7 +118,7 @@ __device__ __forceinline__ void peer_copy(double* __restrict__ dst, const double
 // One exchange, run by workgroup w of the G exchange workgroups (all of blockDim.x
 // threads; G == PeerArgs::G on every rank).
 __device__ __forceinline__ void peer_exchange_body(const PeerArgs& a, const int w, const int G) {
-    uint64_t* status = a.own + kStatus;
+    uint64_t* status = a.status;
     const uint64_t s = sys_load(a.own + kSeq) + 1;
     const uint64_t t_end = wall_clock64() + kPeerTimeoutTicks;
     const int64_t per = (a.cnt + G - 1) / G;

@@ -25,14 +25,10 @@ int kron_v5_launch(int pmax, int epi, const KronPtrs& p, const KronGeom& g, cons
                    double omega, hipStream_t st, int diag_mode);
 void kron_v5_tile(int pmax, bool aligned, int* H, int* TO);
 int kron_v5_rows(int pmax, int epi);
-int kron_v7_launch(int pmax, int epi, const KronPtrs& p, const KronGeom& g, const ToepConst& tc, double omega,
-                   hipStream_t st, int diag, bool dry = false);
-int kron_v7_built();
 int kron_v5_stamps(unsigned long long* host, int64_t n);
 int kron_v5_set_sched(int mode);
 void kron_v5_set_launch_events(hipEvent_t e0, hipEvent_t e1);
 bool kron_v5_launch_events_used();
-int kron_v7_tiles(int pmax, int n1, int n2);
 int kron_tile_rows();
 int kron_tile_cols();
 int vec_launch(int op, const RowGeom& g, double a, double b, const double* x, const double* y,
@@ -589,10 +585,11 @@ int poms_op_set_variant(poms_op* op, int variant) {
     // 90/91, 92-100, 101-113: diagnostic / tuning builds of v3, v4, v5 (110-112: v5
     // two sweeps from zero without sums / x1 scaling, timing only; 113: the Jacobi
     // sweep streaming the x rows no other tile reads)
-    const bool known = variant == 0 || variant == 4 || (variant >= 7 && variant <= 11) ||
-                       (variant >= 90 && variant <= 114) || (variant >= 121 && variant <= 124);
+    // (11, v7, was removed in round 6: an experimental kernel slower than v5)
+    const bool known = variant == 0 || variant == 4 || (variant >= 7 && variant <= 10) ||
+                       (variant >= 90 && variant <= 114);
     if (!op || !known) {
-        set_error("poms_op_set_variant: bad argument (0, 4, 7, 8, 9, 10, 11; 90-114 and 121-124 diagnostic)");
+        set_error("poms_op_set_variant: bad argument (0, 4, 7, 8, 9, 10; 90-114 diagnostic)");
         return 1;
     }
     if (variant > 0 && !op->v2_ok) { set_error("poms_op_set_variant: variant needs pads == pmax"); return 1; }
@@ -609,7 +606,6 @@ int poms_diag_v5_stamps(uint64_t* host_out, int64_t n) {
 int poms_diag_v5_sched(int mode) { return kron_v5_set_sched(mode); }
 
 int poms_variant_built(int variant) {
-    if (variant == 11 || (variant >= 121 && variant <= 124)) return kron_v7_built();
     return (variant == 0 || variant == 4 || (variant >= 7 && variant <= 10) || (variant >= 90 && variant <= 114)) ? 1 : 0;
 }
 
@@ -701,18 +697,6 @@ static bool v5_aligned(const poms_op* o, const double* x) {
     return pitch % 16 == 0 && (reinterpret_cast<uintptr_t>(x + o->L.pads[2]) & 127) == 0;
 }
 
-// v7 (variant 11, kron_v7.hip) runs 3D FORM_SUM operators at p = 3 on the
-// line-aligned layout whose non-Toeplitz axis-1 / axis-2 rows are among the first
-// and last 2p (uniform open knots; the boundary tables hold 4p rows), with v5's
-// corner rule.
-static bool v7_ok(const poms_op* o, const double* x, const double* y) {
-    if (!(v5_ok(o) && o->pmax == 3 && v5_aligned(o, x) && v5_aligned(o, y) && !o->ghost_corners)) return false;
-    const int P = o->pmax;
-    const int64_t n1 = o->L.n[1], n2 = o->L.n[2];
-    return n1 >= 4 * P && n2 >= 4 * P && o->tc.lo1 <= 2 * P && o->tc.hi1 >= n1 - 2 * P && o->tc.lo2 <= 2 * P &&
-           o->tc.hi2 >= n2 - 2 * P;
-}
-
 static int op_geom(poms_op* o, int64_t zb, int64_t ze, KronGeom& g, int v = -1, int v5_to = 0,
                    int64_t zb2 = 0, int64_t ze2 = 0, int epi = EPI_APPLY) {
     if (v < 0) v = o->variant;
@@ -728,10 +712,6 @@ static int op_geom(poms_op* o, int64_t zb, int64_t ze, KronGeom& g, int v = -1, 
     g.tiles1 = (int)((o->L.n[1] + trows - 1) / trows);
     g.tout = v == 10 ? v5_to : (o->tout > 0 ? o->tout : 64 - 2 * o->pmax);
     if (v >= 4) g.tiles2 = (int)((o->L.n[2] + g.tout - 1) / g.tout);
-    if (v == 11) {   // v7: the kernel maps its tiles itself; one flat tile index
-        g.tiles2 = 1;
-        g.tiles1 = kron_v7_tiles(o->pmax, (int)o->L.n[1], (int)o->L.n[2]);
-    }
     if (!is3d) {
         g.z_begin = 0; g.z_end = 1; g.chunk = 1; g.nchunks = 1; g.nch1 = 1; g.z2_begin = g.z2_end = 0;
         return 0;
@@ -756,7 +736,7 @@ static int op_geom(poms_op* o, int64_t zb, int64_t ze, KronGeom& g, int v = -1, 
     const int nz = (int)(ze - zb) + (int)(ze2 - zb2);
     int chunk = o->chunk;
     if (chunk <= 0) {
-        chunk = auto_chunk(nz, g.tiles2 * g.tiles1, o->pmax, (v == 10 || v == 11) ? 256.0 : 512.0);
+        chunk = auto_chunk(nz, g.tiles2 * g.tiles1, o->pmax, v == 10 ? 256.0 : 512.0);
         // the v5 two-sweeps-from-zero launch (VALU-bound) balances better over twice
         // as many chunks: 515^3 p = 3, 86 instead of 172 planes, 836-838 against
         // 865-882 us in two interleaved sweeps, equal medians (833 us) in a third
@@ -773,7 +753,7 @@ static int op_geom(poms_op* o, int64_t zb, int64_t ze, KronGeom& g, int v = -1, 
 
 // variants whose Jacobi epilogue also accumulates x_out . b (v3 and v4 kernels)
 static bool fused_dot_ok(const poms_op* o) {
-    return o->form == FORM_STENCIL || (o->variant >= 4 && o->variant <= 11) || o->variant == 114;
+    return o->form == FORM_STENCIL || (o->variant >= 4 && o->variant <= 10) || o->variant == 114;
 }
 
 
@@ -840,9 +820,6 @@ static int resolve_variant(const poms_op* o, int epi) {
         else
             v = ((epi == EPI_APPLY || epi == EPI_RESID) && o->pmax <= 3) ? 7 : 9;
     }
-    // v7: apply, residual, Jacobi sweep, apply + dot at p = 3 (alignment and the Toeplitz
-    // ranges are checked per call); the sweeps from zero run v5
-    if (v == 11 && !(epi != EPI_JACOBI0 && v5_ok(o) && o->pmax == 3 && !o->ghost_corners)) v = 10;
     if (v == 10 && (!v5_ok(o) || (epi == EPI_JACOBI0 && o->pmax == 3 && !same_toeplitz12(o)))) v = 9;
     return v;
 }
@@ -854,16 +831,15 @@ static int op_run(poms_op* o, int epi, double omega, const double* x, double* y,
     if (epi != EPI_APPLY && !b) { set_error("null right-hand side"); return 1; }
     if (o->form == FORM_STENCIL)
         return stencil_run(o, epi, omega, x, y, b, zb, ze, want_norm, stream, want_dot, zb2, ze2);
-    if (epi == EPI_APPLYDOT && !(o->variant == 4 || o->variant == 8 || o->variant == 9 || o->variant == 10 ||
-                                 o->variant == 11)) {
-        set_error("apply + x.y: kernel variants 4, 8, 9, 10, 11 only");
+    if (epi == EPI_APPLYDOT && !(o->variant == 4 || o->variant == 8 || o->variant == 9 || o->variant == 10)) {
+        set_error("apply + x.y: kernel variants 4, 8, 9, 10 only");
         return 1;
     }
     if (want_dot && ((epi != EPI_JACOBI && epi != EPI_JACOBI0 && epi != EPI_APPLYDOT) || !fused_dot_ok(o))) {
-        set_error("fused x_out.b needs a Jacobi sweep on kernel variants 4-11");
+        set_error("fused x_out.b needs a Jacobi sweep on kernel variants 4-10");
         return 1;
     }
-    if (epi == EPI_JACOBI0 && !(o->variant == 8 || o->variant == 9 || o->variant == 10 || o->variant == 11 ||
+    if (epi == EPI_JACOBI0 && !(o->variant == 8 || o->variant == 9 || o->variant == 10 ||
                                 (o->variant >= 110 && o->variant <= 112) || o->variant == 114)) {
         set_error("two sweeps from zero: kernel variant 8, 9 or 10 only");
         return 1;
@@ -876,27 +852,9 @@ static int op_run(poms_op* o, int epi, double omega, const double* x, double* y,
     // Variant 10 (v5) runs apply / residual / Jacobi / apply+dot of 3D p <= 3
     // operators, and is what 8 picks for them; 9 otherwise.
     int v = resolve_variant(o, epi);
-    if (v == 11 && !v7_ok(o, x, y))   // (as resolve_variant would pick for variant 10)
-        v = (v5_ok(o) && !(epi == EPI_JACOBI0 && o->pmax == 3 && !same_toeplitz12(o))) ? 10 : 9;
-    if (v == 11 || (v >= 121 && v <= 124)) {
-        // v7 not in this build (the product library compiles it out), or this epilogue's
-        // build spills: run v5 instead, as for any other unmet v7 precondition (a
-        // diagnostic v7 build asked for by number fails loudly)
-        KronGeom g7;
-        if (op_geom(o, zb, ze, g7, 11, 0, zb2, ze2, epi)) return 1;
-        const KronPtrs p7{x, y, b, o->a0t, o->b0t, o->a1, o->b1, o->a2, o->b2, nullptr,
-                          want_dot ? o->ctx->scratch : nullptr, o->rdiag0};
-        if (kron_v7_launch(o->pmax, epi, p7, g7, o->tc, omega, nullptr, v >= 121 ? v - 120 : 0, true) != 0) {
-            if (v >= 121) { set_error("v7 diagnostic build unavailable (not built: POMS_WITH_V7=1, or it spills)"); return 1; }
-            v = (v5_ok(o) && !(epi == EPI_JACOBI0 && o->pmax == 3 && !same_toeplitz12(o))) ? 10 : 9;
-        }
-    }
     const int v5_diag = (v >= 101 && v <= 114) ? v - 100 : 0;   // v5 diagnostic / tuning builds
     if (v5_diag) v = 10;
-    const int v7_diag = (v >= 121 && v <= 124) ? v - 120 : 0;   // v7 diagnostic / tuning builds
-    if (v7_diag) v = v7_ok(o, x, y) && epi == EPI_APPLY ? 11 : -1;
-    if (v < 0) { set_error("v7 diagnostic build: aligned p = 3 apply only"); return 1; }
-    o->last_variant = v7_diag ? 120 + v7_diag : v5_diag ? 100 + v5_diag : v;
+    o->last_variant = v5_diag ? 100 + v5_diag : v;
     int v5_h = 0, v5_to = 0;
     if (v == 10) kron_v5_tile(o->pmax, v5_aligned(o, x), &v5_h, &v5_to);
     KronGeom g;
@@ -944,9 +902,7 @@ static int op_run(poms_op* o, int epi, double omega, const double* x, double* y,
             POMS_HIP_CHECK(timing_record(tlh->e0, as_stream(stream)));
         }
     }
-    const int rc = v == 11
-        ? kron_v7_launch(o->pmax, epi, p, g, o->tc, omega, as_stream(stream), v7_diag)
-        : v == 10
+    const int rc = v == 10
         ? kron_v5_launch(o->pmax, epi, p, g, o->tc, v5_h, omega, as_stream(stream), v5_diag)
         : v == 0
         ? kron_launch(o->pmax, o->ndim == 3, o->form, epi, p, g, omega, as_stream(stream))
@@ -994,7 +950,7 @@ int poms_op_apply_dot(poms_op* op, const double* x, double* y, int64_t zb, int64
 int poms_op_apply_dot_supported(poms_op* op, int* yes) {
     if (!op || !yes) { set_error("poms_op_apply_dot_supported: null argument"); return 1; }
     const int v = op->variant;
-    *yes = (op->form == FORM_STENCIL || v == 4 || v == 8 || v == 9 || v == 10 || v == 11) ? 1 : 0;
+    *yes = (op->form == FORM_STENCIL || v == 4 || v == 8 || v == 9 || v == 10) ? 1 : 0;
     return 0;
 }
 
@@ -1010,7 +966,7 @@ int poms_op_from_zero_supported(poms_op* op, int* yes) {
     if (!op || !yes) { set_error("poms_op_from_zero_supported: null argument"); return 1; }
     const int64_t bytes = (int64_t)(op->L.n[0] + 2 * op->L.pads[0]) * row_geom(&op->L).s0 * 8;
     *yes = (op->ndim == 3 && op->form != FORM_STENCIL &&
-            (op->variant == 8 || op->variant == 9 || op->variant == 10 || op->variant == 11 ||
+            (op->variant == 8 || op->variant == 9 || op->variant == 10 ||
              (op->variant >= 110 && op->variant <= 112) || op->variant == 114) &&
             bytes < 0x7ffffff0LL) ? 1 : 0;
     return 0;
@@ -2443,8 +2399,18 @@ static bool pcg_spec_wanted(const poms_op*, const poms_pcg_opts* o) {
     return e && e[0] == '1' && o->maxiter >= 1 && o->jmaxiter >= 3;
 }
 
+static int pcg_jacobi_impl(poms_op* op, poms_comm* comm, const poms_pcg_opts* o, const double* b, double* x,
+                           int has_x0, double* const* work, poms_pcg_info* info, void* stream);
+
+// (a peer exchange that timed out during the call fails it: poms_comm_check)
 int poms_pcg_jacobi(poms_op* op, poms_comm* comm, const poms_pcg_opts* o, const double* b, double* x, int has_x0,
                     double* const* work, poms_pcg_info* info, void* stream) {
+    if (pcg_jacobi_impl(op, comm, o, b, x, has_x0, work, info, stream)) return 1;
+    return comm ? poms_comm_check(comm) : 0;
+}
+
+static int pcg_jacobi_impl(poms_op* op, poms_comm* comm, const poms_pcg_opts* o, const double* b, double* x,
+                           int has_x0, double* const* work, poms_pcg_info* info, void* stream) {
     if (!op || !o || !b || !x || !work || !info) { set_error("poms_pcg_jacobi: null argument"); return 1; }
     for (int i = 0; i < 5; ++i)
         if (!work[i]) { set_error("poms_pcg_jacobi: null work vector"); return 1; }

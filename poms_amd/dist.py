@@ -363,11 +363,15 @@ class NativeComm:
         self.is_host = bool(yes.value)
         self.peer = False
         if os.environ.get("POMS_COMM_PEER", "0") == "1":
-            self.set_peer(True, int(os.environ.get("POMS_PEER_WGS", "32")))
+            self.set_peer(True)
 
-    def set_peer(self, enable: bool, wgs: int = 64) -> None:
-        """Peer transport for the ghost exchange on (every rank alike) or off."""
+    def set_peer(self, enable: bool, wgs: int | None = None) -> None:
+        """Peer transport for the ghost exchange on (every rank alike) or off; ``wgs``
+        exchange workgroups (default ``POMS_PEER_WGS``, else 32: equal on every rank,
+        which the mailbox set-up checks)."""
         from . import _lib
+        if wgs is None:
+            wgs = int(os.environ.get("POMS_PEER_WGS", "32"))
         _lib.call("poms_comm_set_peer", self.h, 1 if enable else 0, int(wgs))
         self.peer = bool(enable)
 
@@ -386,6 +390,12 @@ class NativeComm:
         a, f, t = C.c_int(), C.c_int(), C.c_int()
         _lib.call("poms_comm_peer_status", self.h, C.byref(a), C.byref(f), C.byref(t))
         return {"active": bool(a.value), "fine_grained": bool(f.value), "timed_out": bool(t.value)}
+
+    def check(self) -> None:
+        """Raise if a peer exchange of this communicator timed out (its ghosts, and
+        everything computed from them, are invalid); no synchronisation."""
+        from . import _lib
+        _lib.call("poms_comm_check", self.h)
 
     @property
     def uses_shm(self) -> bool:
@@ -590,6 +600,7 @@ class NativeComm:
     def allreduce(self, t: torch.Tensor, stream, wait_back: bool):
         from . import _lib
         import ctypes as C
+        self.check()
         _lib.call("poms_allreduce_sum", self.h, C.c_void_p(t.data_ptr()), int(t.numel()), stream,
                   1 if wait_back else 0)
 

@@ -11,7 +11,7 @@ cp "$ROOT/poms_amd/csrc/common.hpp" $T/
 /opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -fPIC -std=c++17 -Wall -Wno-unused-function -munsafe-fp-atomics \
     -DPOMS_V5_QUICK -I "$ROOT/include" -c $T/kron_v5.hip -o $T/kron_v5.o
 objs=""
-for s in kron_fused kron_dpp kron_v4 kron_v7 vec_ops transfer kron_solve stencil_general comm poms_abi; do
+for s in kron_fused kron_dpp kron_v4 vec_ops transfer kron_solve stencil_general comm poms_abi; do
   objs="$objs $ROOT/poms_amd/_obj/$s.hip.o"
 done
 /opt/rocm/bin/hipcc --offload-arch=gfx950 -shared -fPIC -o "$OUT" $T/kron_v5.o $objs -L/opt/rocm/lib -lrccl
