@@ -90,6 +90,7 @@ struct poms_comm {
     char* pnext = nullptr;
     bool pprev_ipc = false, pnext_ipc = false;
     bool peer_fine = false;           // own block is fine-grained (coherent) device memory
+    hipStream_t halo_on = nullptr;    // the stream the last exchange was queued on
     uint64_t* peer_status = nullptr;  // timeout flag of the exchange kernel (pinned, device-mapped host memory)
     // an exchange was queued while a stream was being captured: graphs now hold raw
     // pointers into the mailbox block and its flag slots, so the block may no longer be
@@ -107,6 +108,19 @@ struct poms_comm {
     } while (0)
 
 static hipStream_t cstream(void* s) { return reinterpret_cast<hipStream_t>(s); }
+
+// The stream an RCCL call of this communicator goes to: the communication stream, or
+// -- while the caller's stream is being captured into a graph -- the capturing stream
+// itself.  With the HIP 7.0 runtime torch bundles (the one every library process runs
+// on: same SONAME, loaded first), hipStreamEndCapture segfaults when RCCL's grouped
+// send / receive was captured on a stream FORKED from the capturing one by an event;
+// captured on the capturing stream it works, as does the fork with the ROCm 7.2 runtime
+// and a fork around a plain kernel (tools/r06/graph_probe.cpp, profiles/r06/graph_probe/).
+static hipStream_t rccl_stream(poms_comm* c, hipStream_t caller) {
+    hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
+    if (hipStreamIsCapturing(caller, &cs) == hipSuccess && cs != hipStreamCaptureStatusNone) return caller;
+    return c->cs;
+}
 
 // A call that waits on the host (event / stream synchronisation, a host callback)
 // must not run while `s` is being captured into a graph: nothing captured has run,
@@ -675,25 +689,32 @@ int poms_halo_start(poms_comm* c, double* data, int64_t plane_elems, int64_t n_l
             POMS_HIP_CHECK(hipMemcpy(data + (int64_t)(pad + n_local) * plane_elems, rhi, cnt * 8,
                                      hipMemcpyHostToDevice));
         POMS_HIP_CHECK(hipEventRecord(c->ev_halo, st));
+        c->halo_on = st;
         return 0;
     }
-    if (c->peer_on) return peer_exchange(c, data, plane_elems, n_local, pad, width, prev, next, cstream(stream));
-    POMS_HIP_CHECK(hipEventRecord(c->ev_in, cstream(stream)));
-    POMS_HIP_CHECK(hipStreamWaitEvent(c->cs, c->ev_in, 0));
+    if (c->peer_on) {
+        c->halo_on = c->cs;
+        return peer_exchange(c, data, plane_elems, n_local, pad, width, prev, next, cstream(stream));
+    }
+    hipStream_t xs = rccl_stream(c, cstream(stream));
+    if (xs != cstream(stream)) {
+        POMS_HIP_CHECK(hipEventRecord(c->ev_in, cstream(stream)));
+        POMS_HIP_CHECK(hipStreamWaitEvent(xs, c->ev_in, 0));
+    }
     const size_t cnt = (size_t)width * (size_t)plane_elems;
     POMS_NCCL_CHECK(ncclGroupStart());
     if (prev >= 0) {
-        POMS_NCCL_CHECK(ncclSend(data + (int64_t)pad * plane_elems, cnt, ncclDouble, prev, c->comm, c->cs));
-        POMS_NCCL_CHECK(ncclRecv(data + (int64_t)(pad - width) * plane_elems, cnt, ncclDouble, prev, c->comm, c->cs));
+        POMS_NCCL_CHECK(ncclSend(data + (int64_t)pad * plane_elems, cnt, ncclDouble, prev, c->comm, xs));
+        POMS_NCCL_CHECK(ncclRecv(data + (int64_t)(pad - width) * plane_elems, cnt, ncclDouble, prev, c->comm, xs));
     }
     if (next >= 0) {
         POMS_NCCL_CHECK(ncclSend(data + (int64_t)(pad + n_local - width) * plane_elems, cnt, ncclDouble, next,
-                                 c->comm, c->cs));
-        POMS_NCCL_CHECK(ncclRecv(data + (int64_t)(pad + n_local) * plane_elems, cnt, ncclDouble, next, c->comm,
-                                 c->cs));
+                                 c->comm, xs));
+        POMS_NCCL_CHECK(ncclRecv(data + (int64_t)(pad + n_local) * plane_elems, cnt, ncclDouble, next, c->comm, xs));
     }
     POMS_NCCL_CHECK(ncclGroupEnd());
-    POMS_HIP_CHECK(hipEventRecord(c->ev_halo, c->cs));
+    POMS_HIP_CHECK(hipEventRecord(c->ev_halo, xs));
+    c->halo_on = xs;
     return 0;
 }
 
@@ -713,6 +734,15 @@ int poms_allreduce_sum(poms_comm* c, double* buf, int64_t count, void* stream, i
         if (host_allreduce(c, buf, count, cstream(stream))) return 1;
         POMS_HIP_CHECK(hipEventRecord(c->ev_in, cstream(stream)));
         POMS_HIP_CHECK(hipStreamWaitEvent(c->cs, c->ev_in, 0));
+        return 0;
+    }
+    hipStream_t xs = rccl_stream(c, cstream(stream));
+    if (xs == cstream(stream)) {   // (captured: on the capturing stream, then ordered on the communication stream)
+        POMS_NCCL_CHECK(ncclAllReduce(buf, buf, (size_t)count, ncclDouble, ncclSum, c->comm, xs));
+        if (!wait_back) {
+            POMS_HIP_CHECK(hipEventRecord(c->ev_red, xs));
+            POMS_HIP_CHECK(hipStreamWaitEvent(c->cs, c->ev_red, 0));
+        }
         return 0;
     }
     POMS_HIP_CHECK(hipEventRecord(c->ev_in, cstream(stream)));
@@ -860,7 +890,7 @@ int poms_op_run_dist(poms_op* op, poms_comm* c, int epilogue, double omega, cons
         struct Hooks {
             static int ghosts_on(void* a, void* s) {   // `s` waits for the exchange
                 auto* c = static_cast<poms_comm*>(a);
-                if (!c->host && cstream(s) == c->cs) return 0;   // queued behind it already
+                if (cstream(s) == c->halo_on) return 0;   // queued behind it already
                 POMS_HIP_CHECK(hipStreamWaitEvent(cstream(s), c->ev_halo, 0));
                 return 0;
             }

@@ -1032,13 +1032,41 @@ static const int* v5_sched(int P, int epi, const KronGeom& g, const ToepConst& t
     const std::vector<int> key = {dev, P, epi, g.n0, g.n1, g.n2, g.g0, g.z_begin, g.z_end, g.z2_begin, g.z2_end,
                                   g.chunk, g.nch1, g.nchunks, g.tiles1, g.tiles2, g.tout, g.order,
                                   tc.lo0, tc.hi0, tc.lo1, tc.hi1, tc.lo2, tc.hi2};
+    // a table is uploaded on the stream of the launch that built it; a launch on another
+    // stream waits for the upload's event (advisor, round 5: it could otherwise read the
+    // table before the copy landed) until the event is seen complete
+    struct Table {
+        int* d = nullptr;
+        hipEvent_t ev = nullptr;
+        hipStream_t st = nullptr;
+        bool landed = false;
+    };
     static std::mutex mu;
-    static std::map<std::vector<int>, int*> cache;
+    static std::map<std::vector<int>, Table> cache;
     std::lock_guard<std::mutex> lk(mu);
-    auto it = cache.find(key);
-    if (it != cache.end()) return it->second;
     hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
-    if (hipStreamIsCapturing(st, &cs) != hipSuccess || cs != hipStreamCaptureStatusNone) return nullptr;
+    if (hipStreamIsCapturing(st, &cs) != hipSuccess) return nullptr;
+    auto it = cache.find(key);
+    if (it != cache.end()) {
+        Table& tb = it->second;
+        if (!tb.landed) {
+            const hipError_t q = hipEventQuery(tb.ev);
+            if (q == hipSuccess) {
+                tb.landed = true;
+            } else if (st != tb.st) {
+                // inside a capture the host waits for the (tiny) upload instead: an
+                // event recorded outside the capture cannot order a captured launch
+                if (cs != hipStreamCaptureStatusNone ? hipEventSynchronize(tb.ev) != hipSuccess
+                                                     : hipStreamWaitEvent(st, tb.ev, 0) != hipSuccess) {
+                    (void)hipGetLastError();
+                    return nullptr;
+                }
+                if (cs != hipStreamCaptureStatusNone) tb.landed = true;
+            }
+        }
+        return tb.d;
+    }
+    if (cs != hipStreamCaptureStatusNone) return nullptr;
     const int T1 = v5_waves(P, epi), TO = g.tout;
     const bool j0 = epi == EPI_JACOBI0;
     std::vector<double> w(nblk);
@@ -1090,7 +1118,15 @@ static const int* v5_sched(int P, int epi, const KronGeom& g, const ToepConst& t
         host.erase(key);
         return nullptr;
     }
-    cache[key] = d;
+    hipEvent_t ev = nullptr;
+    if (hipEventCreateWithFlags(&ev, hipEventDisableTiming) != hipSuccess || hipEventRecord(ev, st) != hipSuccess) {
+        (void)hipGetLastError();
+        if (ev) (void)hipEventDestroy(ev);
+        (void)hipFreeAsync(d, st);
+        host.erase(key);
+        return nullptr;
+    }
+    cache[key] = Table{d, ev, st, false};
     return d;
 }
 

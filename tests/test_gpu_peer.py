@@ -147,25 +147,30 @@ def test_peer_loopback_operator_matches_rccl_loopback(cells, rank):
             assert torch.equal(u, v) if isinstance(u, torch.Tensor) else u == v, (u, v)
 
 
-def _loopback_op(cells=40, p=3, rank=1, world=4):
+def _loopback_op(cells=40, p=3, rank=1, world=4, peer=True):
     from poms_amd.dist import SlabDistribution
     from poms_amd.splines import assemble_1d, uniform_knots
     from poms_amd.stencil import KronOperator, StencilVectorSpace
     torch.cuda.set_device(0)
     n = cells + p
     d = SlabDistribution.loopback(n, rank, world)
-    d.native.set_peer(True, 32)
+    if peer:
+        d.native.set_peer(True, 32)
     M, K = assemble_1d(uniform_knots(p, cells), p)
     V = StencilVectorSpace([n] * 3, [p] * 3, align=True, dist=d)
     return d, V, KronOperator.laplace(V, [M] * 3, [K] * 3)
 
 
-def test_peer_distributed_sweep_capture_and_replay():
+@pytest.mark.parametrize("peer", [True, False])
+def test_peer_distributed_sweep_capture_and_replay(peer):
     """One distributed Jacobi sweep (exchange, interior launch, boundary launch on the
     communication stream, join) captured into a graph and replayed equals the eager
-    call bitwise.  With RCCL's grouped send/recv the capture crashed at capture end
-    (round-4 verdict item 2, tools/graph_rccl_probe.py)."""
-    d, V, A = _loopback_op()
+    call bitwise -- over the peer transport and over RCCL.  RCCL's grouped send/recv
+    used to crash hipStreamEndCapture: torch's bundled HIP 7.0 runtime segfaults when
+    RCCL P2P is captured on a stream forked from the capturing one; the library now
+    queues captured RCCL calls on the capturing stream (round 6, tools/r06/graph_probe.cpp,
+    profiles/r06/graph_probe/)."""
+    d, V, A = _loopback_op(peer=peer)
     x, b = V.zeros(), V.zeros()
     V.interior(x._data).uniform_(-1, 1)
     V.interior(b._data).uniform_(-1, 1)
@@ -186,12 +191,14 @@ def test_peer_distributed_sweep_capture_and_replay():
     assert not d.native.peer_status()["timed_out"]
 
 
-def test_peer_pcg_graph_replay_matches_step_loop(monkeypatch):
+@pytest.mark.parametrize("peer", [True, False])
+def test_peer_pcg_graph_replay_matches_step_loop(monkeypatch, peer):
     """pcg + damped Jacobi on a loopback slab: the native loop's speculative calls
     replayed from its own captured graph (POMS_PCG_SPEC=1, POMS_PCG_GRAPH=2) give the
-    step-by-step loop's iterates and info bitwise, and the graph was replayed."""
+    step-by-step loop's iterates and info bitwise, and the graph was replayed -- over
+    the peer transport and over RCCL."""
     from poms_amd import solvers
-    d, V, A = _loopback_op(cells=48)
+    d, V, A = _loopback_op(cells=48, peer=peer)
     b = V.zeros()
     V.interior(b._data).fill_(1.0)
     out = {}
@@ -207,3 +214,30 @@ def test_peer_pcg_graph_replay_matches_step_loop(monkeypatch):
     st = A.spec_stats
     assert st["replays"] > 0, st
     assert not d.native.peer_status()["timed_out"]
+
+
+def test_peer_mailboxes_not_rebuilt_after_capture():
+    """Once an exchange has been captured, the mailboxes (whose raw addresses the graph
+    holds) cannot be rebuilt or released: a larger reservation and set_peer(False)
+    fail loudly instead of leaving the graph to write freed memory (advisor, round 5).
+    The graph keeps working."""
+    from poms_amd._lib import PomsError
+    c = _comm(32)
+    n_loc, pad, width, pe = 6, 3, 3, 1024
+    data = _planes(n_loc, pad, pe, 0)
+    st = torch.cuda.Stream()
+    c.peer_reserve(width * pe, 0, 0)
+    g = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(g, stream=st):
+        c.halo_start(data, n_loc, pad, width, 0, 0, st.cuda_stream)
+        c.halo_finish(st.cuda_stream)
+    with pytest.raises(PomsError, match="captured"):
+        c.peer_reserve(64 * width * pe, 0, 0)   # (past the 2^16-double minimum capacity)
+    with pytest.raises(PomsError, match="captured"):
+        c.set_peer(False)
+    data.copy_(_planes(n_loc, pad, pe, 3))
+    torch.cuda.synchronize()
+    g.replay()
+    torch.cuda.synchronize()
+    _check_ghosts(data, n_loc, pad, width, 0, 0)
+    c.check()   # no exchange timed out

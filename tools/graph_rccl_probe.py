@@ -154,6 +154,9 @@ def main():
         tail = "\n".join((r.stdout + r.stderr).strip().splitlines()[-25:])
         print(f"=== stage {s}: exit {r.returncode}\n{tail}\n", flush=True)
         bad = bad or r.returncode != 0
+        if r.returncode < 0 or r.returncode in (124, 134, 137, 139):   # nothing more on the GPU after a crash
+            print("crash / abort: stopping", flush=True)
+            return 1
     return 1 if bad else 0
 
 
