@@ -65,7 +65,7 @@ def parse():
     ap.add_argument("--cpu-cells-1core", type=int, default=64,
                     help="cells per axis of the single-core V-cycle sample")
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--pmc-json", type=str, default=str(ROOT / "profiles" / "r05" / "pmc_traffic" / "pmc_traffic_jacobi.json"),
+    ap.add_argument("--pmc-json", type=str, default=str(ROOT / "profiles" / "r06" / "pmc_traffic" / "pmc_traffic_jacobi.json"),
                     help="tools/pmc_traffic.py summary of a separate rocprofv3 --pmc pass "
                          "(FETCH_SIZE x2 + WRITE_SIZE per launch) used for roofline.traffic; used only "
                          "when its recorded p and kernel variant are this run's")

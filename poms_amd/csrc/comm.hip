@@ -92,6 +92,7 @@ struct poms_comm {
     bool peer_fine = false;           // own block is fine-grained (coherent) device memory
     hipStream_t halo_on = nullptr;    // the stream the last exchange was queued on
     uint64_t* peer_status = nullptr;  // timeout flag of the exchange kernel (pinned, device-mapped host memory)
+    uint64_t* peer_status_dev = nullptr;   // its device address (taken once: not a call to make inside a capture)
     // an exchange was queued while a stream was being captured: graphs now hold raw
     // pointers into the mailbox block and its flag slots, so the block may no longer be
     // rebuilt or released (advisor, round 5)
@@ -265,6 +266,9 @@ static int peer_ensure(poms_comm* c, int64_t cnt, int prev, int next, hipStream_
         POMS_HIP_CHECK(hipHostMalloc(&h, 64, hipHostMallocMapped | hipHostMallocCoherent));
         c->peer_status = static_cast<uint64_t*>(h);
         *c->peer_status = 0;
+        void* sd = nullptr;
+        POMS_HIP_CHECK(hipHostGetDevicePointer(&sd, c->peer_status, 0));
+        c->peer_status_dev = static_cast<uint64_t*>(sd);
     }
     // every earlier exchange of this rank is complete, hence every neighbour's store
     // into the old block (the neighbours, in turn, finish theirs before answering the
@@ -385,9 +389,7 @@ static int peer_fill(poms_comm* c, double* data, int64_t plane_elems, int64_t n_
         a.ack_hi = nb + (loop ? kAckNext : kAckPrev);
     }
     a.G = c->peer_wgs;
-    void* sd = nullptr;
-    POMS_HIP_CHECK(hipHostGetDevicePointer(&sd, c->peer_status, 0));
-    a.status = static_cast<uint64_t*>(sd);
+    a.status = c->peer_status_dev;
     return 0;
 }
 

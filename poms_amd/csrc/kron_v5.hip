@@ -1050,18 +1050,18 @@ static const int* v5_sched(int P, int epi, const KronGeom& g, const ToepConst& t
     if (it != cache.end()) {
         Table& tb = it->second;
         if (!tb.landed) {
-            const hipError_t q = hipEventQuery(tb.ev);
-            if (q == hipSuccess) {
+            // inside a capture no event may be queried or waited on (that invalidates
+            // the capture): a table not yet seen landed is not used there -- the default
+            // order gives the same results bitwise (the partial sums keep their slots)
+            if (cs != hipStreamCaptureStatusNone) return nullptr;
+            if (hipEventQuery(tb.ev) == hipSuccess) {
                 tb.landed = true;
-            } else if (st != tb.st) {
-                // inside a capture the host waits for the (tiny) upload instead: an
-                // event recorded outside the capture cannot order a captured launch
-                if (cs != hipStreamCaptureStatusNone ? hipEventSynchronize(tb.ev) != hipSuccess
-                                                     : hipStreamWaitEvent(st, tb.ev, 0) != hipSuccess) {
+            } else {
+                (void)hipGetLastError();
+                if (st != tb.st && hipStreamWaitEvent(st, tb.ev, 0) != hipSuccess) {
                     (void)hipGetLastError();
                     return nullptr;
                 }
-                if (cs != hipStreamCaptureStatusNone) tb.landed = true;
             }
         }
         return tb.d;
