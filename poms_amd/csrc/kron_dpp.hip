@@ -18,6 +18,9 @@
 // Preconditions: storage pads == P on every used axis (checked by the host).
 #include "common.hpp"
 
+#include <cstdlib>
+#include <type_traits>
+
 namespace poms {
 
 __device__ __forceinline__ double dpp_shr1(double v) {  // lane l <- lane l-1 (lane 0 <- 0)
@@ -68,11 +71,12 @@ kron_v3_kernel(const double* __restrict__ x, double* __restrict__ y,
     constexpr bool T2 = false;   // measured slower (x_in re-read, LDS-table boundary tiles): kept for reference
     constexpr bool XRING = (JAC || APD) && IS3D && !T2;
     constexpr int NRING = P + 1;            // x planes kept for the Jacobi update
-    __shared__ d2 ab_[SUM ? 2 * XRP * 64 : 1];
+    // (2D: one plane, so one (a, b) tile -- the double buffer serves the 3D march)
+    __shared__ d2 ab_[SUM ? (IS3D ? 2 : 1) * XRP * 64 : 1];
     // x of the tile's output rows for the last P+1 planes (the Jacobi epilogue's
     // x_in): re-reading it from HBM P planes later costs 8 B/DOF (L2-evicted)
     __shared__ double xring[XRING ? NRING * T1 * 64 : 1];
-    __shared__ double as_[SUM ? 1 : 2 * XRP * 64];
+    __shared__ double as_[SUM ? 1 : (IS3D ? 2 : 1) * XRP * 64];
     __shared__ double c1a[T1 * W];
     __shared__ double c1b[SUM ? T1 * W : 1];
     __shared__ double red[NW];
@@ -295,7 +299,7 @@ kron_v3_kernel(const double* __restrict__ x, double* __restrict__ y,
             const int q = q2 % NS;
             const int xb = q2 % PF;
             if (t < nplanes) {
-                const int buf = (t & 1) * XRP * 64;
+                const int buf = IS3D ? (t & 1) * XRP * 64 : 0;
                 // ---- axis 2 in registers: DPP shifts of whole rows
 #pragma unroll
                 for (int j = 0; j < NRW; ++j) {
@@ -540,6 +544,21 @@ static int v3_launch_p(bool is3d, int form, int epi, const KronPtrs& p, const Kr
                             : v3_launch_e<P, R, NW, false, FORM_SINGLE, PF, FLAT>(epi, p, g, tc, omega, st);
 }
 
+// Output rows per tile of the 2D p = 3 whole-array build (variant 9): 8 waves x R rows.
+// R = 5 (40-row tiles): at 1024^2 the grid is 26 x 18 = 468 workgroups, one round of the
+// 512 slots (2 per CU), against 1170 (2.3 rounds) for R = 2, and the host adds 468
+// instead of 1170 norm partials per sweep; the 2D cycle 3.17 -> 2.90 ms, interleaved on
+// one box (profiles/r06/r2d/; R = 3, 4, 6 between the two).  POMS_V3_2D_R overrides.
+int kron_v3_rows_2d() {
+    static int r = -1;
+    if (r < 0) {
+        const char* e = getenv("POMS_V3_2D_R");
+        r = e ? atoi(e) : 5;
+        if (r < 2 || r > 6) r = 2;
+    }
+    return 8 * r;
+}
+
 // variant 4: 8 waves x 2 rows (16 x (64-2P) tile, 2 WGs/CU); variant 9: the same
 // tile addressing each array through one buffer resource
 int kron_v3_launch(int variant, int pmax, bool is3d, int form, int epi, const KronPtrs& p,
@@ -552,6 +571,22 @@ int kron_v3_launch(int variant, int pmax, bool is3d, int form, int epi, const Kr
     }
     if (variant == 9) {   // v3 with whole-array buffer resources (arrays < 2 GiB)
         const int64_t bytes = (int64_t)(g.n0 + 2 * g.pd0) * g.s0 * 8;
+        // 2D at p = 3: taller tiles (R rows per wave, kron_v3_rows_2d) so that the grid
+        // is about one round of the CUs (tuning: POMS_V3_2D_R)
+        if (!is3d && pmax == 3 && bytes < 0x7ffffff0LL) {
+            auto l2 = [&](auto rt) {
+                constexpr int RR = decltype(rt)::value;
+                return form == FORM_SUM ? v3_launch_e<3, RR, 8, false, FORM_SUM, 1, true>(epi, p, g, tc, omega, st)
+                                        : v3_launch_e<3, RR, 8, false, FORM_SINGLE, 1, true>(epi, p, g, tc, omega, st);
+            };
+            switch (kron_v3_rows_2d() / 8) {
+                case 3: return l2(std::integral_constant<int, 3>{});
+                case 4: return l2(std::integral_constant<int, 4>{});
+                case 5: return l2(std::integral_constant<int, 5>{});
+                case 6: return l2(std::integral_constant<int, 6>{});
+                default: break;
+            }
+        }
         if (bytes < 0x7ffffff0LL) {
             switch (pmax) {
                 case 1: return v3_launch_p<1, 2, 8, 1, true>(is3d, form, epi, p, g, tc, omega, st);

@@ -30,6 +30,7 @@ int kron_v5_set_sched(int mode);
 void kron_v5_set_launch_events(hipEvent_t e0, hipEvent_t e1);
 bool kron_v5_launch_events_used();
 int kron_tile_rows();
+int kron_v3_rows_2d();
 int kron_tile_cols();
 int vec_launch(int op, const RowGeom& g, double a, double b, const double* x, const double* y,
                double* z, double* w, const double* q, double* partial, hipStream_t st,
@@ -708,7 +709,8 @@ static int op_geom(poms_op* o, int64_t zb, int64_t ze, KronGeom& g, int v = -1, 
     g.pd0 = r.pd0; g.pd1 = r.pd1; g.pd2 = r.pd2;
     g.g0 = (int)o->g0;
     g.tiles2 = (int)((o->L.n[2] + kron_tile_cols() - 1) / kron_tile_cols());
-    const int trows = v == 10 ? kron_v5_rows(o->pmax, epi) : kron_tile_rows();
+    const int trows = v == 10 ? kron_v5_rows(o->pmax, epi)
+                    : (!is3d && v == 9 && o->pmax == 3) ? kron_v3_rows_2d() : kron_tile_rows();
     g.tiles1 = (int)((o->L.n[1] + trows - 1) / trows);
     g.tout = v == 10 ? v5_to : (o->tout > 0 ? o->tout : 64 - 2 * o->pmax);
     if (v >= 4) g.tiles2 = (int)((o->L.n[2] + g.tout - 1) / g.tout);
