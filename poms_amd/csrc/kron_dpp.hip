@@ -61,7 +61,7 @@ kron_v3_kernel(const double* __restrict__ x, double* __restrict__ y,
     // (sweep 1 from x0 = 0), and the epilogue is sweep 2 -- x2 from one pass over b
     constexpr bool J0 = (EPI == EPI_JACOBI0);
     constexpr bool JAC = (EPI == EPI_JACOBI) || J0;
-    static_assert(!J0 || (IS3D && FLAT), "EPI_JACOBI0 is built for the 3D whole-array kernel");
+    static_assert(!J0 || FLAT, "EPI_JACOBI0 is built for the whole-array kernel");
     constexpr bool APD = (EPI == EPI_APPLYDOT);     // apply + x.(Ax) (pcg's p.q)
     // T2 (the whole-array build): axis-2 band rows from the Toeplitz constants
     // (symmetric pair sums) in interior column tiles and from an LDS table in the
@@ -308,16 +308,25 @@ kron_v3_kernel(const double* __restrict__ x, double* __restrict__ y,
                     if constexpr (J0) {
                         // x1 = (omega b) / diag(A) at (plane m, row, column) -- the
                         // diag_scale kernel's expression; clamped indices keep diag
-                        // finite where b is a zero ghost
-                        const int m = g.g0 + z0 - P + t;
-                        const int mc = min(max(m, 0), g.g0 + g.n0 + g.pd0 - 1);
-                        const double q0a = a0t[(mc + P) * W + P];
-                        const double q0b = SUM ? b0t[(mc + P) * W + P] : 0.0;
+                        // finite where b is a zero ghost.  2D (round 6): diag = d1a d2a +
+                        // d1b d2b, the epilogue's diag_parts expression, so that x1 at a
+                        // stencil input and at the output point are the same bits
                         const int row = min(max(r0 - P + wv + j * NW, 0), g.n1 - 1);
                         const double q1a = a1[row * W + P];
                         const double q1b = SUM ? b1[row * W + P] : 0.0;
-                        double dg = SUM ? q0a * (q1a * d2a) + q0b * (q1b * d2a + q1a * d2b)
-                                        : q0a * q1a * d2a;
+                        double dg;
+                        if constexpr (IS3D) {
+                            const int m = g.g0 + z0 - P + t;
+                            const int mc = min(max(m, 0), g.g0 + g.n0 + g.pd0 - 1);
+                            const double q0a = a0t[(mc + P) * W + P];
+                            const double q0b = SUM ? b0t[(mc + P) * W + P] : 0.0;
+                            dg = SUM ? q0a * (q1a * d2a) + q0b * (q1b * d2a + q1a * d2b) : q0a * q1a * d2a;
+                        } else {
+                            // (the row's own band entries: a halo row of a fast1 tile may lie
+                            // outside the Toeplitz interior; inside it they equal tc.t1a/t1b[0]
+                            // bitwise, which the epilogue uses for the output rows)
+                            dg = SUM ? (q1a * d2a + q1b * d2b) : q1a * d2a;
+                        }
                         double rc = __builtin_amdgcn_rcp(dg);
                         double e = fma(-dg, rc, 1.0);
                         rc = fma(rc, e, rc);
@@ -519,11 +528,11 @@ static int v3_launch_e(int epi, const KronPtrs& p, const KronGeom& g, const Toep
         return 0;
     }
     if (epi == EPI_JACOBI0) {
-        if constexpr (IS3D && FLAT) {
+        if constexpr (FLAT) {
             v3_launch_t<P, R, NW, IS3D, FORM, EPI_JACOBI0, PF, 0, FLAT>(p, g, tc, omega, st);
             return 0;
         }
-        set_error("two sweeps from zero: 3D operators with the whole-array kernel (variant 8/9) only");
+        set_error("two sweeps from zero: the whole-array kernel (variant 8/9) only");
         return 1;
     }
     switch (epi) {

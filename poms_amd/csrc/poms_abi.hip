@@ -960,14 +960,18 @@ int poms_op_jacobi_from_zero(poms_op* op, double omega, const double* b, double*
                              int64_t zb, int64_t ze, int want_norm, void* stream) {
     if (!op || !b || !x_out) { set_error("jacobi from zero: null argument"); return 1; }
     if (b == x_out) { set_error("jacobi from zero: x_out must not alias b"); return 1; }
-    if (op->ndim != 3) { set_error("jacobi from zero: 3D operators only"); return 1; }
+    int yes = 0;
+    if (poms_op_from_zero_supported(op, &yes)) return 1;
+    if (!yes) { set_error("jacobi from zero: not supported by this operator (poms_op_from_zero_supported)"); return 1; }
     return op_run(op, EPI_JACOBI0, omega, b, x_out, b, zb, ze, want_norm, stream, want_norm);
 }
 
 int poms_op_from_zero_supported(poms_op* op, int* yes) {
     if (!op || !yes) { set_error("poms_op_from_zero_supported: null argument"); return 1; }
     const int64_t bytes = (int64_t)(op->L.n[0] + 2 * op->L.pads[0]) * row_geom(&op->L).s0 * 8;
-    *yes = (op->ndim == 3 && op->form != FORM_STENCIL &&
+    // 2D (round 6, v3): not on a block of a decomposition (its ghost rows' x1 would need
+    // the neighbours' diagonal)
+    *yes = ((op->ndim == 3 || (op->ndim == 2 && !op->ghost_corners)) && op->form != FORM_STENCIL &&
             (op->variant == 8 || op->variant == 9 || op->variant == 10 ||
              (op->variant >= 110 && op->variant <= 112) || op->variant == 114) &&
             bytes < 0x7ffffff0LL) ? 1 : 0;
@@ -1024,7 +1028,11 @@ static int op_run_epi(poms_op* op, int epilogue, double omega, const double* x, 
             if (op_run(op, EPI_JACOBI, omega, x, y, b, zb, ze, wn ? 1 : 0, stream, wd ? 1 : 0, zb2, ze2)) return 1;
             break;
         case EPI_JACOBI0:   // x = b: norm_out <- ||dr_2||^2, dot_out <- ||x1||^2
-            if (op->ndim != 3) { set_error("jacobi from zero: 3D operators only"); return 1; }
+            {
+                int fz = 0;
+                if (poms_op_from_zero_supported(op, &fz)) return 1;
+                if (!fz) { set_error("jacobi from zero: not supported by this operator"); return 1; }
+            }
             if (b == y) { set_error("jacobi from zero: x_out must not alias b"); return 1; }
             if (wn != wd) { set_error("jacobi from zero: both norms or neither"); return 1; }
             if (op_run(op, EPI_JACOBI0, omega, b, y, b, zb, ze, wn ? 1 : 0, stream, wn ? 1 : 0, zb2, ze2)) return 1;
@@ -2077,7 +2085,7 @@ struct PcgRun {
         const int maxit = o->jmaxiter;
         double *x = A, *xn = B;
         int fz = 0, k0;
-        if (op->ndim == 3 && maxit >= 2 && maxit != 2 && op->form != FORM_STENCIL) (void)poms_op_from_zero_supported(op, &fz);
+        if (maxit >= 2 && maxit != 2 && op->form != FORM_STENCIL) (void)poms_op_from_zero_supported(op, &fz);
         if (fz) {   // sweeps 1, 2 from x = 0: [||x1||^2, ||dr2||^2]
             int vi;
             if (sjrun(EPI_JACOBI0, rhs, A, rhs, true, true, &vi)) return 1;
@@ -2123,7 +2131,7 @@ struct PcgRun {
         Pend q[2];
         int nq = 0, ring = 0, k0;
         int fz = 0;
-        if (op->ndim == 3 && maxit >= 2 && maxit != 2 && op->form != FORM_STENCIL) (void)poms_op_from_zero_supported(op, &fz);
+        if (maxit >= 2 && maxit != 2 && op->form != FORM_STENCIL) (void)poms_op_from_zero_supported(op, &fz);
         if (fz) {   // sweeps 1, 2 from x = 0 in one pass over rhs: [||x1||^2, ||dr2||^2]
             const int h0 = arm(H_J0, 2);
             if (jrun(EPI_JACOBI0, rhs, A, rhs, true, true, h0)) return 1;

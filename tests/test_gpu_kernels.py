@@ -230,9 +230,11 @@ def test_jacobi_sweep_fused_dot(gpu, variant, ndim, cells, p):
 
 @pytest.mark.parametrize("variant", [8, 9, 10])
 @pytest.mark.parametrize("ndim,cells,p", [(3, (25, 18, 70), 3), (3, (20, 24, 65), 2), (3, (14, 12, 66), 5),
-                                          (3, (21, 33, 40), 1)])
+                                          (3, (21, 33, 40), 1), (2, (64, 70), 3), (2, (150, 130), 3),
+                                          (2, (40, 33), 2), (2, (37, 90), 5)])
 def test_jacobi_from_zero(gpu, ndim, cells, p, variant):
-    """poms_op_jacobi_from_zero == diag_scale (sweep 1) followed by one sweep, with both norms."""
+    """poms_op_jacobi_from_zero == diag_scale (sweep 1) followed by one sweep, with both norms
+    (2D since round 6: the v3 build, 40-row tiles at p = 3)."""
     from poms_amd.stencil import KronOperator
     rng = np.random.default_rng(5)
     F = [assemble_1d(uniform_knots(p, N), p) for N in cells]
