@@ -67,6 +67,23 @@ struct AssembleAxis {
     int nel, nq, p, n;
 };
 
+// pcg's scalars folded into the flat vector updates (one rank, round 6): every block
+// reduces `n` per-block partials in reduce_partials_kernel's order (the same bits as
+// the one-block kernels they replace) and forms the scalar itself; block 0 stores it.
+//  * V_RUPD (alpha): p.q from the apply + dot partials, alpha = sc[sr] / p.q; block 0
+//    stores p.q, 1, alpha, alpha at sc[1..4] (pcg_alpha_kernel's slots) and, with
+//    copy_sr, sc[0] = sc[sr] (the s.r_old update a folded beta left pending);
+//  * V_XPUPD (beta): s.r_new from the last sweep's x . rhs partials, beta = s.r_new /
+//    sc[0]; block 0 stores s.r_new at sc[6] and beta at sc[5] -- NOT sc[0], which the
+//    other blocks are reading (the next r update's copy_sr does that).
+struct AlphaFold {
+    const double* part = nullptr;   // null: no fold, the coefficients as before
+    int n = 0;
+    double* sc = nullptr;
+    int sr = 0;                     // V_RUPD: slot of s.r
+    int copy_sr = 0;
+};
+
 // Padded row layout used by the row-wise vector kernels.
 struct RowGeom {
     int64_t s0, s1;

@@ -39,7 +39,7 @@ int reduce_launch(const double* partial, int count, double* out, hipStream_t st,
 int reduce_wide_launch(const double* partial, int count, double* out, hipStream_t st, int accumulate = 0);
 int vec_flat_launch(int op, int64_t count, double a, double b, const double* x, const double* y,
                     double* z, double* w, const double* q, double* partial, hipStream_t st,
-                    int* nblk_out, const double* ab = nullptr);
+                    int* nblk_out, const double* ab = nullptr, const AlphaFold* af = nullptr);
 int zero_ghosts_launch(const RowGeom& g, double* z, hipStream_t st);
 int diag_scale_blocks(bool is3d, const RowGeom& g);
 int diag_scale_launch(bool is3d, int form, const RowGeom& g, int P, int g0, double scale,
@@ -1761,6 +1761,12 @@ __global__ void __launch_bounds__(256) pcg_alpha_kernel(const double* __restrict
 // s.r_new from the last damped-Jacobi sweep's per-block partials (reduce_partials_kernel's
 // order: the same bits), then beta = s.r_new / s.r_old and s.r_old <- s.r_new, in one
 // launch (one rank: saves the one-block reduction launch per pcg iteration)
+// s.r_old <- s.r_new, where a beta folded into the x/p update left it pending and no
+// folded r update follows (AlphaFold)
+__global__ void pcg_sr_fix_kernel(double* sc) {
+    if (threadIdx.x == 0) sc[SC_SR] = sc[SC_SRN];
+}
+
 __global__ void __launch_bounds__(256) pcg_beta_kernel(const double* __restrict__ part, int count, double* sc) {
     __shared__ double red[4];
     double s = 0.0;
@@ -1802,7 +1808,55 @@ struct PcgRun {
         }
         if (op_run_epi(op, EPI_APPLYDOT, o->omega, p, q, p, 0, n0, 0, 0, false, true, stv)) return 1;
         const int64_t n = op->last_partials;   // (the dot's partials at scratch + n, as poms_op_run_reduce2 reads them)
-        hipLaunchKernelGGL(pcg_alpha_kernel, dim3(1), dim3(256), 0, st, op->ctx->scratch + n, (int)n, sc);
+        // alpha is formed by the r update that follows (rupd: AlphaFold), or by
+        // pcg_alpha_kernel when that cannot take it (flush_alpha)
+        alpha_part = op->ctx->scratch + n;
+        alpha_n = n;
+        return 0;
+    }
+    const double* alpha_part = nullptr;   // p.q's partials awaiting alpha (apd_alpha)
+    int64_t alpha_n = 0;
+    bool sr_stale = false;                // a folded beta left s.r_old <- s.r_new pending
+    int fix_sr() {
+        if (!sr_stale) return 0;
+        hipLaunchKernelGGL(pcg_sr_fix_kernel, dim3(1), dim3(64), 0, st, sc);
+        sr_stale = false;
+        POMS_HIP_CHECK(hipGetLastError());
+        return 0;
+    }
+    static bool fold_on() {   // POMS_ALPHA_FOLD=0: the one-block scalar kernels (tuning / A-B)
+        static const bool f = !(getenv("POMS_ALPHA_FOLD") && getenv("POMS_ALPHA_FOLD")[0] == '0');
+        return f;
+    }
+    // beta folded into the x/p update: x += alpha p, p = s + beta p with beta from the
+    // last sweep's x . rhs partials (dot_part); 1 if it cannot (the caller runs
+    // pcg_beta_kernel and the plain update), -1 on error
+    int xpupd_beta(double* x, double* p, const double* s) {
+        if (!fold_on() || !direct() || (op->L.flags & POMS_LAYOUT_GHOST_DATA) || dot_part_n < 0) return 1;
+        const RowGeom g = row_geom(&op->L);
+        const int64_t off = (int64_t)g.pd0 * g.s0, count = (int64_t)g.n0 * g.s0;
+        const int head = (reinterpret_cast<uintptr_t>(x + off) & 15) ? 1 : 0;
+        const int64_t nbp = std::max<int64_t>(1, ((count - head) / 2 + 1023) / 1024);
+        if (dot_part_n * nbp > (int64_t)1 << 20) return 1;
+        if (fix_sr()) return -1;   // (beta reads s.r_old at sc[SC_SR])
+        AlphaFold bf;
+        bf.part = dot_part;
+        bf.n = (int)dot_part_n;
+        bf.sc = sc;
+        static_assert(SC_SR == 0 && SC_BETA == 5 && SC_SRN == 6, "AlphaFold's beta slots");
+        int nb = 0;
+        if (vec_flat_launch(V_XPUPD, count, 0.0, 0.0, s + off, nullptr, x + off, p + off, nullptr, nullptr, st, &nb,
+                            sc + SC_ALPHA2, &bf) != 0)
+            return 1;
+        if (hipGetLastError() != hipSuccess) { set_error("x/p update with beta: launch failed"); return -1; }
+        sr_stale = true;
+        return 0;
+    }
+    int flush_alpha() {
+        if (fix_sr()) return 1;
+        if (!alpha_part) return 0;
+        hipLaunchKernelGGL(pcg_alpha_kernel, dim3(1), dim3(256), 0, st, alpha_part, (int)alpha_n, sc);
+        alpha_part = nullptr;
         POMS_HIP_CHECK(hipGetLastError());
         return 0;
     }
@@ -2001,8 +2055,26 @@ struct PcgRun {
             if (nbp <= host_partials_max()) {
                 int nb = 0;
                 double* reg = op->sv_part + (size_t)h * poms_op::kSvPart;
+                // alpha folded into this launch where its blocks' extra reads of the
+                // partials are small (2D: 468 partials x ~515 blocks; not the 3D grid's
+                // 495 x 65536): one launch less per pcg iteration (round 6)
+                AlphaFold af;
+                static const bool fold = !(getenv("POMS_ALPHA_FOLD") && getenv("POMS_ALPHA_FOLD")[0] == '0');
+                if (fold && alpha_part && alpha_n * nbp <= (int64_t)1 << 20) {
+                    af.part = alpha_part;
+                    af.n = (int)alpha_n;
+                    af.sc = sc;
+                    af.sr = sr_stale ? SC_SRN : SC_SR;   // (a folded beta's s.r_new, copied to SC_SR by block 0)
+                    af.copy_sr = sr_stale ? 1 : 0;
+                    static_assert(SC_SR == 0 && SC_PQ == 1 && SC_ONE == 2 && SC_ALPHA == 3 && SC_ALPHA2 == 4,
+                                  "AlphaFold's slots");
+                } else if (flush_alpha()) {
+                    return 1;
+                }
                 if (vec_flat_launch(V_RUPD, count, 0.0, 0.0, nullptr, nullptr, nullptr, r + off, q + off, reg, st, &nb,
-                                    sc + SC_ALPHA) == 0) {
+                                    sc + SC_ALPHA, af.part ? &af : nullptr) == 0) {
+                    if (af.part) sr_stale = false;
+                    alpha_part = nullptr;
                     POMS_HIP_CHECK(hipGetLastError());
                     op->sv_npart[h] = nb;
                     op->sv_pkind[h] = 1;
@@ -2010,6 +2082,7 @@ struct PcgRun {
                 }
             }
         }
+        if (flush_alpha()) return 1;
         double* d = hslot(h);
         if (!d || poms_pcg_r_update_dev(op->ctx, &op->L, sc + SC_ALPHA, r, q, d, stv) || lazy_post(h, 1)) return 1;
         return 0;
@@ -2544,12 +2617,19 @@ static int pcg_jacobi_impl(poms_op* op, poms_comm* comm, const poms_pcg_opts* o,
             k -= 1;
             break;
         }
-        if (dd && R.dot_part_n >= 0)   // x . rhs's partials from the last sweep, reduced here
-            hipLaunchKernelGGL(pcg_beta_kernel, dim3(1), dim3(256), 0, R.st, R.dot_part, (int)R.dot_part_n, R.sc);
-        else
-            hipLaunchKernelGGL(pcg_scalars_kernel, dim3(1), dim3(64), 0, R.st, R.sc, 1);
-        if (poms_pcg_xp_update_dev(ctx, L, R.sc + SC_ALPHA2, x, p, sn, stream)) return 1;
+        // beta folded into the x/p update where it can be (one rank, small grids)
+        const int fb = (dd && R.dot_part_n >= 0) ? R.xpupd_beta(x, p, sn) : 1;
+        if (fb < 0) return 1;
+        if (fb > 0) {
+            if (R.fix_sr()) return 1;
+            if (dd && R.dot_part_n >= 0)   // x . rhs's partials from the last sweep, reduced here
+                hipLaunchKernelGGL(pcg_beta_kernel, dim3(1), dim3(256), 0, R.st, R.dot_part, (int)R.dot_part_n, R.sc);
+            else
+                hipLaunchKernelGGL(pcg_scalars_kernel, dim3(1), dim3(64), 0, R.st, R.sc, 1);
+            if (poms_pcg_xp_update_dev(ctx, L, R.sc + SC_ALPHA2, x, p, sn, stream)) return 1;
+        }
     }
+    if (R.fix_sr() || R.flush_alpha()) return 1;
     if (k > o->maxiter) k = o->maxiter;
     info->niter = k;
     info->success = nrmr < o->tol * nrmr0 ? 1 : 0;

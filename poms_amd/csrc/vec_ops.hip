@@ -106,11 +106,42 @@ __global__ void __launch_bounds__(256)
 vec_flat_kernel(const int head, const int64_t nd2, const int tail, double a, double b,
                 const double* __restrict__ x, const double* __restrict__ yv, double* __restrict__ z,
                 double* __restrict__ w, const double* __restrict__ q, double* __restrict__ partial,
-                const double* __restrict__ ab) {
+                const double* __restrict__ ab, const AlphaFold af) {
     if (ab != nullptr) { a = ab[0]; b = ab[1]; }   // coefficients from device memory
     typedef double d2 __attribute__((ext_vector_type(2)));
     constexpr int U = 4;
     __shared__ double red[4];
+    if constexpr (OP == V_RUPD || OP == V_XPUPD) {
+        if (af.part != nullptr) {   // alpha / beta from partials (see AlphaFold)
+            double sp = 0.0;
+            for (int i = threadIdx.x; i < af.n; i += 256) sp += af.part[i];
+            const double t = block_sum_256(sp, red);
+            if (threadIdx.x == 0) {
+                double v;
+                if constexpr (OP == V_RUPD) {   // t = p.q
+                    v = af.sc[af.sr] / t;
+                    if (blockIdx.x == 0) {
+                        af.sc[1] = t;
+                        af.sc[2] = 1.0;
+                        af.sc[3] = v;
+                        af.sc[4] = v;
+                        if (af.copy_sr) af.sc[0] = af.sc[af.sr];
+                    }
+                } else {                        // t = s.r_new
+                    v = t / af.sc[0];
+                    if (blockIdx.x == 0) {
+                        af.sc[6] = t;
+                        af.sc[5] = v;
+                    }
+                }
+                red[0] = v;
+            }
+            __syncthreads();
+            if constexpr (OP == V_RUPD) a = red[0];
+            else b = red[0];
+            __syncthreads();   // (red is the final reduction's again)
+        }
+    }
     double s = 0.0;
     const d2* X = (const d2*)(x + head);
     const d2* Y = (const d2*)(yv + head);
@@ -363,7 +394,8 @@ int zero_ghosts_launch(const RowGeom& g, double* z, hipStream_t st) {
 // (nothing launched) otherwise, and for ops without a flat form (V_FILL).
 int vec_flat_launch(int op, int64_t count, double a, double b, const double* x, const double* y,
                     double* z, double* w, const double* q, double* partial, hipStream_t st,
-                    int* nblk_out, const double* ab) {
+                    int* nblk_out, const double* ab, const AlphaFold* af) {
+    const AlphaFold afv = (af != nullptr && (op == V_RUPD || op == V_XPUPD)) ? *af : AlphaFold{};
     if (op == V_FILL || count < 4) return 1;
     int mis = -1;
     for (const void* ptr : {(const void*)x, (const void*)y, (const void*)z, (const void*)w, (const void*)q}) {
@@ -395,10 +427,10 @@ int vec_flat_launch(int op, int64_t count, double a, double b, const double* x, 
     case OPV:                                                                                         \
         if (plain)                                                                                    \
             hipLaunchKernelGGL((vec_flat_kernel<OPV, false>), dim3((int)nb), dim3(256), 0, st, head, nd2, tail, a, b, \
-                               x, y, z, w, q, partial, ab);                                           \
+                               x, y, z, w, q, partial, ab, afv);                                      \
         else                                                                                          \
             hipLaunchKernelGGL((vec_flat_kernel<OPV, true>), dim3((int)nb), dim3(256), 0, st, head, nd2, tail, a, b, \
-                               x, y, z, w, q, partial, ab);                                           \
+                               x, y, z, w, q, partial, ab, afv);                                      \
         return 0;
         POMS_VF(V_AXPBY)
         POMS_VF(V_SCALE)
