@@ -127,11 +127,16 @@ __device__ __forceinline__ void v5_lds_barrier() {
 // 154 us, 8 waves 136, v3 135-146; profiles/r02/j0_16wave/).
 // (12 waves at 168 VGPRs fit the p = 5 apply but ran 254 us against 185 at 256^3,
 // profiles/r02/configs/kb_p5_waves12.log vs kb_p5_waves8.log.)
-constexpr int v5_waves(int P, int EPI) { return (P == 3 || (P < 3 && EPI != EPI_JACOBI0)) ? 16 : 8; }
+// (Round 6: the p = 3 two-sweeps-from-zero build whose axis-1 / axis-2 Toeplitz rows
+// differ -- two sets of constants -- spills at 16 waves; it runs 8-wave tiles, with its
+// two running sums back in VGPRs, instead of falling back to v3.)
+constexpr int v5_waves(int P, int EPI, bool SAME12 = true) {
+    return ((P == 3 && (EPI != EPI_JACOBI0 || SAME12)) || (P < 3 && EPI != EPI_JACOBI0)) ? 16 : 8;
+}
 
 template <int P, int EPI, int D, int MODE = 0, int CP = 0, bool XH = false, bool ST16 = true, bool JDOT = true,
           bool SAME12 = false>
-__global__ void __launch_bounds__(64 * v5_waves(P, EPI), 1)
+__global__ void __launch_bounds__(64 * v5_waves(P, EPI, SAME12), 1)
 kron_v5_kernel(const double* __restrict__ x, double* __restrict__ y, const double* __restrict__ bvec,
                const double* __restrict__ a0t, const double* __restrict__ b0t,
                const double* __restrict__ a1, const double* __restrict__ b1,
@@ -140,7 +145,7 @@ kron_v5_kernel(const double* __restrict__ x, double* __restrict__ y, const doubl
                const double* __restrict__ rdiag0, const KronGeom g, const ToepConst tc,
                const int H, const double omega) {
     constexpr int W = 2 * P + 1;
-    constexpr int NW = v5_waves(P, EPI);
+    constexpr int NW = v5_waves(P, EPI, SAME12);
     constexpr int T1 = NW;              // output rows per tile: one per wave
     constexpr int XR = T1 + 2 * P;      // x rows per plane tile
     constexpr int TC = 128;             // lane-columns per tile
@@ -190,7 +195,7 @@ kron_v5_kernel(const double* __restrict__ x, double* __restrict__ y, const doubl
     // J0: per-lane running sums (||dr_2||^2, ||x1||^2) in LDS, not VGPRs: the 4
     // VGPRs they would pin for the whole march are what p = 3 lacks at 16 waves
     // (p = 3 only: the 8-wave builds of p <= 2 keep them in VGPRs, which they have)
-    constexpr bool JSL = J0 && P == 3;
+    constexpr bool JSL = J0 && P == 3 && NW == 16;
     // J0 diagnostic builds (MODE 3: no sums, 4: no x1 scaling of the rows, 5: both;
     // results wrong by design -- timing only)
     constexpr bool J0NS = J0 && (MODE == 3 || MODE == 5);
@@ -892,13 +897,13 @@ static int v5_launch_t2(const KronPtrs& p, const KronGeom& g, const ToepConst& t
     const int nblk = g.tiles2 * g.tiles1 * g.nchunks;
     if (t_v5_ev0 != nullptr) {   // a timed launch: the events on the dispatch itself
         hipExtLaunchKernelGGL((kron_v5_kernel<P, EPI, D, MODE, CP, XH, ST16, JDOT, SAME12>), dim3(nblk),
-                              dim3(64 * v5_waves(P, EPI)), 0, st, t_v5_ev0, t_v5_ev1, 0, p.x, p.y, p.b, p.a0t,
+                              dim3(64 * v5_waves(P, EPI, SAME12)), 0, st, t_v5_ev0, t_v5_ev1, 0, p.x, p.y, p.b, p.a0t,
                               p.b0t, p.a1, p.b1, p.a2, p.b2, p.partial, p.partial2, p.rdiag0, g, tc, H, omega);
         t_v5_ev0 = t_v5_ev1 = nullptr;
         t_v5_ev_used = true;
         return 0;
     }
-    hipLaunchKernelGGL((kron_v5_kernel<P, EPI, D, MODE, CP, XH, ST16, JDOT, SAME12>), dim3(nblk), dim3(64 * v5_waves(P, EPI)), 0, st, p.x,
+    hipLaunchKernelGGL((kron_v5_kernel<P, EPI, D, MODE, CP, XH, ST16, JDOT, SAME12>), dim3(nblk), dim3(64 * v5_waves(P, EPI, SAME12)), 0, st, p.x,
                        p.y, p.b, p.a0t, p.b0t, p.a1, p.b1, p.a2, p.b2, p.partial, p.partial2, p.rdiag0, g, tc, H, omega);
     return 0;
 }
@@ -1011,6 +1016,8 @@ void kron_v5_tile(int pmax, bool aligned, int* H, int* TO) {
 // slow paths.  Built once per geometry and device, outside any graph capture (a
 // launch during a capture that has no table yet keeps the default order).
 // POMS_V5_SCHED=0 turns it off.
+int kron_v5_rows(int pmax, int epi, int same12);
+
 static std::atomic<int> g_v5_sched{-1};
 
 int kron_v5_set_sched(int mode) {   // poms_diag_v5_sched
@@ -1067,7 +1074,9 @@ static const int* v5_sched(int P, int epi, const KronGeom& g, const ToepConst& t
         return tb.d;
     }
     if (cs != hipStreamCaptureStatusNone) return nullptr;
-    const int T1 = v5_waves(P, epi), TO = g.tout;
+    bool same12 = true;
+    for (int k = 0; k <= P; ++k) same12 = same12 && tc.t1a[k] == tc.t2a[k] && tc.t1b[k] == tc.t2b[k];
+    const int T1 = kron_v5_rows(P, epi, same12 ? 1 : 0), TO = g.tout;
     const bool j0 = epi == EPI_JACOBI0;
     std::vector<double> w(nblk);
     for (int b = 0; b < nblk; ++b) {
@@ -1198,7 +1207,7 @@ int kron_v5_launch(int pmax, int epi, const KronPtrs& p, const KronGeom& g_in, c
     return 1;
 }
 
-int kron_v5_rows(int pmax, int epi) { return v5_waves(pmax, epi); }
+int kron_v5_rows(int pmax, int epi, int same12) { return v5_waves(pmax, epi, same12 != 0); }
 
 // MODE 6 stamps: copy n u64 (<= kV5Stamps) to host (zeroed after the copy)
 int kron_v5_stamps(unsigned long long* host, int64_t n) {

@@ -24,7 +24,7 @@ int kron_v4_launch(int pmax, bool is3d, int form, int epi, const KronPtrs& p, co
 int kron_v5_launch(int pmax, int epi, const KronPtrs& p, const KronGeom& g, const ToepConst& tc, int H,
                    double omega, hipStream_t st, int diag_mode);
 void kron_v5_tile(int pmax, bool aligned, int* H, int* TO);
-int kron_v5_rows(int pmax, int epi);
+int kron_v5_rows(int pmax, int epi, int same12);
 int kron_v5_stamps(unsigned long long* host, int64_t n);
 int kron_v5_set_sched(int mode);
 void kron_v5_set_launch_events(hipEvent_t e0, hipEvent_t e1);
@@ -698,6 +698,8 @@ static bool v5_aligned(const poms_op* o, const double* x) {
     return pitch % 16 == 0 && (reinterpret_cast<uintptr_t>(x + o->L.pads[2]) & 127) == 0;
 }
 
+static bool same_toeplitz12(const poms_op* o);
+
 static int op_geom(poms_op* o, int64_t zb, int64_t ze, KronGeom& g, int v = -1, int v5_to = 0,
                    int64_t zb2 = 0, int64_t ze2 = 0, int epi = EPI_APPLY) {
     if (v < 0) v = o->variant;
@@ -709,7 +711,7 @@ static int op_geom(poms_op* o, int64_t zb, int64_t ze, KronGeom& g, int v = -1, 
     g.pd0 = r.pd0; g.pd1 = r.pd1; g.pd2 = r.pd2;
     g.g0 = (int)o->g0;
     g.tiles2 = (int)((o->L.n[2] + kron_tile_cols() - 1) / kron_tile_cols());
-    const int trows = v == 10 ? kron_v5_rows(o->pmax, epi)
+    const int trows = v == 10 ? kron_v5_rows(o->pmax, epi, same_toeplitz12(o) ? 1 : 0)
                     : (!is3d && v == 9 && o->pmax == 3) ? kron_v3_rows_2d() : kron_tile_rows();
     g.tiles1 = (int)((o->L.n[1] + trows - 1) / trows);
     g.tout = v == 10 ? v5_to : (o->tout > 0 ? o->tout : 64 - 2 * o->pmax);
@@ -744,7 +746,8 @@ static int op_geom(poms_op* o, int64_t zb, int64_t ze, KronGeom& g, int v = -1, 
         // 865-882 us in two interleaved sweeps, equal medians (833 us) in a third
         // (profiles/r03/chunks/); the other epilogues keep the model's pick (Jacobi
         // 715 us at 172 against 729 at 86)
-        if (v == 10 && epi == EPI_JACOBI0 && o->pmax == 3 && chunk / 2 >= 8 * o->pmax) chunk = (chunk + 1) / 2;
+        if (v == 10 && epi == EPI_JACOBI0 && o->pmax == 3 && same_toeplitz12(o) && chunk / 2 >= 8 * o->pmax)
+            chunk = (chunk + 1) / 2;   // (the 16-wave build only)
     }
     chunk = std::max(1, std::min(chunk, std::max(nz, 1)));
     g.chunk = chunk;
@@ -806,15 +809,15 @@ static int resolve_variant(const poms_op* o, int epi) {
     int v = o->variant;
     if (v == 8) {
         const bool plain = epi == EPI_APPLY || epi == EPI_RESID || epi == EPI_JACOBI;
-        if (o->ndim == 3 && v5_ok(o) &&
-            (epi != EPI_JACOBI0 || o->pmax != 3 || same_toeplitz12(o)))
+        if (o->ndim == 3 && v5_ok(o))
             v = 10;   // v5: kernel_bench at 515^3 p = 3; 8-wave tiles at 256^3 p = 4, 5
                       // (profiles/r02/configs/kb_p5_waves8.log: apply 231 -> 185 us at p = 5);
                       // sweeps from zero at p <= 2 and p = 4, 5 (8-wave tiles; at 256^3
                       // p = 4 208 vs 291 us for v3, p = 5 261 vs 428 us,
                       // profiles/r05/late/kb_p45_j0.log) and at p = 3 (16-wave tiles, 930 vs
                       // 945 us for v3 at 515^3, profiles/r02/j0_16wave/) where axes 1 and 2
-                      // share their rows (the other build spills)
+                      // share their rows, 8-wave tiles where they do not (round 6; the
+                      // 16-wave build of that case spills)
         else if (o->ndim == 3)
             v = ((epi == EPI_APPLY && o->pmax >= 3) || (plain && o->pmax >= 4)) ? 7 : 9;
         else if (epi == EPI_JACOBI && o->pmax <= 3)
@@ -822,7 +825,7 @@ static int resolve_variant(const poms_op* o, int epi) {
         else
             v = ((epi == EPI_APPLY || epi == EPI_RESID) && o->pmax <= 3) ? 7 : 9;
     }
-    if (v == 10 && (!v5_ok(o) || (epi == EPI_JACOBI0 && o->pmax == 3 && !same_toeplitz12(o)))) v = 9;
+    if (v == 10 && !v5_ok(o)) v = 9;
     return v;
 }
 

@@ -456,7 +456,8 @@ def test_native_run_dist_single_rank(gpu):
 
 @pytest.mark.parametrize("p,cells,align", [(1, (21, 33, 150), False), (2, (20, 24, 131), True),
                                            (2, (20, 24, 131), False), (3, (25, 140, 140), True),
-                                           (3, (25, 18, 140), True)])
+                                           (3, (25, 18, 140), True), (3, (25, 18, 140), False),
+                                           (3, (40, 70, 250), True)])
 def test_v5_jacobi_from_zero_coverage(gpu, p, cells, align):
     """Two sweeps from zero on v5 (16-wave tiles at p <= 3; wide axis 2 -> several
     128-column tiles, aligned and unaligned layouts, a two-range launch) against
@@ -470,9 +471,10 @@ def test_v5_jacobi_from_zero_coverage(gpu, p, cells, align):
     V = StencilVectorSpace(n, [p] * 3, align=align)
     A = KronOperator.laplace(V, [f[0] for f in F], [f[1] for f in F])
     A.set_variant(8)
-    # the default picks v5 at p <= 2, and at p = 3 when axes 1 and 2 share their
-    # Toeplitz rows (equal cell counts); v3 otherwise (even when v5 is asked for)
-    want = 10 if p <= 2 or cells[1] == cells[2] else 9
+    # the default picks v5 for every case: at p = 3 16-wave tiles when axes 1 and 2
+    # share their Toeplitz rows (equal cell counts), 8-wave tiles otherwise (round 6;
+    # v3 took those before)
+    want = 10
     assert A.kernel_variant("jacobi_from_zero") == want
     A.set_variant(10)
     assert A.kernel_variant("jacobi_from_zero") == want
