@@ -178,7 +178,8 @@ int poms_op_last_variant(poms_op* op, int* variant);
 /* One operator launch on planes [z_begin, z_end) and its reductions, in one
  * call: epilogue as in poms_op_kernel_variant (0 apply y = A x; 1 residual
  * y = b - A x; 2 Jacobi sweep y = x + omega (b - A x)/diag; 3 sweeps 1-2 from
- * zero, x = b; 4 apply + x.y).  If norm_out / dot_out (device) are non-null the
+ * zero, x = b; 4 apply + x.y; 6 two sweeps from x, poms_op_sweep2_supported).
+ * If norm_out / dot_out (device) are non-null the
  * per-block partials are reduced into them (accumulate: added to their value),
  * as poms_op_jacobi_sweep_dot / poms_op_apply_dot + poms_reduce_partials_at
  * would: Jacobi: norm = ||dr||^2, dot = x_out . b; from zero: norm = ||dr_2||^2,
@@ -236,11 +237,18 @@ int poms_op_fused_dot_supported(poms_op* op, int* yes);
  * x_out = x1 + omega (b - A x1) / diag(A).  With want_norm, ||dr_2||^2 partials
  * go to scratch[0, count) and ||x1||^2 = ||dr_1||^2 partials to
  * scratch[count, 2 count).  Replaces the first two iterations of
- * `sources/solvers.py:207-219` (x0 = None).  3D, variants 8-10, arrays < 2 GiB
- * (poms_op_from_zero_supported).                                              */
+ * `sources/solvers.py:207-219` (x0 = None).  3D, and 2D without ghost corners;
+ * variants 8-10, arrays < 2 GiB (poms_op_from_zero_supported).               */
 int poms_op_jacobi_from_zero(poms_op* op, double omega, const double* b, double* x_out,
                              int64_t z_begin, int64_t z_end, int want_norm, void* stream);
 int poms_op_from_zero_supported(poms_op* op, int* yes);
+/* Two damped-Jacobi sweeps k, k+1 of `sources/solvers.py:207-219` in one launch:
+ * poms_op_run_reduce2 with epilogue 6 (x -> y; plane range [0, 1)): norm_out <-
+ * ||dr_{k+1}||^2, dot_out <- ||dr_k||^2; x_k is not stored.  y is bitwise the
+ * result of two poms_op_jacobi_sweep calls (variant 9).  One-rank 2D p = 3
+ * Kronecker operators whose sweeps run variant 9, arrays < 2 GiB (1 in *yes);
+ * poms_pcg_jacobi uses it for the smoother's middle sweeps (POMS_J2=0: off).    */
+int poms_op_sweep2_supported(poms_op* op, int* yes);
 /* x = scale * b / diag(A) on the interior.  With scale = 1 this is
  * `jacobi(A, b)` (`sources/solvers.py:139-163`); with scale = omega it is the
  * first damped-Jacobi sweep from x0 = 0 (A.0 = 0 exactly).                    */

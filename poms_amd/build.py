@@ -16,7 +16,7 @@ HERE = Path(__file__).resolve().parent
 CSRC = HERE / "csrc"
 LIB = HERE / "libpoms_hip.so"
 OBJ = HERE / "_obj"
-SOURCES = ["kron_fused.hip", "kron_dpp.hip", "kron_v4.hip", "kron_v5.hip", "vec_ops.hip", "transfer.hip", "kron_solve.hip", "stencil_general.hip", "comm.hip", "poms_abi.hip"]
+SOURCES = ["kron_fused.hip", "kron_dpp.hip", "kron_v4.hip", "kron_v5.hip", "kron_2d.hip", "vec_ops.hip", "transfer.hip", "kron_solve.hip", "stencil_general.hip", "comm.hip", "poms_abi.hip"]
 ARCH = os.environ.get("POMS_OFFLOAD_ARCH", "gfx950")
 
 

@@ -15,7 +15,8 @@ enum Form : int { FORM_SINGLE = 0, FORM_SUM = 1, FORM_STENCIL = 2 };
 enum Epi : int { EPI_APPLY = 0, EPI_RESID = 1, EPI_JACOBI = 2,
                  EPI_JACOBI0 = 3,   /* two damped-Jacobi sweeps from x0 = 0 (x planes = b) */
                  EPI_APPLYDOT = 4,  /* y = A x and per-block sums of x . y              */
-                 EPI_DIAG = 5       /* x = scale b / diag(A) (general stencil form)    */ };
+                 EPI_DIAG = 5,      /* x = scale b / diag(A) (general stencil form)    */
+                 EPI_JACOBI2 = 6    /* two sweeps from x in one launch (2D, kron_2d.hip) */ };
 
 // Geometry of one fused Kronecker launch (all extents local to this rank's slab).
 struct KronGeom {
@@ -83,6 +84,19 @@ struct AlphaFold {
     int sr = 0;                     // V_RUPD: slot of s.r
     int copy_sr = 0;
 };
+
+// 2D Jacobi expressions shared by kron_v3_kernel and kron2d_j2_kernel, written with
+// contraction off so that both kernels form the same bits whatever the compiler
+// fuses around them (the two-sweep launch must reproduce two single sweeps):
+// diag(A) = d1a d2a + d1b d2b, and x_out = x + dr with dr rounded.
+__device__ __forceinline__ double diag2d_sum(double d1a, double d2a, double d1b, double d2b) {
+#pragma clang fp contract(off)
+    return d1a * d2a + d1b * d2b;
+}
+__device__ __forceinline__ double add_nc(double a, double b) {
+#pragma clang fp contract(off)
+    return a + b;
+}
 
 // Padded row layout used by the row-wise vector kernels.
 struct RowGeom {

@@ -198,7 +198,7 @@ kron_v3_kernel(const double* __restrict__ x, double* __restrict__ y,
             dX = d1a * d2a;
             dY = SUM ? (d1b * d2a + d1a * d2b) : 0.0;
         } else {
-            dX = SUM ? (d1a * d2a + d1b * d2b) : d1a * d2a;
+            dX = SUM ? diag2d_sum(d1a, d2a, d1b, d2b) : d1a * d2a;
             dY = 0.0;
         }
     };
@@ -269,7 +269,8 @@ kron_v3_kernel(const double* __restrict__ x, double* __restrict__ y,
                 }
                 if constexpr (J0 && !XRING) ex[r] = omega * eb[r] * rc;   // x1 at the output point
                 const double dr = omega * (eb[r] - v[r]) * rc;
-                outv = ex[r] + dr;
+                if constexpr (IS3D) outv = ex[r] + dr;
+                else outv = add_nc(ex[r], dr);   // (kron2d_j2_kernel's bits)
                 nrm = ok ? fma(dr, dr, nrm) : nrm;
                 if constexpr (J0) dotp = ok ? fma(ex[r], ex[r], dotp) : dotp;   // ||x1||^2 = ||dr_1||^2
                 else dotp = ok ? fma(outv, eb[r], dotp) : dotp;                  // x_out . b (pcg's s.r)
@@ -325,7 +326,7 @@ kron_v3_kernel(const double* __restrict__ x, double* __restrict__ y,
                             // (the row's own band entries: a halo row of a fast1 tile may lie
                             // outside the Toeplitz interior; inside it they equal tc.t1a/t1b[0]
                             // bitwise, which the epilogue uses for the output rows)
-                            dg = SUM ? (q1a * d2a + q1b * d2b) : q1a * d2a;
+                            dg = SUM ? diag2d_sum(q1a, d2a, q1b, d2b) : q1a * d2a;
                         }
                         double rc = __builtin_amdgcn_rcp(dg);
                         double e = fma(-dg, rc, 1.0);

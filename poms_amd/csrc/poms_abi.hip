@@ -31,6 +31,10 @@ void kron_v5_set_launch_events(hipEvent_t e0, hipEvent_t e1);
 bool kron_v5_launch_events_used();
 int kron_tile_rows();
 int kron_v3_rows_2d();
+int kron2d_j2_rows();
+int kron2d_j2_cols(int pmax);
+int kron2d_j2_launch(int pmax, int form, const KronPtrs& p, const KronGeom& g, const ToepConst& tc, double omega,
+                     hipStream_t st);
 int kron_tile_cols();
 int vec_launch(int op, const RowGeom& g, double a, double b, const double* x, const double* y,
                double* z, double* w, const double* q, double* partial, hipStream_t st,
@@ -829,11 +833,56 @@ static int resolve_variant(const poms_op* o, int epi) {
     return v;
 }
 
+// Two Jacobi sweeps per launch (EPI_JACOBI2, kron_2d.hip): one-rank 2D p = 3
+// Kronecker operators whose single sweep runs the v3 whole-array kernel (variant 9),
+// whose bits the two-sweep kernel reproduces
+static bool sweep2_ok(const poms_op* o) {
+    if (o->ndim != 2 || o->pmax != 3 || o->form == FORM_STENCIL || o->ghost_corners) return false;
+    if (o->L.pads[1] != 3 || o->L.pads[2] != 3 || resolve_variant(o, EPI_JACOBI) != 9) return false;
+    const int64_t bytes = (int64_t)(o->L.n[0] + 2 * o->L.pads[0]) * row_geom(&o->L).s0 * 8;
+    return bytes < 0x7ffffff0LL;
+}
+
+// partials as op_run: norm (sweep k+1) and dot (sweep k) at part_dst / the scratch
+static int op_run_j2(poms_op* o, double omega, const double* x, double* y, const double* b, int want_norm,
+                     int want_dot, void* stream) {
+    if (!sweep2_ok(o)) { set_error("two sweeps per launch: one-rank 2D p = 3 Kronecker operators (variant 9) only"); return 1; }
+    if (x == y || b == y) { set_error("two sweeps per launch: x_out must not alias x_in or b"); return 1; }
+    KronGeom g;
+    if (op_geom(o, 0, 1, g, 9, 0, 0, 0, EPI_JACOBI)) return 1;
+    g.tout = kron2d_j2_cols(o->pmax);
+    g.tiles2 = (int)((o->L.n[2] + g.tout - 1) / g.tout);
+    g.tiles1 = (int)((o->L.n[1] + kron2d_j2_rows() - 1) / kron2d_j2_rows());
+    const int64_t nblk = (int64_t)g.tiles2 * g.tiles1;
+    o->last_variant = 9;
+    if (nblk == 0) { o->last_partials = 0; return 0; }
+    const int64_t dbase = o->dot_base < 0 ? nblk : o->dot_base;
+    if ((want_norm || want_dot) && (o->part_off + nblk > dbase || dbase + o->part_off + nblk > kScratch)) {
+        set_error("too many blocks for the partial-sum scratch");
+        return 1;
+    }
+    double* pn = o->ctx->scratch + o->part_off;
+    double* pd = o->ctx->scratch + dbase + o->part_off;
+    o->last_part_host = false;
+    if (o->part_dst && ((want_norm ? 1 : 0) + (want_dot ? 1 : 0)) * nblk <= o->part_cap) {
+        pn = o->part_dst;
+        pd = o->part_dst + (want_norm ? nblk : 0);
+        o->last_part_host = true;
+    }
+    KronPtrs p{x, y, b, o->a0t, o->b0t, o->a1, o->b1, o->a2, o->b2, want_norm ? pn : nullptr,
+               want_dot ? pd : nullptr, nullptr};
+    if (kron2d_j2_launch(o->pmax, o->form, p, g, o->tc, omega, as_stream(stream))) return 1;
+    POMS_HIP_CHECK(hipGetLastError());
+    o->last_partials = (want_norm || want_dot) ? nblk : 0;
+    return 0;
+}
+
 static int op_run(poms_op* o, int epi, double omega, const double* x, double* y, const double* b,
                   int64_t zb, int64_t ze, int want_norm, void* stream, int want_dot = 0,
                   int64_t zb2 = 0, int64_t ze2 = 0) {
     if (!o || !x || !y) { set_error("null operator or vector"); return 1; }
     if (epi != EPI_APPLY && !b) { set_error("null right-hand side"); return 1; }
+    if (epi == EPI_JACOBI2) return op_run_j2(o, omega, x, y, b, want_norm, want_dot, stream);
     if (o->form == FORM_STENCIL)
         return stencil_run(o, epi, omega, x, y, b, zb, ze, want_norm, stream, want_dot, zb2, ze2);
     if (epi == EPI_APPLYDOT && !(o->variant == 4 || o->variant == 8 || o->variant == 9 || o->variant == 10)) {
@@ -981,6 +1030,12 @@ int poms_op_from_zero_supported(poms_op* op, int* yes) {
     return 0;
 }
 
+int poms_op_sweep2_supported(poms_op* op, int* yes) {
+    if (!op || !yes) { set_error("poms_op_sweep2_supported: null argument"); return 1; }
+    *yes = sweep2_ok(op) ? 1 : 0;
+    return 0;
+}
+
 int poms_op_fused_dot_supported(poms_op* op, int* yes) {
     if (!op || !yes) { set_error("poms_op_fused_dot_supported: null argument"); return 1; }
     *yes = fused_dot_ok(op) ? 1 : 0;
@@ -1039,6 +1094,10 @@ static int op_run_epi(poms_op* op, int epilogue, double omega, const double* x, 
             if (b == y) { set_error("jacobi from zero: x_out must not alias b"); return 1; }
             if (wn != wd) { set_error("jacobi from zero: both norms or neither"); return 1; }
             if (op_run(op, EPI_JACOBI0, omega, b, y, b, zb, ze, wn ? 1 : 0, stream, wn ? 1 : 0, zb2, ze2)) return 1;
+            break;
+        case EPI_JACOBI2:   // two sweeps from x: norm_out <- ||dr_{k+1}||^2, dot_out <- ||dr_k||^2
+            if (zb != 0 || ze != 1 || zb2 != ze2) { set_error("two sweeps per launch: 2D (planes [0, 1))"); return 1; }
+            if (op_run(op, EPI_JACOBI2, omega, x, y, b, 0, 1, wn ? 1 : 0, stream, wd ? 1 : 0)) return 1;
             break;
         case EPI_APPLYDOT:
             if (x == y) { set_error("apply: y must not alias x"); return 1; }
@@ -2202,22 +2261,26 @@ struct PcgRun {
         *dot_done = 0;
         double* bufs[3] = {A, B, C};
         const int nb = C ? 3 : 2, depth = C ? 2 : 1;
-        int cur = 0;                         // buffer of the latest queued x
-        struct Pend { int kind, h, buf; };   // 1: sweep norm in slot h; 2: the from-zero pair
-        Pend q[2];
+        // two sweeps per launch (one rank, 2D p = 3, three buffers; POMS_J2=0: off):
+        // sweeps k, k+1 from bufs[cur] into bufs[nxt]; x_k is not stored
+        static const bool j2_env = !(getenv("POMS_J2") && getenv("POMS_J2")[0] == '0');
+        const bool j2 = j2_env && C && direct() && sweep2_ok(op);
+        int cur = 0;                              // buffer of the latest queued x
+        struct Pend { int kind, h, buf, in; };    // 1: sweep norm in slot h; 2: the from-zero
+        Pend q[2];                                // pair; 3: a two-sweep launch from bufs[in]
         int nq = 0, ring = 0, k0;
         int fz = 0;
         if (maxit >= 2 && maxit != 2 && op->form != FORM_STENCIL) (void)poms_op_from_zero_supported(op, &fz);
         if (fz) {   // sweeps 1, 2 from x = 0 in one pass over rhs: [||x1||^2, ||dr2||^2]
             const int h0 = arm(H_J0, 2);
             if (jrun(EPI_JACOBI0, rhs, A, rhs, true, true, h0)) return 1;
-            q[nq++] = Pend{2, h0, 0};
+            q[nq++] = Pend{2, h0, 0, -1};
             k0 = 3;
         } else {
             if (maxit < 1) { set_error("pcg: jacobi maxiter < 1"); return 1; }
             const int h = arm(H_JN, 1);
             if (diag_scale_norm(rhs, A, h)) return 1;
-            q[nq++] = Pend{1, h, 0};
+            q[nq++] = Pend{1, h, 0, -1};
             ring = 1;
             k0 = 2;
         }
@@ -2239,6 +2302,19 @@ struct PcgRun {
                     done = true;
                     res = bufs[f.buf];
                 }
+            } else if (f.kind == 3) {
+                if (get(f.h, 0) < tol2) {   // stopped after sweep k: x_k, one sweep from the
+                    // launch's input (intact: only one launch was queued after it) into the
+                    // buffer that launch wrote (abandoned)
+                    double* xk = bufs[(f.buf + 1) % nb];
+                    if (op_run_epi(op, EPI_JACOBI, o->omega, bufs[f.in], xk, rhs, 0, n0, 0, 0, false, false, stv))
+                        return 1;
+                    done = true;
+                    res = xk;
+                } else if (get(f.h, 1) < tol2) {
+                    done = true;
+                    res = bufs[f.buf];
+                }
             } else if (get(f.h) < tol2) {
                 done = true;
                 res = bufs[f.buf];
@@ -2249,6 +2325,22 @@ struct PcgRun {
             const bool last = k == maxit;
             const int nxt = (cur + 1) % nb;
             int h = -1;
+            if (j2 && k + 1 < maxit) {   // sweeps k, k+1: [||dr_k||^2, ||dr_{k+1}||^2]
+                h = arm(H_J0, 2);
+                if (jrun(EPI_JACOBI2, bufs[cur], bufs[nxt], rhs, true, true, h)) return 1;
+                // every open test is read now: a two-sweep launch's own (below) after the
+                // next launch, because the one after that would overwrite its input
+                while (nq > 0) {
+                    bool done;
+                    double* res = nullptr;
+                    if (settle(done, res)) return 1;
+                    if (done) { *out = res; return 0; }
+                }
+                q[nq++] = Pend{3, h, nxt, cur};
+                cur = nxt;
+                ++k;
+                continue;
+            }
             if (last) {   // the last sweep's norm cannot change the result: x . rhs instead
                 dot_part_n = -1;
                 if (direct() && dot_idx == SC_SRN && op->dot_base < 0 && op->part_off == 0 && !op->part_dst &&
@@ -2266,13 +2358,13 @@ struct PcgRun {
                 ring ^= 1;
             }
             cur = nxt;
-            if (nq == depth) {   // the test of the sweep `depth` back, read after this one is queued
-                bool done;
+            if (nq == depth || (nq > 0 && q[0].kind == 3)) {   // the test of the sweep `depth`
+                bool done;                                      // back, read after this one is queued
                 double* res = nullptr;
                 if (settle(done, res)) return 1;
                 if (done) { *out = res; return 0; }
             }
-            if (!last) q[nq++] = Pend{1, h, cur};
+            if (!last) q[nq++] = Pend{1, h, cur, -1};
         }
         while (nq > 0) {   // tests still open after the last sweep (its own has none)
             bool done;
@@ -2632,7 +2724,10 @@ static int pcg_jacobi_impl(poms_op* op, poms_comm* comm, const poms_pcg_opts* o,
             if (poms_pcg_xp_update_dev(ctx, L, R.sc + SC_ALPHA2, x, p, sn, stream)) return 1;
         }
     }
-    if (R.fix_sr() || R.flush_alpha()) return 1;
+    // (a folded beta's pending s.r_old <- s.r_new is dropped: the next call's first
+    // psolve writes s.r before anything reads it)
+    R.sr_stale = false;
+    if (R.flush_alpha()) return 1;
     if (k > o->maxiter) k = o->maxiter;
     info->niter = k;
     info->success = nrmr < o->tol * nrmr0 ? 1 : 0;

@@ -294,7 +294,7 @@ diag_scale_kernel(const RowGeom g, const int P, const int g0, const double scale
             if constexpr (FORM == FORM_SUM) {
                 const double d2b = dg2b[c];
                 if constexpr (IS3D) diag = d0a * (d1a * d2a) + d0b * (d1b * d2a + d1a * d2b);
-                else diag = d1a * d2a + d1b * d2b;
+                else diag = diag2d_sum(d1a, d2a, d1b, d2b);   // (the 2D sweeps' diag bits)
             } else {
                 diag = d0a * d1a * d2a;
             }

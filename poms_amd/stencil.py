@@ -708,7 +708,7 @@ class KronOperator:
                 raise TypeError("vector does not belong to this operator's space")
 
     # epilogue codes of poms_op_run_reduce
-    _EPI = {"apply": 0, "residual": 1, "jacobi": 2, "jacobi2": 3, "apply_dot": 4}
+    _EPI = {"apply": 0, "residual": 1, "jacobi": 2, "jacobi2": 3, "apply_dot": 4, "sweep2": 6}
 
     def _run(self, kind: str, x: StencilVector, y: StencilVector, b: StencilVector | None = None,
              omega: float = 0.0, norm_out: torch.Tensor | None = None, dot_out: torch.Tensor | None = None):
@@ -895,6 +895,35 @@ class KronOperator:
         v = C.c_int()
         _lib.call("poms_op_from_zero_supported", self._h, C.byref(v))
         return bool(v.value)
+
+    @property
+    def sweep2_supported(self) -> bool:
+        """Two sweeps per launch (``poms_op_sweep2_supported``): one-rank 2D p = 3."""
+        if self.space.is_distributed:
+            return False
+        v = C.c_int()
+        _lib.call("poms_op_sweep2_supported", self._h, C.byref(v))
+        return bool(v.value)
+
+    def jacobi_sweep2(self, b: StencilVector, x_in: StencilVector, x_out: StencilVector, omega: float,
+                      want_norm: bool = False):
+        """Damped-Jacobi sweeps k and k+1 from x_in in one launch; x_out = x_{k+1}
+        (bitwise two :meth:`jacobi_sweep` calls).  Returns ``(||dr_k||^2,
+        ||dr_{k+1}||^2)`` with ``want_norm``, else None."""
+        self._check(b, x_in, x_out)
+        if x_out is x_in or x_out is b:
+            raise ValueError("x_out must not alias x_in or b")
+        if not self.sweep2_supported:
+            raise NotImplementedError("jacobi_sweep2: one-rank 2D p = 3 Kronecker operators only")
+        nb = self.space.scalar_buffer()
+        # norm_out <- ||dr_{k+1}||^2 (slot 1), dot_out <- ||dr_k||^2 (slot 0)
+        self._run("sweep2", x_in, x_out, b=b, omega=omega, norm_out=nb[1:2] if want_norm else None,
+                  dot_out=nb[0:1] if want_norm else None)
+        x_out._mark_written()
+        if not want_norm:
+            return None
+        host = nb.cpu()
+        return float(host[0]), float(host[1])
 
     def jacobi_from_zero(self, b: StencilVector, x_out: StencilVector, omega: float,
                          want_norm: bool = False, lazy: bool = False):

@@ -259,6 +259,68 @@ def test_jacobi_from_zero(gpu, ndim, cells, p, variant):
     assert not bool(g.any())
 
 
+@pytest.mark.parametrize("cells,kind,form,align", [
+    ((64, 64), "spline", "sum", False),
+    ((150, 130), "spline", "sum", True),     # ragged tiles on both axes
+    ((7, 9), "spline", "sum", False),        # smaller than one tile
+    ((1024, 1024), "spline", "sum", True),   # the 2D bench grid (22 x 20 tiles)
+    ((61, 300), "random", "sum", False),     # no Toeplitz interior: band rows per row / per lane
+    ((90, 70), "spline", "product", False),
+    ((100, 97), "random", "product", True),
+])
+def test_jacobi_sweep2(gpu, cells, kind, form, align):
+    """Two damped-Jacobi sweeps per launch (kron_2d.hip, epilogue 6) == two single
+    v3 sweeps, bitwise over the whole storage (ghosts stay zero), into a clean and
+    into a dirty output buffer; both norms (their sums group the points by the
+    two-sweep kernel's tiles: equal to rounding)."""
+    import torch
+    from poms_amd.stencil import KronOperator, StencilVectorSpace
+    p = 3
+    rng = np.random.default_rng(sum(cells))
+    F = [_factors(p, N, rng, kind) for N in cells]
+    n = [N + p for N in cells]
+    V = StencilVectorSpace(n, [p, p], align=align)
+    if form == "sum":
+        A = KronOperator.laplace(V, [f[0] for f in F], [f[1] for f in F])
+    else:
+        A = KronOperator.product(V, [f[0] for f in F])
+    assert A.sweep2_supported
+    b = V.zeros().from_numpy(rng.standard_normal(n))
+    x0 = V.zeros().from_numpy(rng.standard_normal(n))
+    x1, x2 = V.zeros(), V.zeros()
+    om = 2.0 / 3.0
+    n1 = A.jacobi_sweep(b, x0, x1, om, want_norm=True)
+    n2 = A.jacobi_sweep(b, x1, x2, om, want_norm=True)
+    y = V.zeros()
+    m1, m2 = A.jacobi_sweep2(b, x0, y, om, want_norm=True)
+    assert torch.equal(y._data, x2._data)
+    assert abs(m1 - n1) <= 1e-12 * n1 and abs(m2 - n2) <= 1e-12 * n2
+    ref = orc.kron_sum_apply if form == "sum" else None
+    if ref is not None and max(cells) <= 300:   # and against the oracle's two sweeps
+        xr = x0.to_local_numpy()
+        M1, K1, M2, K2 = F[0][0], F[0][1], F[1][0], F[1][1]
+        d1 = lambda B: B[:, p]
+        D = np.outer(d1(M1) + d1(K1), d1(M2)) + np.outer(d1(M1), d1(K2))
+        for _ in range(2):
+            xr = xr + om * (b.to_local_numpy() - ref(xr, [f[0] for f in F], [f[1] for f in F])) / D
+        assert rel(y.to_local_numpy(), xr) <= 1e-12
+    y2 = V.zeros().from_numpy(rng.standard_normal(n))   # stale interior: every point is rewritten
+    assert A.jacobi_sweep2(b, x0, y2, om) is None
+    assert torch.equal(y2._data, x2._data)
+
+
+def test_jacobi_sweep2_supported(gpu):
+    """Two sweeps per launch: one-rank 2D p = 3 only."""
+    from poms_amd.stencil import KronOperator, StencilVectorSpace
+    for nd, p in ((2, 2), (3, 3)):
+        F = assemble_1d(uniform_knots(p, 20), p)
+        V = StencilVectorSpace([20 + p] * nd, [p] * nd)
+        A = KronOperator.laplace(V, [F[0]] * nd, [F[1]] * nd)
+        assert not A.sweep2_supported
+        with pytest.raises(NotImplementedError):
+            A.jacobi_sweep2(V.zeros(), V.zeros(), V.zeros(), 0.5)
+
+
 @pytest.mark.parametrize("variant", [4, 8, 9, 10])
 @pytest.mark.parametrize("ndim,cells,p", [(3, (25, 18, 70), 3), (2, (64, 64), 3), (3, (14, 12, 66), 5)])
 def test_apply_fused_inner(gpu, variant, ndim, cells, p):

@@ -335,6 +335,13 @@ def test_damped_jacobi_maxiter2_stops_after_sweep1(gpu, ndim, N, p):
     (3, 128, 2, 1e-8, False, 1e-6, 4),
     (3, 128, 3, 1e-10, False, 1e-6, 3),
     (3, 96, 3, 1e-7, True, 1e-6, 4),
+    # 2D p = 3 with the lookahead: two sweeps per launch; damped Jacobi stopping at
+    # various sweeps, inside a two-sweep launch (x_k re-formed) or after it
+    (2, 64, 3, 1e-4, False, 1e-6, 10),
+    (2, 64, 3, 1e-6, False, 1e-6, 10),
+    (2, 64, 3, 1e-7, True, 1e-6, 10),
+    (2, 150, 3, 3e-8, False, 1e-6, 10),
+    (2, 150, 3, 1e-9, True, 1e-6, 10),
 ])
 @pytest.mark.parametrize("lookahead", ["0", "1"])
 def test_native_pcg_matches_python_loop(gpu, monkeypatch, lookahead, ndim, N, p, scale, x0, tol, maxiter):
