@@ -134,9 +134,16 @@ constexpr int v5_waves(int P, int EPI, bool SAME12 = true) {
     return ((P == 3 && (EPI != EPI_JACOBI0 || SAME12)) || (P < 3 && EPI != EPI_JACOBI0)) ? 16 : 8;
 }
 
+// Waves per SIMD the build must leave room for (__launch_bounds__): the p >= 4 apply
+// with a 3-deep x ring runs two 8-wave workgroups per CU (78 KB of LDS, <= 128 VGPRs,
+// no scratch) instead of one with a 4-deep ring: at 261^3 p = 5 183.8 -> 132.4 us,
+// p = 4 146.2 -> 101.8 us (MALL-flushed kernel_bench medians, profiles/r06/p45/).  The
+// p = 5 apply + dot spills at 128 VGPRs and keeps one workgroup per CU.
+constexpr int v5_min_waves(int P, int EPI, int D) { return (P >= 4 && EPI == EPI_APPLY && D == 3) ? 4 : 1; }
+
 template <int P, int EPI, int D, int MODE = 0, int CP = 0, bool XH = false, bool ST16 = true, bool JDOT = true,
           bool SAME12 = false>
-__global__ void __launch_bounds__(64 * v5_waves(P, EPI, SAME12), 1)
+__global__ void __launch_bounds__(64 * v5_waves(P, EPI, SAME12), v5_min_waves(P, EPI, D))
 kron_v5_kernel(const double* __restrict__ x, double* __restrict__ y, const double* __restrict__ bvec,
                const double* __restrict__ a0t, const double* __restrict__ b0t,
                const double* __restrict__ a1, const double* __restrict__ b1,
@@ -973,6 +980,8 @@ static int v5_launch_p(int epi, const KronPtrs& p, const KronGeom& g, const Toep
         // vs 10 interleaved on one box, median 548-550 vs 583-621 us, equal minima;
         // the streamed rows made the apply's time scatter, profiles/r02/j0ab/)
         case EPI_APPLY:
+            // p >= 4: a 3-deep x ring, two workgroups per CU (v5_min_waves)
+            if constexpr (P >= 4) return v5_launch_t<P, EPI_APPLY, 3, 0, 6>(p, g, tc, H, omega, st);
             if (store_policy() == 1) return v5_launch_t<P, EPI_APPLY, 4, 0, 2 | 16>(p, g, tc, H, omega, st);
             if (store_policy() == 2) return v5_launch_t<P, EPI_APPLY, 4, 0, 2 | 32>(p, g, tc, H, omega, st);
             return v5_launch_t<P, EPI_APPLY, 4, 0, 6>(p, g, tc, H, omega, st);
