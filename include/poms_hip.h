@@ -249,6 +249,14 @@ int poms_op_from_zero_supported(poms_op* op, int* yes);
  * Kronecker operators whose sweeps run variant 9, arrays < 2 GiB (1 in *yes);
  * poms_pcg_jacobi uses it for the smoother's middle sweeps (POMS_J2=0: off).    */
 int poms_op_sweep2_supported(poms_op* op, int* yes);
+/* Damped-Jacobi sweeps 1-3 of `sources/solvers.py:207-219` from x0 = 0 in one launch
+ * (operators of poms_op_sweep2_supported): x1 = omega b / diag(A) formed as b is
+ * read, then two sweeps; x_out = x3, bitwise poms_op_jacobi_from_zero followed by
+ * poms_op_jacobi_sweep.  norms_out (device, 3 doubles, or NULL) <- ||x1||^2,
+ * ||dr_2||^2, ||dr_3||^2.  poms_pcg_jacobi starts the smoother with it where it runs
+ * the two-sweep launches (POMS_J2FZ=0: off).                                      */
+int poms_op_jacobi3_from_zero(poms_op* op, double omega, const double* b, double* x_out, double* norms_out,
+                              void* stream);
 /* x = scale * b / diag(A) on the interior.  With scale = 1 this is
  * `jacobi(A, b)` (`sources/solvers.py:139-163`); with scale = omega it is the
  * first damped-Jacobi sweep from x0 = 0 (A.0 = 0 exactly).                    */

@@ -117,6 +117,7 @@ _SIGS = {
     "poms_op_jacobi_from_zero": [_vp, _d, _vp, _vp, _i64, _i64, _i, _vp],
     "poms_op_from_zero_supported": [_vp, C.POINTER(_i)],
     "poms_op_sweep2_supported": [_vp, C.POINTER(_i)],
+    "poms_op_jacobi3_from_zero": [_vp, _d, _vp, _vp, _vp, _vp],
     "poms_op_diag_scale": [_vp, _d, _vp, _vp, _i, _vp],
     "poms_op_last_partials": [_vp, C.POINTER(_i64)],
     "poms_op_set_ghost_corners": [_vp, _i],

@@ -16,7 +16,8 @@ enum Epi : int { EPI_APPLY = 0, EPI_RESID = 1, EPI_JACOBI = 2,
                  EPI_JACOBI0 = 3,   /* two damped-Jacobi sweeps from x0 = 0 (x planes = b) */
                  EPI_APPLYDOT = 4,  /* y = A x and per-block sums of x . y              */
                  EPI_DIAG = 5,      /* x = scale b / diag(A) (general stencil form)    */
-                 EPI_JACOBI2 = 6    /* two sweeps from x in one launch (2D, kron_2d.hip) */ };
+                 EPI_JACOBI2 = 6,   /* two sweeps from x in one launch (2D, kron_2d.hip) */
+                 EPI_JACOBI3Z = 7   /* sweeps 1-3 from x = 0 in one launch (2D, kron_2d.hip) */ };
 
 // Geometry of one fused Kronecker launch (all extents local to this rank's slab).
 struct KronGeom {

@@ -35,6 +35,8 @@
 // array < 2 GiB.
 #include "common.hpp"
 
+#include <cstdio>
+#include <cstdlib>
 #include <type_traits>
 
 namespace poms {
@@ -60,12 +62,13 @@ constexpr int kJ2EdgeRows = 4;   // output rows of waves 0 and 7, which also car
 // (44-row tiles: 1027^2 is 24 x 20 = 480 workgroups, one round of the 512 slots)
 constexpr int kJ2Tile = 2 * kJ2EdgeRows + (kJ2Waves - 2) * kJ2Rows;
 
-template <int P, int R, int RE, int FORM>
+template <int P, int R, int RE, int FORM, bool FZ = false>
 __global__ void __launch_bounds__(kJ2Waves * 64, 4)   // 2 workgroups (16 waves) per CU
 kron2d_j2_kernel(const double* __restrict__ x, double* __restrict__ y, const double* __restrict__ bvec,
                  const double* __restrict__ a1, const double* __restrict__ b1,
                  const double* __restrict__ a2, const double* __restrict__ b2,
-                 double* __restrict__ part_k1, double* __restrict__ part_k, const KronGeom g,
+                 double* __restrict__ part_k1, double* __restrict__ part_k, double* __restrict__ part_0,
+                 const KronGeom g,
                  const ToepConst tc, const double omega) {
     constexpr int NW = kJ2Waves;
     constexpr int W = 2 * P + 1;
@@ -76,7 +79,7 @@ kron2d_j2_kernel(const double* __restrict__ x, double* __restrict__ y, const dou
     typedef double d2 __attribute__((ext_vector_type(2)));
     __shared__ d2 ab_[SUM ? XR * 64 : 1];
     __shared__ double as_[SUM ? 1 : XR * 64];
-    __shared__ double red[2 * NW];
+    __shared__ double red[3 * NW];
     __shared__ double c2t[(SUM ? 2 : 1) * W * 64];   // [a|b][k][lane] boundary-tile axis-2 rows
 
     const int tid = threadIdx.x;
@@ -111,7 +114,9 @@ kron2d_j2_kernel(const double* __restrict__ x, double* __restrict__ y, const dou
     // phase-B rows (interior rows r0 - P .. r0 + T + P - 1) inside the axis-1 Toeplitz
     // interior: the band rows from tc (the same values bitwise); in the first and last
     // tile rows by scalar loads of the band table (the rows are wave-uniform)
-    const bool fast1 = (r0 - P >= tc.lo1) && (r0 + T + P <= tc.hi1);
+    // (FZ scales every x-tile row by 1/diag: all of them in the interior)
+    const bool fast1 = FZ ? (r0 - 2 * P >= tc.lo1) && (r0 + T + 2 * P <= tc.hi1)
+                          : (r0 - P >= tc.lo1) && (r0 + T + P <= tc.hi1);
 
     const uint32_t arr_bytes = (uint32_t)((int64_t)(g.n0 + 2 * g.pd0) * g.s0 * 8);
     const __amdgpu_buffer_rsrc_t rx = make_rsrc(x, arr_bytes);
@@ -122,7 +127,7 @@ kron2d_j2_kernel(const double* __restrict__ x, double* __restrict__ y, const dou
     // voffset: the load returns 0
     auto off_of = [&](int q) { return ((r0 - P + q) * (int)g.s1 + (c0 - P + lane)) * 8; };
 
-    double n_k = 0.0, n_k1 = 0.0;
+    double n_k = 0.0, n_k1 = 0.0, n_0 = 0.0;
     // axis 2 of one row held by this lane's column: (sum_k F2a[k] v[c+k-P], sum_k F2b[k] v[c+k-P])
     auto axis2 = [&](double v, double& sa, double& sb, auto c2) {
         double sh[W];
@@ -250,6 +255,23 @@ kron2d_j2_kernel(const double* __restrict__ x, double* __restrict__ y, const dou
         };
         constexpr bool RC1 = F1 && !SLOW2;
         const double rc1 = RC1 ? rdiag(P, d2a, d2b, f1_c) : 0.0;
+        if constexpr (FZ) {
+            // x is b: keep b of the phase-B rows, then x1 = (omega b) / diag(A) at every
+            // x-tile point (poms_op_diag_scale's expression; zero outside the domain)
+#pragma unroll
+            for (int r = 0; r < NB; ++r) Bv[r] = X[BA + r];
+#pragma unroll
+            for (int j = 0; j < NA; ++j) {
+                const int q = a_lo + j;
+                const int ir = r0 - 2 * P + q;
+                const bool ok = col_in && ir >= 0 && ir < g.n1;
+                const double rc = RC1 ? rc1 : rdiag(q, d2a, d2b, f1_c);
+                const double v = omega * X[j] * rc;
+                X[j] = ok ? v : 0.0;
+                const bool own = ok && lane >= 2 * P && lane < 2 * P + TO && q >= 2 * P && q < T + 2 * P;
+                n_0 = own ? fma(v, v, n_0) : n_0;   // ||x1||^2 = ||dr_1||^2
+            }
+        }
         // ---- phase A: axis 2 of x
 #pragma unroll
         for (int j = 0; j < NA; ++j) {
@@ -259,8 +281,10 @@ kron2d_j2_kernel(const double* __restrict__ x, double* __restrict__ y, const dou
             if constexpr (SLOW2) __builtin_amdgcn_sched_barrier(0);
         }
         // b of the phase-B rows (not live during phase A)
+        if constexpr (!FZ) {
 #pragma unroll
-        for (int j = 0; j < NB; ++j) Bv[j] = bload(rb, off_of(b_lo + j));
+            for (int j = 0; j < NB; ++j) Bv[j] = bload(rb, off_of(b_lo + j));
+        }
         __syncthreads();
         // ---- phase B: sweep k on rows [b_lo, b_lo + NB)
         {
@@ -281,7 +305,7 @@ kron2d_j2_kernel(const double* __restrict__ x, double* __restrict__ y, const dou
         }
         double Bd[ND];   // b of the phase-D rows, again (L2): Bv is not kept live past phase B
 #pragma unroll
-        for (int r = 0; r < ND; ++r) Bd[r] = bload(rb, off_of(d_lo + r));
+        for (int r = 0; r < ND; ++r) Bd[r] = FZ ? Bv[DA - BA + r] : bload(rb, off_of(d_lo + r));
         __syncthreads();   // every wave's phase-B reads of the LDS tile are done
         // ---- phase C: axis 2 of x_k
 #pragma unroll
@@ -322,36 +346,76 @@ kron2d_j2_kernel(const double* __restrict__ x, double* __restrict__ y, const dou
         else roles(c2_l, std::false_type{});
     }
 
-    if (part_k1 != nullptr || part_k != nullptr) {
+    if (part_k1 != nullptr || part_k != nullptr || part_0 != nullptr) {
 #pragma unroll
         for (int off = 32; off > 0; off >>= 1) {
             n_k += __shfl_xor(n_k, off, 64);
             n_k1 += __shfl_xor(n_k1, off, 64);
+            if constexpr (FZ) n_0 += __shfl_xor(n_0, off, 64);
         }
         if (lane == 0) {
             red[wv] = n_k;
             red[NW + wv] = n_k1;
+            red[2 * NW + wv] = n_0;
         }
         __syncthreads();
         if (tid == 0) {
-            double s = 0.0, s1 = 0.0;
+            double s = 0.0, s1 = 0.0, s0 = 0.0;
             for (int w = 0; w < NW; ++w) {
                 s += red[w];
                 s1 += red[NW + w];
+                s0 += red[2 * NW + w];
             }
             if (part_k != nullptr) part_k[blockIdx.x] = s;
             if (part_k1 != nullptr) part_k1[blockIdx.x] = s1;
+            if (FZ && part_0 != nullptr) part_0[blockIdx.x] = s0;
         }
     }
 }
 
-int kron2d_j2_rows() { return kJ2Tile; }
+// tile shape (R, RE): POMS_J2_TILE=r,re (tuning: 6,4 default; 7,5; 6,5; 5,4; 5,3)
+static void j2_tile(int* r, int* re) {
+    static int R = -1, RE = -1;
+    if (R < 0) {
+        R = kJ2Rows;
+        RE = kJ2EdgeRows;
+        if (const char* e = getenv("POMS_J2_TILE")) {
+            int a = 0, b = 0;
+            if (sscanf(e, "%d,%d", &a, &b) == 2 &&
+                ((a == 7 && b == 5) || (a == 6 && b == 5) || (a == 5 && b == 4) || (a == 5 && b == 3))) {
+                R = a;
+                RE = b;
+            }
+        }
+    }
+    *r = R;
+    *re = RE;
+}
+int kron2d_j2_rows() {
+    int r, re;
+    j2_tile(&r, &re);
+    return 2 * re + (kJ2Waves - 2) * r;
+}
+int kron2d_j2_rows_default() { return kJ2Tile; }
 int kron2d_j2_cols(int pmax) { return 64 - 4 * pmax; }
 
+template <int R, int RE, bool FZ = false>
+static void j2_launch_t(int form, const KronPtrs& p, double* part0, const KronGeom& g, const ToepConst& tc,
+                        double omega, hipStream_t st, int nblk) {
+    if (form == FORM_SUM)
+        hipLaunchKernelGGL((kron2d_j2_kernel<3, R, RE, FORM_SUM, FZ>), dim3(nblk), dim3(kJ2Waves * 64), 0, st, p.x,
+                           p.y, p.b, p.a1, p.b1, p.a2, p.b2, p.partial, p.partial2, part0, g, tc, omega);
+    else
+        hipLaunchKernelGGL((kron2d_j2_kernel<3, R, RE, FORM_SINGLE, FZ>), dim3(nblk), dim3(kJ2Waves * 64), 0, st, p.x,
+                           p.y, p.b, p.a1, p.b1, p.a2, p.b2, p.partial, p.partial2, part0, g, tc, omega);
+}
+
 // Two sweeps x -> y; p.partial: sweep k+1's ||dr||^2 per block, p.partial2: sweep k's.
+// from_zero: sweeps 1-3 from x = 0 (p.x = p.b), part0: ||x1||^2 per block (p.partial2:
+// sweep 2, p.partial: sweep 3).
 // g: the operator's 2D geometry with tiles1 / tiles2 for kron2d_j2_rows / _cols.
 int kron2d_j2_launch(int pmax, int form, const KronPtrs& p, const KronGeom& g, const ToepConst& tc, double omega,
-                     hipStream_t st) {
+                     hipStream_t st, bool from_zero, double* part0) {
     if (pmax != 3 || (form != FORM_SUM && form != FORM_SINGLE)) {
         set_error("two sweeps per launch: 2D p = 3 Kronecker operators only");
         return 1;
@@ -362,12 +426,18 @@ int kron2d_j2_launch(int pmax, int form, const KronPtrs& p, const KronGeom& g, c
         return 1;
     }
     const int nblk = g.tiles1 * g.tiles2;
-    if (form == FORM_SUM)
-        hipLaunchKernelGGL((kron2d_j2_kernel<3, kJ2Rows, kJ2EdgeRows, FORM_SUM>), dim3(nblk), dim3(kJ2Waves * 64), 0, st, p.x, p.y,
-                           p.b, p.a1, p.b1, p.a2, p.b2, p.partial, p.partial2, g, tc, omega);
-    else
-        hipLaunchKernelGGL((kron2d_j2_kernel<3, kJ2Rows, kJ2EdgeRows, FORM_SINGLE>), dim3(nblk), dim3(kJ2Waves * 64), 0, st, p.x,
-                           p.y, p.b, p.a1, p.b1, p.a2, p.b2, p.partial, p.partial2, g, tc, omega);
+    int r, re;
+    j2_tile(&r, &re);
+    if (from_zero) {   // (the default tile only)
+        if (r != kJ2Rows || re != kJ2EdgeRows) { set_error("three sweeps from zero: default tile only"); return 1; }
+        j2_launch_t<kJ2Rows, kJ2EdgeRows, true>(form, p, part0, g, tc, omega, st, nblk);
+        return 0;
+    }
+    if (r == 7) j2_launch_t<7, 5>(form, p, nullptr, g, tc, omega, st, nblk);
+    else if (r == 6 && re == 5) j2_launch_t<6, 5>(form, p, nullptr, g, tc, omega, st, nblk);
+    else if (r == 5 && re == 4) j2_launch_t<5, 4>(form, p, nullptr, g, tc, omega, st, nblk);
+    else if (r == 5 && re == 3) j2_launch_t<5, 3>(form, p, nullptr, g, tc, omega, st, nblk);
+    else j2_launch_t<kJ2Rows, kJ2EdgeRows>(form, p, nullptr, g, tc, omega, st, nblk);
     return 0;
 }
 

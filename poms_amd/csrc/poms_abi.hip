@@ -34,7 +34,8 @@ int kron_v3_rows_2d();
 int kron2d_j2_rows();
 int kron2d_j2_cols(int pmax);
 int kron2d_j2_launch(int pmax, int form, const KronPtrs& p, const KronGeom& g, const ToepConst& tc, double omega,
-                     hipStream_t st);
+                     hipStream_t st, bool from_zero, double* part0);
+int kron2d_j2_rows_default();
 int kron_tile_cols();
 int vec_launch(int op, const RowGeom& g, double a, double b, const double* x, const double* y,
                double* z, double* w, const double* q, double* partial, hipStream_t st,
@@ -843,19 +844,45 @@ static bool sweep2_ok(const poms_op* o) {
     return bytes < 0x7ffffff0LL;
 }
 
-// partials as op_run: norm (sweep k+1) and dot (sweep k) at part_dst / the scratch
-static int op_run_j2(poms_op* o, double omega, const double* x, double* y, const double* b, int want_norm,
+// partials as op_run: norm (sweep k+1) and dot (sweep k) at part_dst / the scratch.
+// EPI_JACOBI3Z (x = b): all three sums or none, ||x1||^2, ||dr_2||^2, ||dr_3||^2 side by
+// side (part_dst, or scratch[0, 3n))
+static int op_run_j2(poms_op* o, int epi, double omega, const double* x, double* y, const double* b, int want_norm,
                      int want_dot, void* stream) {
     if (!sweep2_ok(o)) { set_error("two sweeps per launch: one-rank 2D p = 3 Kronecker operators (variant 9) only"); return 1; }
     if (x == y || b == y) { set_error("two sweeps per launch: x_out must not alias x_in or b"); return 1; }
+    const bool fz = epi == EPI_JACOBI3Z;
+    if (fz && (x != b || want_norm != want_dot)) { set_error("three sweeps from zero: x = b, all three sums or none"); return 1; }
     KronGeom g;
     if (op_geom(o, 0, 1, g, 9, 0, 0, 0, EPI_JACOBI)) return 1;
+    const int trows = fz ? kron2d_j2_rows_default() : kron2d_j2_rows();
     g.tout = kron2d_j2_cols(o->pmax);
     g.tiles2 = (int)((o->L.n[2] + g.tout - 1) / g.tout);
-    g.tiles1 = (int)((o->L.n[1] + kron2d_j2_rows() - 1) / kron2d_j2_rows());
+    g.tiles1 = (int)((o->L.n[1] + trows - 1) / trows);
     const int64_t nblk = (int64_t)g.tiles2 * g.tiles1;
     o->last_variant = 9;
     if (nblk == 0) { o->last_partials = 0; return 0; }
+    if (fz) {
+        double* s0 = nullptr;
+        o->last_part_host = false;
+        if (want_norm) {
+            if (o->part_dst && 3 * nblk <= o->part_cap) {
+                s0 = o->part_dst;
+                o->last_part_host = true;
+            } else if (o->part_off == 0 && o->dot_base < 0 && 3 * nblk <= kScratch) {
+                s0 = o->ctx->scratch;
+            } else {
+                set_error("too many blocks for the partial-sum scratch");
+                return 1;
+            }
+        }
+        KronPtrs p{b, y, b, o->a0t, o->b0t, o->a1, o->b1, o->a2, o->b2, s0 ? s0 + 2 * nblk : nullptr,
+                   s0 ? s0 + nblk : nullptr, nullptr};
+        if (kron2d_j2_launch(o->pmax, o->form, p, g, o->tc, omega, as_stream(stream), true, s0)) return 1;
+        POMS_HIP_CHECK(hipGetLastError());
+        o->last_partials = want_norm ? nblk : 0;
+        return 0;
+    }
     const int64_t dbase = o->dot_base < 0 ? nblk : o->dot_base;
     if ((want_norm || want_dot) && (o->part_off + nblk > dbase || dbase + o->part_off + nblk > kScratch)) {
         set_error("too many blocks for the partial-sum scratch");
@@ -871,7 +898,7 @@ static int op_run_j2(poms_op* o, double omega, const double* x, double* y, const
     }
     KronPtrs p{x, y, b, o->a0t, o->b0t, o->a1, o->b1, o->a2, o->b2, want_norm ? pn : nullptr,
                want_dot ? pd : nullptr, nullptr};
-    if (kron2d_j2_launch(o->pmax, o->form, p, g, o->tc, omega, as_stream(stream))) return 1;
+    if (kron2d_j2_launch(o->pmax, o->form, p, g, o->tc, omega, as_stream(stream), false, nullptr)) return 1;
     POMS_HIP_CHECK(hipGetLastError());
     o->last_partials = (want_norm || want_dot) ? nblk : 0;
     return 0;
@@ -882,7 +909,7 @@ static int op_run(poms_op* o, int epi, double omega, const double* x, double* y,
                   int64_t zb2 = 0, int64_t ze2 = 0) {
     if (!o || !x || !y) { set_error("null operator or vector"); return 1; }
     if (epi != EPI_APPLY && !b) { set_error("null right-hand side"); return 1; }
-    if (epi == EPI_JACOBI2) return op_run_j2(o, omega, x, y, b, want_norm, want_dot, stream);
+    if (epi == EPI_JACOBI2 || epi == EPI_JACOBI3Z) return op_run_j2(o, epi, omega, x, y, b, want_norm, want_dot, stream);
     if (o->form == FORM_STENCIL)
         return stencil_run(o, epi, omega, x, y, b, zb, ze, want_norm, stream, want_dot, zb2, ze2);
     if (epi == EPI_APPLYDOT && !(o->variant == 4 || o->variant == 8 || o->variant == 9 || o->variant == 10)) {
@@ -1036,6 +1063,18 @@ int poms_op_sweep2_supported(poms_op* op, int* yes) {
     return 0;
 }
 
+int poms_op_jacobi3_from_zero(poms_op* op, double omega, const double* b, double* x_out, double* norms_out,
+                              void* stream) {
+    if (!op || !b || !x_out) { set_error("jacobi3 from zero: null argument"); return 1; }
+    const bool wn = norms_out != nullptr;
+    if (op_run(op, EPI_JACOBI3Z, omega, b, x_out, b, 0, 1, wn ? 1 : 0, stream, wn ? 1 : 0)) return 1;
+    const int64_t n = op->last_partials;
+    if (wn)
+        for (int i = 0; i < 3; ++i) reduce_launch(op->ctx->scratch + i * n, (int)n, norms_out + i, as_stream(stream));
+    POMS_HIP_CHECK(hipGetLastError());
+    return 0;
+}
+
 int poms_op_fused_dot_supported(poms_op* op, int* yes) {
     if (!op || !yes) { set_error("poms_op_fused_dot_supported: null argument"); return 1; }
     *yes = fused_dot_ok(op) ? 1 : 0;
@@ -1098,6 +1137,11 @@ static int op_run_epi(poms_op* op, int epilogue, double omega, const double* x, 
         case EPI_JACOBI2:   // two sweeps from x: norm_out <- ||dr_{k+1}||^2, dot_out <- ||dr_k||^2
             if (zb != 0 || ze != 1 || zb2 != ze2) { set_error("two sweeps per launch: 2D (planes [0, 1))"); return 1; }
             if (op_run(op, EPI_JACOBI2, omega, x, y, b, 0, 1, wn ? 1 : 0, stream, wd ? 1 : 0)) return 1;
+            break;
+        case EPI_JACOBI3Z:   // sweeps 1-3 from x = 0 (x = b): norm_out <- ||dr_3||^2, dot_out <- ||dr_2||^2
+            // (poms_op_run_reduce2 cannot return the third sum: poms_op_jacobi3_from_zero)
+            if (zb != 0 || ze != 1 || zb2 != ze2) { set_error("three sweeps from zero: 2D (planes [0, 1))"); return 1; }
+            if (op_run(op, EPI_JACOBI3Z, omega, b, y, b, 0, 1, wn ? 1 : 0, stream, wd ? 1 : 0)) return 1;
             break;
         case EPI_APPLYDOT:
             if (x == y) { set_error("apply: y must not alias x"); return 1; }
@@ -1973,6 +2017,23 @@ struct PcgRun {
                                 (int)op->L.pads[0], op->pmax, o->prev, o->next, 1, wn ? 1 : 0, wd ? 1 : 0, nullptr,
                                 nullptr, (wn ? 1 : 0) + (wd ? 1 : 0), host + h, &tk[h], stv);
     }
+    // sweeps 1-3 from x = 0 (one rank): [||x1||^2, ||dr_2||^2, ||dr_3||^2] into slots h .. h+2
+    int jrun3(const double* rhs, double* y, int h) {
+        op->part_dst = op->sv_part + (size_t)h * poms_op::kSvPart;
+        op->part_cap = 3 * host_partials_max();
+        const int rc = op_run_epi(op, EPI_JACOBI3Z, o->omega, rhs, y, rhs, 0, n0, 0, 0, true, true, stv);
+        op->part_dst = nullptr;
+        if (rc) return 1;
+        const int64_t n = op->last_partials;
+        if (op->last_part_host) {
+            op->sv_npart[h] = (int)n;
+            op->sv_pkind[h] = 4;
+            return 0;
+        }
+        for (int i = 0; i < 3; ++i) reduce_launch(op->ctx->scratch + i * n, (int)n, host + h + i, st);
+        POMS_HIP_CHECK(hipGetLastError());
+        return 0;
+    }
     // Arm `cnt` consecutive host slots for the next launch and return the first.
     // Direct mode takes fresh slots from a ring: a launch the loop abandoned (an
     // early damped-Jacobi stop leaves the next sweep queued) still writes ITS slot
@@ -1994,8 +2055,7 @@ struct PcgRun {
             reinterpret_cast<volatile double*>(host)[h + i] = -1.0;   // norms are >= 0
             op->sv_seq[h + i] = op->sv_seq_next;
             if (op->sv_npart[h + i] > 0) {   // an abandoned launch's partials (complete by now): re-arm
-                const int nsum = ((op->sv_pkind[h + i] & 1) ? 1 : 0) + ((op->sv_pkind[h + i] & 2) ? 1 : 0);
-                part_arm(op->sv_part + (size_t)(h + i) * poms_op::kSvPart, nsum * op->sv_npart[h + i]);
+                part_arm(op->sv_part + (size_t)(h + i) * poms_op::kSvPart, pk_nsum(op->sv_pkind[h + i]) * op->sv_npart[h + i]);
                 op->sv_npart[h + i] = 0;
                 op->sv_pkind[h + i] = 0;
             }
@@ -2035,7 +2095,7 @@ struct PcgRun {
     int settle_partials(int h) {
         const int n = op->sv_npart[h];
         double* reg = op->sv_part + (size_t)h * poms_op::kSvPart;
-        const int nsum = ((op->sv_pkind[h] & 1) ? 1 : 0) + ((op->sv_pkind[h] & 2) ? 1 : 0);
+        const int nsum = pk_nsum(op->sv_pkind[h]);
         for (int i = 0; i < nsum * n; ++i) {
             for (long k = 1; part_unset(reg + i); ++k) {
                 __builtin_ia32_pause();
@@ -2047,13 +2107,19 @@ struct PcgRun {
         }
         std::atomic_thread_fence(std::memory_order_acquire);
         const bool wn = op->sv_pkind[h] & 1, wd = op->sv_pkind[h] & 2;
-        if (wn) host[h + (wd ? 1 : 0)] = host_reduce(reg, n);
-        if (wd) host[h] = host_reduce(reg + (wn ? n : 0), n);
+        if (op->sv_pkind[h] & 4) {   // three sums, slots h .. h+2 (EPI_JACOBI3Z)
+            for (int i = 0; i < 3; ++i) host[h + i] = host_reduce(reg + (size_t)i * n, n);
+        } else {
+            if (wn) host[h + (wd ? 1 : 0)] = host_reduce(reg, n);
+            if (wd) host[h] = host_reduce(reg + (wn ? n : 0), n);
+        }
         part_arm(reg, nsum * n);
         op->sv_npart[h] = 0;
         op->sv_pkind[h] = 0;
         return 0;
     }
+    // sums in a slot region: bit 0 a norm, bit 1 a dot, bit 2 three sums (EPI_JACOBI3Z)
+    static int pk_nsum(int pk) { return (pk & 4) ? 3 : ((pk & 1) ? 1 : 0) + ((pk & 2) ? 1 : 0); }
     static bool part_unset(const double* v) {
         uint64_t u;
         const volatile uint64_t* q = reinterpret_cast<const volatile uint64_t*>(v);
@@ -2267,11 +2333,19 @@ struct PcgRun {
         const bool j2 = j2_env && C && direct() && sweep2_ok(op);
         int cur = 0;                              // buffer of the latest queued x
         struct Pend { int kind, h, buf, in; };    // 1: sweep norm in slot h; 2: the from-zero
-        Pend q[2];                                // pair; 3: a two-sweep launch from bufs[in]
+        Pend q[2];                                // pair; 3: a two-sweep launch from bufs[in];
+                                                  // 5: sweeps 1-3 from zero
         int nq = 0, ring = 0, k0;
         int fz = 0;
         if (maxit >= 2 && maxit != 2 && op->form != FORM_STENCIL) (void)poms_op_from_zero_supported(op, &fz);
-        if (fz) {   // sweeps 1, 2 from x = 0 in one pass over rhs: [||x1||^2, ||dr2||^2]
+        // sweeps 1-3 from x = 0 in one launch where the two-sweep launches run (POMS_J2FZ=0: off)
+        static const bool j3_env = !(getenv("POMS_J2FZ") && getenv("POMS_J2FZ")[0] == '0');
+        if (fz && j2 && j3_env && maxit >= 4) {   // [||x1||^2, ||dr2||^2, ||dr3||^2]
+            const int h0 = arm(H_J0, 3);
+            if (jrun3(rhs, A, h0)) return 1;
+            q[nq++] = Pend{5, h0, 0, -1};
+            k0 = 4;
+        } else if (fz) {   // sweeps 1, 2 from x = 0 in one pass over rhs: [||x1||^2, ||dr2||^2]
             const int h0 = arm(H_J0, 2);
             if (jrun(EPI_JACOBI0, rhs, A, rhs, true, true, h0)) return 1;
             q[nq++] = Pend{2, h0, 0, -1};
@@ -2299,6 +2373,20 @@ struct PcgRun {
                     done = true;
                     res = x1;
                 } else if (get(f.h, 1) < tol2) {
+                    done = true;
+                    res = bufs[f.buf];
+                }
+            } else if (f.kind == 5) {   // sweeps 1-3 from zero; x1 and x2 re-formed into the
+                double* xr = bufs[(f.buf + 1) % nb];   // buffer the abandoned next launch wrote
+                if (get(f.h, 0) < tol2) {
+                    if (poms_op_diag_scale(op, o->omega, rhs, xr, 0, stv)) return 1;
+                    done = true;
+                    res = xr;
+                } else if (get(f.h, 1) < tol2) {
+                    if (op_run_epi(op, EPI_JACOBI0, o->omega, rhs, xr, rhs, 0, n0, 0, 0, false, false, stv)) return 1;
+                    done = true;
+                    res = xr;
+                } else if (get(f.h, 2) < tol2) {
                     done = true;
                     res = bufs[f.buf];
                 }
@@ -2358,7 +2446,7 @@ struct PcgRun {
                 ring ^= 1;
             }
             cur = nxt;
-            if (nq == depth || (nq > 0 && q[0].kind == 3)) {   // the test of the sweep `depth`
+            if (nq == depth || (nq > 0 && (q[0].kind == 3 || q[0].kind == 5))) {   // the test of the sweep `depth`
                 bool done;                                      // back, read after this one is queued
                 double* res = nullptr;
                 if (settle(done, res)) return 1;

@@ -925,6 +925,24 @@ class KronOperator:
         host = nb.cpu()
         return float(host[0]), float(host[1])
 
+    def jacobi3_from_zero(self, b: StencilVector, x_out: StencilVector, omega: float, want_norm: bool = False):
+        """Damped-Jacobi sweeps 1-3 from x0 = 0 in one launch (``poms_op_jacobi3_from_zero``;
+        the operators of :attr:`sweep2_supported`); x_out = x3.  Returns ``(||x1||^2,
+        ||dr_2||^2, ||dr_3||^2)`` with ``want_norm``, else None."""
+        self._check(b, x_out)
+        if x_out is b:
+            raise ValueError("x_out must not alias b")
+        if not self.sweep2_supported:
+            raise NotImplementedError("jacobi3_from_zero: one-rank 2D p = 3 Kronecker operators only")
+        nb = self.space.scalar_buffer()
+        _lib.call("poms_op_jacobi3_from_zero", self._h, float(omega), rt.ptr(b._data), rt.ptr(x_out._data),
+                  rt.ptr(nb[0:3]) if want_norm else None, _stream())
+        x_out._mark_written()
+        if not want_norm:
+            return None
+        host = nb.cpu()
+        return float(host[0]), float(host[1]), float(host[2])
+
     def jacobi_from_zero(self, b: StencilVector, x_out: StencilVector, omega: float,
                          want_norm: bool = False, lazy: bool = False):
         """Damped-Jacobi sweeps 1 and 2 from x0 = 0 in one pass over b; x_out = x2.

@@ -309,6 +309,33 @@ def test_jacobi_sweep2(gpu, cells, kind, form, align):
     assert torch.equal(y2._data, x2._data)
 
 
+@pytest.mark.parametrize("cells,kind", [((64, 64), "spline"), ((150, 130), "spline"), ((7, 9), "spline"),
+                                        ((1024, 1024), "spline"), ((61, 300), "random")])
+def test_jacobi3_from_zero(gpu, cells, kind):
+    """Sweeps 1-3 from zero in one launch (epilogue 7) == the from-zero pair followed by
+    one sweep, bitwise; the three norms to rounding."""
+    import torch
+    from poms_amd.stencil import KronOperator, StencilVectorSpace
+    p = 3
+    rng = np.random.default_rng(sum(cells) + 1)
+    F = [_factors(p, N, rng, kind) for N in cells]
+    n = [N + p for N in cells]
+    V = StencilVectorSpace(n, [p, p], align=True)
+    A = KronOperator.laplace(V, [f[0] for f in F], [f[1] for f in F])
+    b = V.zeros().from_numpy(rng.standard_normal(n))
+    x2, x3 = V.zeros(), V.zeros()
+    om = 2.0 / 3.0
+    n1, n2 = A.jacobi_from_zero(b, x2, om, want_norm=True)
+    n3 = A.jacobi_sweep(b, x2, x3, om, want_norm=True)
+    y = V.zeros().from_numpy(rng.standard_normal(n))   # stale interior: every point is rewritten
+    m1, m2, m3 = A.jacobi3_from_zero(b, y, om, want_norm=True)
+    assert torch.equal(y._data, x3._data)
+    for a, c in ((m1, n1), (m2, n2), (m3, n3)):
+        assert abs(a - c) <= 1e-12 * c
+    assert A.jacobi3_from_zero(b, y, om) is None
+    assert torch.equal(y._data, x3._data)
+
+
 def test_jacobi_sweep2_supported(gpu):
     """Two sweeps per launch: one-rank 2D p = 3 only."""
     from poms_amd.stencil import KronOperator, StencilVectorSpace
