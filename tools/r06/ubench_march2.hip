@@ -1,3 +1,5 @@
+// Build: hipcc --offload-arch=gfx950 -O3 tools/r06/ubench_march2.hip -o tools/r06/ubench_march2.bin;
+// run: tools/r06/ubench_march2.bin [case] [fill]  (case: one measurement, else all; fill 1: non-zero x).
 // Round 6: memory-only models of the p = 3 apply's march at 515^3 (line-aligned
 // layout: pitch 528, interior column 0 on a 128-B line), as tools/ubench_march.hip,
 // with two additions:

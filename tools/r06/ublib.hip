@@ -1,3 +1,5 @@
+// Build (CPU side, in-tree): hipcc --offload-arch=gfx950 -O3 -shared -fPIC tools/r06/ublib.hip -o tools/r06/ublib.so
+// (loaded by tools/r06/ublib_bench.py and ublib_offsets.py).
 // Round 6: memory-only models of the p = 3 apply's march at 515^3 (line-aligned
 // layout: pitch 528, interior column 0 on a 128-B line), as tools/ubench_march.hip,
 // with two additions:
