@@ -110,6 +110,9 @@ struct poms_op {
     // at scratch + (dot_base < 0 ? nblk : dot_base) + part_off (op_run_split puts two
     // launches' partials side by side and reduces them once)
     int64_t part_off = 0, dot_base = -1;
+    // op_run_split's interior launch: the communication stream's exchange and boundary
+    // launch run beside it (the automatic chunking leaves them CUs, op_geom)
+    bool split_interior = false;
     int ndim = 3, form = FORM_SUM, pmax = 1, chunk = 0, tout = 0;
     poms_layout L{};
     int64_t g0 = 0, n0g = 1;
@@ -745,13 +748,33 @@ static int op_geom(poms_op* o, int64_t zb, int64_t ze, KronGeom& g, int v = -1, 
     const int nz = (int)(ze - zb) + (int)(ze2 - zb2);
     int chunk = o->chunk;
     if (chunk <= 0) {
-        chunk = auto_chunk(nz, g.tiles2 * g.tiles1, o->pmax, v == 10 ? 256.0 : 512.0);
+        const double slots = v == 10 ? 256.0 : 512.0;
+        const int tiles = g.tiles2 * g.tiles1;
+        chunk = auto_chunk(nz, tiles, o->pmax, slots);
+        // The interior launch of a distributed call shares the GPU with the exchange and
+        // the boundary launch on the communication stream: one chunk (one short round
+        // that leaves CUs to them) where it fits 3/4 of the slots and costs at most 1.4x
+        // the plane steps of the chunked grid (POMS_SPLIT_ONE=0: off).  Loopback proxy,
+        // rank 1, interleaved (profiles/r06/split_chunk/): 8 ranks (59 interior planes)
+        // 41.7-41.8 -> 38.7-38.9 ms per cycle, 4 ranks (123) 60.6-60.8 -> 58.8-59.1 ms;
+        // at 2 ranks (252 planes, 1.43x) one chunk was slower (103.7 -> 111.1 ms) and
+        // the rule keeps the chunks there
+        static const bool split_one = !(getenv("POMS_SPLIT_ONE") && getenv("POMS_SPLIT_ONE")[0] == '0');
+        bool one = false;
+        if (o->split_interior && split_one && tiles <= 0.75 * slots && chunk < nz) {
+            const int nc = (nz + chunk - 1) / chunk;
+            const double r = (double)nc * tiles / slots;
+            const double fr = std::floor(r);
+            const double rounds = r > 1.0 ? fr + std::min(1.0, (r - fr) * 5.0) : 1.0;
+            one = nz + 2 * o->pmax <= 1.4 * rounds * (chunk + 2 * o->pmax);
+            if (one) chunk = nz;
+        }
         // the v5 two-sweeps-from-zero launch (VALU-bound) balances better over twice
         // as many chunks: 515^3 p = 3, 86 instead of 172 planes, 836-838 against
         // 865-882 us in two interleaved sweeps, equal medians (833 us) in a third
         // (profiles/r03/chunks/); the other epilogues keep the model's pick (Jacobi
         // 715 us at 172 against 729 at 86)
-        if (v == 10 && epi == EPI_JACOBI0 && o->pmax == 3 && same_toeplitz12(o) && chunk / 2 >= 8 * o->pmax)
+        if (!one && v == 10 && epi == EPI_JACOBI0 && o->pmax == 3 && same_toeplitz12(o) && chunk / 2 >= 8 * o->pmax)
             chunk = (chunk + 1) / 2;   // (the 16-wave build only)
     }
     chunk = std::max(1, std::min(chunk, std::max(nz, 1)));
@@ -1181,7 +1204,10 @@ int op_run_split(poms_op* op, int epilogue, double omega, const double* x, doubl
     } reset{op};
     op->part_off = 0;
     op->dot_base = kScratch / 2;
-    if (op_run_epi(op, epilogue, omega, x, y, b, ib, ie, 0, 0, wn, wd, stream)) return 1;
+    op->split_interior = true;
+    const int rci = op_run_epi(op, epilogue, omega, x, y, b, ib, ie, 0, 0, wn, wd, stream);
+    op->split_interior = false;
+    if (rci) return 1;
     const int64_t n1 = op->last_partials;
     void* bs = h.bstream ? h.bstream : stream;
     if (h.ghosts_on(h.arg, bs)) return 1;
