@@ -339,6 +339,18 @@ int poms_restrict(poms_transfer* tr, const double* fine, double* coarse, void* s
 /* fine += (P0 (x) P1 (x) P2) coarse on the local slab.
  * Replaces `xc_p = P.dot(xc)` + `xf = xf + rf` (`sources/mg_jac.py:102-112`). */
 int poms_prolong_add(poms_transfer* tr, const double* coarse, double* fine, void* stream);
+/* Fused residual -> restriction (`sources/mg_jac.py:93-94`, `rf = bf - Af.dot(xf)`
+ * then `rc = R.dot(rf)`): set once per operator, then
+ *   coarse = R (b - A x)   (local slab contribution; the caller all-reduces)
+ * with r = b - A x never stored.  G[r] are HOST dense row-major (rows_d x nc_d)
+ * matrices F_r^T P_d, one per role of poms_op_create's factor list (FORM_SUM: A0 M0
+ * A1 B1 M2 K2; FORM_SINGLE: F0 - F1 - F2 -; 2D: roles 0 and 1 unused), rows as the
+ * P_d given to poms_transfer_create.  x needs no up-to-date ghost regions.
+ * Results equal poms_op_residual + poms_restrict to rounding (R b - (R A) x is
+ * summed in another order).  Dense-P transfers only (nc_d <= 32).              */
+int poms_transfer_set_operator(poms_transfer* tr, int form, const double* const* G);
+int poms_resid_restrict(poms_transfer* tr, const double* b, const double* x, double* coarse,
+                        void* stream);
 
 /* ---- coarse solve ---------------------------------------------------------- */
 /* y = Minv x with a dense (n x n) row-major DEVICE matrix (the factorised

@@ -136,6 +136,8 @@ _SIGS = {
     "poms_transfer_destroy": [_vp],
     "poms_restrict": [_vp, _vp, _vp, _vp],
     "poms_prolong_add": [_vp, _vp, _vp, _vp],
+    "poms_transfer_set_operator": [_vp, _i, C.POINTER(C.c_void_p)],
+    "poms_resid_restrict": [_vp, _vp, _vp, _vp, _vp],
     "poms_dense_matvec": [_vp, _i64, _vp, _vp, _vp, _vp],
     "poms_ksolve_create": [_vp, _i, _LP, _i64, C.POINTER(C.c_void_p), C.POINTER(_i64), C.POINTER(_i),
                            C.POINTER(_i), _pp],

@@ -1,5 +1,6 @@
 // extern "C" boundary of libpoms_hip.so (declared in include/poms_hip.h).
 #include "common.hpp"
+#include "transfer.hpp"
 #include "split_hooks.hpp"
 #include "../../include/poms_hip.h"
 
@@ -242,6 +243,15 @@ struct poms_transfer {
     double *t0 = nullptr, *t1 = nullptr;
     double* part = nullptr;   // split-axis restriction partials (few lines)
     int64_t part_n = 0;
+    // fused residual -> restriction (poms_transfer_set_operator / poms_resid_restrict)
+    int rform = -1;           // POMS_FORM_SUM / POMS_FORM_SINGLE; -1: no operator set
+    int ncf = 0;              // columns of the fused passes' matrices (8, 12, 16, 32)
+    double* Gf[6]{};          // F^T P per operator role (last axis negated), ncf columns
+    double* Pf[3]{};          // P, ncf columns
+    double* ru = nullptr;     // axis-0 outputs: 3 x [c0][n1][n2]
+    double* rv = nullptr;     // axis-1 outputs: 3 x [c0][c1][n2]
+    double* mpart = nullptr;  // chunk partials of the fused passes
+    int64_t mpart_n = 0;
 };
 
 struct poms_ksolve {
@@ -1515,7 +1525,8 @@ int poms_transfer_create(poms_ctx* ctx, int ndim, const poms_layout* fine, int64
 int poms_transfer_destroy(poms_transfer* t) {
     if (!t) return 0;
     for (double* p : {t->Pm[0], t->Pm[1], t->Pm[2], t->t0, t->t1, t->Pb[0], t->Pb[1], t->Pb[2], t->Rb[0],
-                      t->Rb[1], t->Rb[2], t->part})
+                      t->Rb[1], t->Rb[2], t->part, t->Gf[0], t->Gf[1], t->Gf[2], t->Gf[3], t->Gf[4], t->Gf[5],
+                      t->Pf[0], t->Pf[1], t->Pf[2], t->ru, t->rv, t->mpart})
         if (p) (void)hipFree(p);
     for (int* p : {t->jlo[0], t->jlo[1], t->jlo[2], t->ilo[0], t->ilo[1], t->ilo[2]})
         if (p) (void)hipFree(p);
@@ -1616,6 +1627,186 @@ int poms_prolong_add(poms_transfer* t, const double* coarse, double* fine, void*
     } else {
         a1.out_base = fbase; a1.out_sb2 = 1; a1.out_si = g.s1; a1.accumulate = 1;
         if (tpass(t, false, 1, a1, t->t1, fine, st)) return 1;
+    }
+    POMS_HIP_CHECK(hipGetLastError());
+    return 0;
+}
+
+// ---- fused residual -> restriction ------------------------------------------------
+// G[r] are HOST dense row-major (rows of axis d x nc_d) matrices F_r^T P_d, one per
+// operator role in poms_op_create's factor order (A0 M0 A1 B1 M2 K2 for FORM_SUM,
+// F0 - F1 - F2 - for FORM_SINGLE; 2D: roles 0, 1 unused).  Rows as P's: axis 0 global
+// (3D), axes 1 and 2 the transfer's own.
+int poms_transfer_set_operator(poms_transfer* t, int form, const double* const* G) {
+    if (!t || !G || (form != FORM_SUM && form != FORM_SINGLE)) {
+        set_error("poms_transfer_set_operator: bad argument");
+        return 1;
+    }
+    if (t->banded) { set_error("poms_transfer_set_operator: coarse extents > 32 (banded transfer)"); return 1; }
+    const bool is3d = t->ndim == 3;
+    const bool sum = form == FORM_SUM;
+    int64_t ncmax = 1;
+    for (int d = 0; d < 3; ++d) ncmax = std::max(ncmax, t->nc[d]);
+    const int ncf = ncmax <= 8 ? 8 : ncmax <= 12 ? 12 : ncmax <= 16 ? 16 : 32;
+    for (int r = 0; r < 6; ++r) {
+        const bool need = (r / 2 > 0 || is3d) && (sum || r % 2 == 0);
+        if (need && !G[r]) { set_error("poms_transfer_set_operator: missing factor"); return 1; }
+    }
+    POMS_HIP_CHECK(hipSetDevice(t->ctx->device));
+    for (double*& p : t->Gf) { if (p) (void)hipFree(p); p = nullptr; }
+    for (double*& p : t->Pf) { if (p) (void)hipFree(p); p = nullptr; }
+    if (t->ru) (void)hipFree(t->ru);
+    if (t->rv) (void)hipFree(t->rv);
+    t->ru = t->rv = nullptr;
+    t->rform = -1;
+    int rc = 0;
+    auto pad = [&](const double* src, int d, double sign, double** dev) {
+        std::vector<double> m(t->nf[d] * ncf, 0.0);
+        for (int64_t i = 0; i < t->nf[d]; ++i)
+            for (int64_t j = 0; j < t->nc[d]; ++j) m[i * ncf + j] = sign * src[i * t->nc[d] + j];
+        return upload(m.data(), m.size(), dev);
+    };
+    for (int r = 0; r < 6 && !rc; ++r) {
+        const int d = r / 2;
+        if ((d == 0 && !is3d) || !G[r] || (!sum && r % 2)) continue;
+        rc |= pad(G[r], d, d == 2 ? -1.0 : 1.0, &t->Gf[r]);
+    }
+    // P padded to ncf: the transfer keeps only its own (16 / 32-column) copy on the device
+    for (int d = is3d ? 0 : 1; d < 3 && !rc; ++d) {
+        std::vector<double> pm(t->nf[d] * t->ncm);
+        if (hipMemcpy(pm.data(), t->Pm[d], pm.size() * sizeof(double), hipMemcpyDeviceToHost) != hipSuccess) {
+            rc = 1;
+            break;
+        }
+        std::vector<double> pc(t->nf[d] * t->nc[d]);
+        for (int64_t i = 0; i < t->nf[d]; ++i)
+            for (int64_t j = 0; j < t->nc[d]; ++j) pc[i * t->nc[d] + j] = pm[i * t->ncm + j];
+        rc |= pad(pc.data(), d, 1.0, &t->Pf[d]);
+    }
+    const int64_t n1 = t->L.n[1], n2 = t->L.n[2];
+    const size_t su = (size_t)t->nc[0] * n1 * n2, sv = (size_t)t->nc[0] * t->nc[1] * n2;
+    if (!rc && hipMalloc(reinterpret_cast<void**>(&t->ru), 3 * std::max<size_t>(su, 1) * sizeof(double)) != hipSuccess) rc = 1;
+    if (!rc && hipMalloc(reinterpret_cast<void**>(&t->rv), 3 * std::max<size_t>(sv, 1) * sizeof(double)) != hipSuccess) rc = 1;
+    if (rc) {
+        if (g_err.empty()) set_error("poms_transfer_set_operator: allocation failed");
+        return 1;
+    }
+    t->ncf = ncf;
+    t->rform = form;
+    return 0;
+}
+
+static int mpass(poms_transfer* t, const MultiPass& mp, hipStream_t st) {
+    const int64_t need = mrestrict_scratch(mp, t->ncf);
+    if (need > t->mpart_n) {
+        if (t->mpart) (void)hipFree(t->mpart);
+        t->mpart = nullptr;
+        t->mpart_n = 0;
+        if (hipMalloc(reinterpret_cast<void**>(&t->mpart), need * sizeof(double)) != hipSuccess) {
+            set_error("resid_restrict: partial-sum buffer allocation failed");
+            return 1;
+        }
+        t->mpart_n = need;
+    }
+    return mrestrict_launch(t->ncf, mp, t->mpart, st);
+}
+
+// coarse = R (b - A x), local slab contribution (the caller all-reduces).  Three
+// passes (2D: two); the FORM_SUM factorisation shares its axis-0 and axis-1 outputs:
+//   u_a = G_A0 x, u_m = G_M0 x, u_c = P0 b                          (axis 0)
+//   v_1 = G_A1 u_a + G_B1 u_m, v_2 = G_A1 u_m, v_3 = P1 u_c           (axis 1)
+//   coarse = P2 v_3 - G_M2 v_1 - G_K2 v_2                            (axis 2)
+// since A = A0 (x) A1 (x) M2 + M0 (x) B1 (x) M2 + M0 (x) A1 (x) K2 (2D: A1 (x) M2 +
+// B1 (x) K2; FORM_SINGLE: F0 (x) F1 (x) F2).  x needs no ghost planes: each fine
+// row enters through its own row of G.
+int poms_resid_restrict(poms_transfer* t, const double* b, const double* x, double* coarse, void* stream) {
+    if (!t || !b || !x || !coarse) { set_error("poms_resid_restrict: null argument"); return 1; }
+    if (t->rform < 0) { set_error("poms_resid_restrict: no operator set (poms_transfer_set_operator)"); return 1; }
+    const RowGeom g = row_geom(&t->L);
+    const int64_t n0 = g.n0, n1 = g.n1, n2 = g.n2;
+    const int64_t c0 = t->nc[0], c1 = t->nc[1], c2 = t->nc[2];
+    hipStream_t st = as_stream(stream);
+    const int64_t fbase = (int64_t)g.pd0 * g.s0 + (int64_t)g.pd1 * g.s1 + g.pd2;
+    const bool sum = t->rform == FORM_SUM;
+    const size_t su = (size_t)c0 * n1 * n2, sv = (size_t)c0 * c1 * n2;
+    double* u[3] = {t->ru, t->ru + su, t->ru + 2 * su};
+    double* v[3] = {t->rv, t->rv + sv, t->rv + 2 * sv};
+    double* const* G = t->Gf;
+    auto clear = [](MultiPass& mp) {
+        mp = MultiPass{};
+    };
+    // the axis-2 pass (the last) reads w[0..2] with w[0] = the P-chain of b
+    auto last = [&](const double* wb, const double* w1, const double* w2, const AxisPass& a2) {
+        MultiPass mp;
+        clear(mp);
+        mp.ps = a2;
+        mp.ni = sum ? 3 : 2;
+        mp.no = 1;
+        mp.in[0] = wb; mp.in[1] = w1; mp.in[2] = sum ? w2 : nullptr;
+        mp.out[0] = coarse;
+        mp.m[0][0] = t->Pf[2];
+        mp.m[0][1] = G[4];
+        mp.m[0][2] = sum ? G[5] : nullptr;
+        return mpass(t, mp, st);
+    };
+    AxisPass a2{};
+    a2.nA = c0 * c1; a2.nB1 = 1; a2.nB2 = 1;
+    a2.in_sa = n2; a2.in_si = 1;
+    a2.out_sa = c2; a2.out_si = 1;
+    a2.nI = (int)n2; a2.nJ = (int)c2; a2.goff = 0;
+    if (t->ndim == 3) {
+        MultiPass mp;
+        clear(mp);
+        AxisPass& a0 = mp.ps;
+        a0.nA = 1; a0.nB1 = n1; a0.nB2 = n2;
+        a0.in_base = fbase; a0.in_sb1 = g.s1; a0.in_sb2 = 1; a0.in_si = g.s0;
+        a0.out_sb1 = n2; a0.out_sb2 = 1; a0.out_si = n1 * n2;
+        a0.nI = (int)n0; a0.nJ = (int)c0; a0.goff = (int)t->g0;
+        mp.ni = 2;
+        mp.in[0] = x; mp.in[1] = b;
+        // outputs: u_c (b), u_a, [u_m]
+        mp.no = sum ? 3 : 2;
+        mp.out[0] = u[0]; mp.out[1] = u[1]; mp.out[2] = u[2];
+        mp.m[0][1] = t->Pf[0];
+        mp.m[1][0] = G[0];
+        if (sum) mp.m[2][0] = G[1];
+        if (mpass(t, mp, st)) return 1;
+        MultiPass m1;
+        clear(m1);
+        AxisPass& a1 = m1.ps;
+        a1.nA = c0; a1.nB1 = 1; a1.nB2 = n2;
+        a1.in_base = 0; a1.in_sa = n1 * n2; a1.in_sb2 = 1; a1.in_si = n2;
+        a1.out_sa = c1 * n2; a1.out_sb2 = 1; a1.out_si = n2;
+        a1.nI = (int)n1; a1.nJ = (int)c1; a1.goff = 0;
+        m1.ni = sum ? 3 : 2;
+        m1.in[0] = u[0]; m1.in[1] = u[1]; m1.in[2] = u[2];
+        m1.no = sum ? 3 : 2;
+        m1.out[0] = v[0]; m1.out[1] = v[1]; m1.out[2] = v[2];
+        m1.m[0][0] = t->Pf[1];              // v_3 (here v[0]) = P1 u_c
+        m1.m[1][1] = G[2];                  // v_1 = G_A1 u_a + G_B1 u_m
+        if (sum) {
+            m1.m[1][2] = G[3];
+            m1.m[2][2] = G[2];              // v_2 = G_A1 u_m
+        }
+        if (mpass(t, m1, st)) return 1;
+        if (last(v[0], v[1], v[2], a2)) return 1;
+    } else {
+        MultiPass mp;
+        clear(mp);
+        AxisPass& a1 = mp.ps;
+        a1.nA = 1; a1.nB1 = 1; a1.nB2 = n2;
+        a1.in_base = fbase; a1.in_sb2 = 1; a1.in_si = g.s1;
+        a1.out_sa = c1 * n2; a1.out_sb2 = 1; a1.out_si = n2;
+        a1.nI = (int)n1; a1.nJ = (int)c1; a1.goff = 0;
+        mp.ni = 2;
+        mp.in[0] = x; mp.in[1] = b;
+        mp.no = sum ? 3 : 2;
+        mp.out[0] = v[0]; mp.out[1] = v[1]; mp.out[2] = v[2];
+        mp.m[0][1] = t->Pf[1];              // P1 b
+        mp.m[1][0] = G[2];                  // G_A1 x (-> M2)
+        if (sum) mp.m[2][0] = G[3];         // G_B1 x (-> K2)
+        if (mpass(t, mp, st)) return 1;
+        if (last(v[0], v[1], v[2], a2)) return 1;
     }
     POMS_HIP_CHECK(hipGetLastError());
     return 0;

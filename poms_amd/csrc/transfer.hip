@@ -10,7 +10,7 @@
 // columns with zeros).  The dominant pass (axis 0 of the fine slab) streams the
 // fine vector once: 8 B/DOF for restriction, 16 B/DOF for prolong-add.
 // Coarse extents > 32 (multilevel hierarchies) use the banded gather kernels.
-#include "common.hpp"
+#include "transfer.hpp"
 
 #include <algorithm>
 
@@ -38,11 +38,20 @@ restrict_pass_kernel(const AxisPass ps, const double* __restrict__ Pm,
     double acc[NCM];
 #pragma unroll
     for (int j = 0; j < NCM; ++j) acc[j] = 0.0;
-    for (int i = i_begin; i < i_end; ++i) {
-        const double v = src[(int64_t)i * ps.in_si];
-        const double* prow = Pm + (int64_t)(ps.goff + i) * NCM;
+    // the loads of BT rows are issued before any is used (one load in flight per
+    // wave left the 515^3 axis-0 pass latency-bound, round 6)
+    constexpr int BT = 8;
+    for (int i0 = i_begin; i0 < i_end; i0 += BT) {
+        double v[BT];
 #pragma unroll
-        for (int j = 0; j < NCM; ++j) acc[j] = fma(prow[j], v, acc[j]);
+        for (int u = 0; u < BT; ++u) v[u] = (i0 + u < i_end) ? src[(int64_t)(i0 + u) * ps.in_si] : 0.0;
+#pragma unroll
+        for (int u = 0; u < BT; ++u) {
+            if (i0 + u >= i_end) break;
+            const double* prow = Pm + (int64_t)(ps.goff + i0 + u) * NCM;
+#pragma unroll
+            for (int j = 0; j < NCM; ++j) acc[j] = fma(prow[j], v[u], acc[j]);
+        }
     }
     if (ks > 1) {   // partials [chunk][j][line]: coalesced over lines
 #pragma unroll
@@ -64,7 +73,15 @@ restrict_sum_kernel(const AxisPass ps, int ncm, int ks, const double* __restrict
     const int j = (int)(tid / nline);
     const int64_t line = tid - (int64_t)j * nline;
     double s = 0.0;
-    for (int k = 0; k < ks; ++k) s += part[((int64_t)k * ncm + j) * nline + line];
+    int k = 0;
+    for (; k + 8 <= ks; k += 8) {   // 8 loads in flight, added in chunk order
+        double w[8];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) w[u] = part[((int64_t)(k + u) * ncm + j) * nline + line];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) s += w[u];
+    }
+    for (; k < ks; ++k) s += part[((int64_t)k * ncm + j) * nline + line];
     const int64_t b2 = line % ps.nB2;
     const int64_t t1 = line / ps.nB2;
     const int64_t b1 = t1 % ps.nB1;
@@ -91,14 +108,23 @@ prolong_pass_kernel(const AxisPass ps, const double* __restrict__ Pm,
     // outputs are independent: few lines split the expanded axis over blockIdx.y
     const int ks = gridDim.y, kc = (ps.nI + ks - 1) / ks;
     const int i_end = min(ps.nI, (int)blockIdx.y * kc + kc);
-    for (int i = blockIdx.y * kc; i < i_end; ++i) {
-        const double* prow = Pm + (int64_t)(ps.goff + i) * NCM;
-        double s = 0.0;
+    // BT rows per step: the accumulated rows' loads are issued together, before the
+    // stores (one read-modify-write in flight per wave was latency-bound)
+    constexpr int BT = 8;
+    for (int i0 = blockIdx.y * kc; i0 < i_end; i0 += BT) {
+        double old[BT];
 #pragma unroll
-        for (int j = 0; j < NCM; ++j) s = fma(prow[j], cv[j], s);
-        double* o = dst + (int64_t)i * ps.out_si;
-        if (ps.accumulate) *o += s;
-        else *o = s;
+        for (int u = 0; u < BT; ++u)
+            old[u] = (ps.accumulate && i0 + u < i_end) ? dst[(int64_t)(i0 + u) * ps.out_si] : 0.0;
+#pragma unroll
+        for (int u = 0; u < BT; ++u) {
+            if (i0 + u >= i_end) break;
+            const double* prow = Pm + (int64_t)(ps.goff + i0 + u) * NCM;
+            double s = 0.0;
+#pragma unroll
+            for (int j = 0; j < NCM; ++j) s = fma(prow[j], cv[j], s);
+            dst[(int64_t)(i0 + u) * ps.out_si] = ps.accumulate ? old[u] + s : s;
+        }
     }
 }
 
@@ -152,6 +178,149 @@ prolong_band_kernel(const AxisPass ps, const double* __restrict__ Pb, const int*
     double* o = out + ps.out_base + a * ps.out_sa + b1 * ps.out_sb1 + b2 * ps.out_sb2 + (int64_t)i * ps.out_si;
     if (ps.accumulate) *o += s;
     else *o = s;
+}
+
+// ---- fused residual -> restriction (sources/mg_jac.py:93-94) ----------------------
+// rc = R (b - A x) = R b - (R A) x with A = sum_t (x)_d F_{t,d}: every factor of R A
+// is a (nf x nc) matrix G = F^T P (host, poms_transfer_set_operator), so R A x is
+// sum-factorised like R itself and neither r = b - A x nor A x is ever stored.  One
+// pass over axis d reads up to 3 inputs and forms up to 3 outputs
+//     out[o][.. J ..] = sum_i sum_k M[o][k][goff + i][J] in[k][.. i ..]
+// (rows padded to NCM columns with zeros; a null M[o][k] is no term).  The first pass
+// streams x and b once: 16 B per fine DOF, against 24 (residual) + 8 (restriction).
+// Every thread marches one line; the inputs of BT consecutive rows are loaded before
+// any of them is used, so BT x NI loads per wave are in flight instead of one.
+template <int NCM, int NO>
+__global__ void __launch_bounds__(256)
+mrestrict_kernel(const MultiPass mp, double* __restrict__ part) {
+    constexpr int BT = 4;
+    const AxisPass& ps = mp.ps;
+    const int64_t tid = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    const int64_t nline = ps.nA * ps.nB1 * ps.nB2;
+    if (tid >= nline) return;
+    const int ks = gridDim.y, kc = (ps.nI + ks - 1) / ks;
+    const int i_begin = blockIdx.y * kc, i_end = min(ps.nI, i_begin + kc);
+    const int64_t b2 = tid % ps.nB2;
+    const int64_t t1 = tid / ps.nB2;
+    const int64_t b1 = t1 % ps.nB1;
+    const int64_t a = t1 / ps.nB1;
+    const int64_t ioff = ps.in_base + a * ps.in_sa + b1 * ps.in_sb1 + b2 * ps.in_sb2;
+    double acc[NO][NCM];
+#pragma unroll
+    for (int o = 0; o < NO; ++o)
+#pragma unroll
+        for (int j = 0; j < NCM; ++j) acc[o][j] = 0.0;
+    for (int i0 = i_begin; i0 < i_end; i0 += BT) {
+        double v[BT][3];
+#pragma unroll
+        for (int u = 0; u < BT; ++u)
+#pragma unroll
+            for (int k = 0; k < 3; ++k)
+                v[u][k] = (k < mp.ni && i0 + u < i_end) ? mp.in[k][ioff + (int64_t)(i0 + u) * ps.in_si] : 0.0;
+#pragma unroll
+        for (int u = 0; u < BT; ++u) {
+            if (i0 + u >= i_end) break;
+            const int64_t row = (int64_t)(ps.goff + i0 + u) * NCM;
+#pragma unroll
+            for (int o = 0; o < NO; ++o)
+#pragma unroll
+                for (int k = 0; k < 3; ++k) {
+                    const double* m = mp.m[o][k];
+                    if (m == nullptr) continue;
+#pragma unroll
+                    for (int j = 0; j < NCM; ++j) acc[o][j] = fma(m[row + j], v[u][k], acc[o][j]);
+                }
+        }
+    }
+    if (ks > 1) {   // partials [chunk][o][j][line]: coalesced over lines
+#pragma unroll
+        for (int o = 0; o < NO; ++o)
+#pragma unroll
+            for (int j = 0; j < NCM; ++j)
+                if (j < ps.nJ) part[(((int64_t)blockIdx.y * NO + o) * NCM + j) * nline + tid] = acc[o][j];
+        return;
+    }
+    const int64_t doff = ps.out_base + a * ps.out_sa + b1 * ps.out_sb1 + b2 * ps.out_sb2;
+#pragma unroll
+    for (int o = 0; o < NO; ++o)
+#pragma unroll
+        for (int j = 0; j < NCM; ++j)
+            if (j < ps.nJ) mp.out[o][doff + (int64_t)j * ps.out_si] = acc[o][j];
+}
+
+// Sum of the ks chunk partials of every output, in chunk order (deterministic); the
+// loads of 8 chunks are issued before they are added.
+__global__ void __launch_bounds__(256)
+mrestrict_sum_kernel(const MultiPass mp, int ncm, int no, int ks, const double* __restrict__ part) {
+    const AxisPass& ps = mp.ps;
+    const int64_t nline = ps.nA * ps.nB1 * ps.nB2;
+    const int64_t tid = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    if (tid >= nline * ps.nJ * no) return;
+    const int64_t line = tid % nline;
+    const int oj = (int)(tid / nline);
+    const int j = oj % ps.nJ, o = oj / ps.nJ;
+    const double* pp = part + ((int64_t)o * ncm + j) * nline + line;
+    const int64_t cs = (int64_t)no * ncm * nline;   // one chunk's partials
+    double s = 0.0;
+    int k = 0;
+    for (; k + 8 <= ks; k += 8) {
+        double w[8];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) w[u] = pp[(int64_t)(k + u) * cs];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) s += w[u];
+    }
+    for (; k < ks; ++k) s += pp[(int64_t)k * cs];
+    const int64_t b2 = line % ps.nB2;
+    const int64_t t1 = line / ps.nB2;
+    const int64_t b1 = t1 % ps.nB1;
+    const int64_t a = t1 / ps.nB1;
+    mp.out[o][ps.out_base + a * ps.out_sa + b1 * ps.out_sb1 + b2 * ps.out_sb2 + (int64_t)j * ps.out_si] = s;
+}
+
+// chunks of a multi-output pass: at least 32768 threads where the lines are few, the
+// chunk partials (no x ncm per line and chunk) kept below the pass's input reads
+static int mrestrict_split(int64_t nline, int nI, int ni, int no, int ncm) {
+    if (nline >= 32768 || nI < 64) return 1;
+    const int64_t want = (32768 + nline - 1) / nline;
+    const int64_t cap = std::max<int64_t>(1, (int64_t)nI * ni / ((int64_t)no * ncm));
+    return (int)std::max<int64_t>(1, std::min<int64_t>({want, cap, (int64_t)nI / 16, 256}));
+}
+
+int64_t mrestrict_scratch(const MultiPass& mp, int ncm) {   // doubles of partials a pass needs
+    const int64_t nline = mp.ps.nA * mp.ps.nB1 * mp.ps.nB2;
+    const int ks = mrestrict_split(nline, mp.ps.nI, mp.ni, mp.no, ncm);
+    return ks > 1 ? ks * (int64_t)mp.no * ncm * nline : 0;
+}
+
+template <int NCM>
+static void mrestrict_go(const MultiPass& mp, dim3 grid, double* part, hipStream_t st) {
+    if (mp.no == 1) hipLaunchKernelGGL((mrestrict_kernel<NCM, 1>), grid, dim3(256), 0, st, mp, part);
+    else if (mp.no == 2) hipLaunchKernelGGL((mrestrict_kernel<NCM, 2>), grid, dim3(256), 0, st, mp, part);
+    else hipLaunchKernelGGL((mrestrict_kernel<NCM, 3>), grid, dim3(256), 0, st, mp, part);
+}
+
+int mrestrict_launch(int ncm, const MultiPass& mp, double* part, hipStream_t st) {
+    const int64_t nline = mp.ps.nA * mp.ps.nB1 * mp.ps.nB2;
+    const int nb = (int)((nline + 255) / 256);
+    if (nb == 0) return 0;
+    if (mp.no < 1 || mp.no > 3 || mp.ni < 1 || mp.ni > 3) { set_error("resid_restrict: 1..3 inputs / outputs"); return 1; }
+    const int ks = part ? mrestrict_split(nline, mp.ps.nI, mp.ni, mp.no, ncm) : 1;
+    const dim3 grid(nb, ks);
+    double* pk = ks > 1 ? part : nullptr;
+    switch (ncm) {
+        case 8: mrestrict_go<8>(mp, grid, pk, st); break;
+        case 12: mrestrict_go<12>(mp, grid, pk, st); break;
+        case 16: mrestrict_go<16>(mp, grid, pk, st); break;
+        case 32: mrestrict_go<32>(mp, grid, pk, st); break;
+        default: set_error("resid_restrict: coarse extent must be <= 32"); return 1;
+    }
+    if (ks > 1) {
+        const int64_t nsum = nline * mp.ps.nJ * mp.no;
+        hipLaunchKernelGGL(mrestrict_sum_kernel, dim3((unsigned)((nsum + 255) / 256)), dim3(256), 0, st, mp, ncm,
+                           mp.no, ks, part);
+    }
+    return 0;
 }
 
 int transfer_band_launch(bool restrict_dir, const AxisPass& ps, const double* band, const int* lo, int w,

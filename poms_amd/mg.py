@@ -11,7 +11,7 @@ the device.
 
 Cycle (`sources/mg_jac.py:84-119`):
     xf, info_pre = pcg(Af, damped_jacobi, bf, tol, maxiter)     # pre-smoothing
-    rf = bf - Af xf ; rc = R rf (+ all-reduce over slabs)         # restriction
+    rc = R (bf - Af xf) (+ all-reduce over slabs)                 # residual -> restriction, fused
     xc = Ac^{-1} rc                                               # coarse solve
     xf = xf + P xc ; ghost exchange                               # correction
     xf2, info_pos = pcg(Af, damped_jacobi, bf, x0=xf, tol, maxiter)  # post-smoothing
@@ -74,7 +74,7 @@ class TwoLevelVCycle:
     def __init__(self, p: int, ncells_fine: int, ncells_coarse: int = 8, ndim: int = 3, *,
                  dist=None, mass_coef: float = 1.0, device=None, knots_fine=None, knots_coarse=None,
                  tol: float = 1e-6, maxiter: int = 10, chunk: int = 0, align: bool = True,
-                 post_smoother: str = "jacobi"):
+                 post_smoother: str = "jacobi", fused_restrict: bool = True):
         self.p, self.ndim = int(p), int(ndim)
         if post_smoother not in ("jacobi", "glt"):
             raise ValueError("post_smoother must be 'jacobi' (mg_jac.py) or 'glt' (mg_glt.py)")
@@ -94,6 +94,9 @@ class TwoLevelVCycle:
         if chunk:
             self.A.set_chunk(chunk)
         self.transfer = KronTransfer(self.space, [P1] * ndim)
+        # residual -> restriction in one pass over x and b (KronTransfer.resid_restrict);
+        # False: the residual vector and the restriction, as the reference computes them
+        self.fused_restrict = bool(fused_restrict) and self.transfer.set_operator(self.A)
         from .splines import band_to_dense
         Md, Kd = band_to_dense(M), band_to_dense(K)
         Mc, Kc = P1.T @ Md @ P1, P1.T @ Kd @ P1
@@ -134,8 +137,11 @@ class TwoLevelVCycle:
         """One V-cycle; returns ``(xf2, info_pre, info_pos)``."""
         A = self.A
         xf, info_pre = pcg(A, damped_jacobi, bf, x0=x0, tol=self.tol, maxiter=self.maxiter)
-        rf = A.residual(bf, xf)
-        rc = self.transfer.restrict(rf, out=self.rc)
+        if self.fused_restrict:
+            rc = self.transfer.resid_restrict(A, bf, xf, out=self.rc)
+        else:
+            rf = A.residual(bf, xf)
+            rc = self.transfer.restrict(rf, out=self.rc)
         xc = self.coarse_solve(rc, self.xc)
         self.transfer.prolong_add(xc, xf)
         xf.update_ghost_regions()
@@ -168,7 +174,7 @@ class MultilevelVCycle:
 
     def __init__(self, p: int, ncells_fine: int, ncells_coarsest: int = 8, ndim: int = 3, *,
                  dist=None, mass_coef: float = 1.0, device=None, tol: float = 1e-6, maxiters=None,
-                 align: bool = True, chunk: int = 0):
+                 align: bool = True, chunk: int = 0, fused_restrict: bool = True):
         if ncells_fine < ncells_coarsest or ncells_coarsest < 1:
             raise ValueError("need ncells_fine >= ncells_coarsest >= 1")
         self.p, self.ndim, self.tol = int(p), int(ndim), tol
@@ -204,6 +210,8 @@ class MultilevelVCycle:
             self.spaces.append(V)
             self.ops.append(A)
             self.transfers.append(KronTransfer(V, [self.P1[l]] * ndim))
+        # fused residual -> restriction where the transfer is dense (coarse extents <= 32)
+        self.fused = [bool(fused_restrict) and tr.set_operator(A) for tr, A in zip(self.transfers, self.ops)]
         # coarsest level: dense inverse of its operator (assembled = Galerkin, nested)
         from .splines import band_to_dense
         Mc, Kc = band_to_dense(self.M1d[-1]), band_to_dense(self.K1d[-1])
@@ -239,8 +247,10 @@ class MultilevelVCycle:
     def _level(self, l: int, b: StencilVector, x0: StencilVector | None) -> StencilVector:
         A, tr = self.ops[l], self.transfers[l]
         x, ipre = pcg(A, damped_jacobi, b, x0=x0, tol=self.tol, maxiter=self.maxiters[l])
-        r = A.residual(b, x)
-        rc = tr.restrict(r, out=self.rcs[l])
+        if self.fused[l]:
+            rc = tr.resid_restrict(A, b, x, out=self.rcs[l])
+        else:
+            rc = tr.restrict(A.residual(b, x), out=self.rcs[l])
         if l + 1 == self.nlevels - 1:
             ec = self.xc
             _lib.call("poms_dense_matvec", self.spaces[0].ctx, rc.numel(), rt.ptr(self.Ainv), rt.ptr(rc),

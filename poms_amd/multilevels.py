@@ -96,6 +96,64 @@ class KronTransfer:
                 rt.Comm.from_env(d.group).allreduce_sum_(out)
         return out
 
+    def set_operator(self, A) -> bool:
+        """Prepare the fused ``R (b - A x)`` for the Kronecker operator ``A`` (a
+        :class:`~poms_amd.stencil.KronOperator` on this transfer's space): the host forms
+        ``G = F^T P_d`` for every 1D factor ``F`` of ``A`` (rows sliced like ``P_d``).
+        Returns False where the fused path does not apply (banded transfers, coarse
+        extents > 32; general stencils), and the caller keeps residual + restrict."""
+        from .splines import band_to_dense
+        V = self.space
+        if A.space is not V or A.form not in ("sum", "single") or max(self.nc) > 32:
+            return False
+        nd = V.ndim
+        lead = 3 - nd
+        P = A.pmax
+
+        def dense(band):   # 1-row bands are the scalar factors of the 1D operator
+            return band[:, P:P + 1].copy() if band.shape[0] == 1 else band_to_dense(band)
+
+        # role -> storage axis (poms_op_create's factor order)
+        roles = ["A0", "M0", "A1", "B1", "M2", "K2"] if A.form == "sum" else ["F0", None, "F1", None, "F2", None]
+        Pl = [np.ones((1, 1))] * lead + list(self.P)
+        G = []
+        for r, name in enumerate(roles):
+            ax = r // 2
+            if name is None or (ax == 0 and nd < 3):
+                G.append(None)
+                continue
+            g = dense(A.bands[name]).T @ Pl[ax]
+            if V.is_cart and ax >= 1 and g.shape[0] > 1:   # (KronTransfer's own slicing of P)
+                d = ax - lead
+                g = g[V.starts[d]:V.ends[d] + 1]
+            G.append(np.ascontiguousarray(g, dtype=np.float64))
+        self._G = G
+        garr = (C.c_void_p * 6)(*[None if g is None else g.ctypes.data_as(C.c_void_p) for g in G])
+        try:
+            _lib.call("poms_transfer_set_operator", self._h, _lib.FORM_SUM if A.form == "sum" else _lib.FORM_SINGLE,
+                      garr)
+        except _lib.PomsError:
+            return False
+        self._op = A
+        return True
+
+    def resid_restrict(self, A, b: StencilVector, x: StencilVector, out: torch.Tensor | None = None,
+                       allreduce: bool = True) -> torch.Tensor:
+        """``rc = R (b - A x)`` (+ sum over slabs) without storing the residual
+        (`sources/mg_jac.py:93-95`; fused: one pass over x and b instead of the residual's
+        24 B/DOF plus the restriction's 8)."""
+        if getattr(self, "_op", None) is not A and not self.set_operator(A):
+            raise ValueError("fused residual -> restriction does not apply to this operator / transfer")
+        out = self.coarse_empty() if out is None else out
+        _lib.call("poms_resid_restrict", self._h, rt.ptr(b._data), rt.ptr(x._data), rt.ptr(out), rt.stream_handle())
+        if allreduce and self.space.is_distributed:
+            d = self.space.dist
+            if d.native is not None:
+                d.native.allreduce(out, rt.stream_handle(), wait_back=True)
+            else:
+                rt.Comm.from_env(d.group).allreduce_sum_(out)
+        return out
+
     def prolong_add(self, coarse: torch.Tensor, fine: StencilVector) -> StencilVector:
         """``fine += P xc`` on the owned slab (`sources/mg_jac.py:102-112`)."""
         _lib.call("poms_prolong_add", self._h, rt.ptr(coarse), rt.ptr(fine._data), rt.stream_handle())

@@ -184,12 +184,18 @@ def run_gpu():
     tr.prolong_add(torch.from_numpy(xc).cuda(), z)
     pz = np.einsum("ia,jb,kc,abc->ijk", P1, P1, P1, xc.reshape((P1.shape[1],) * 3))
     check(rel(z.to_local_numpy(), pz[sl]) <= 1e-14, "distributed prolongation")
+    # fused residual -> restriction over the slabs (no ghost planes needed) + allreduce
+    x._ghost_valid = False
+    rcf = tr.resid_restrict(A, b, x).cpu().numpy()
+    fullr = np.einsum("ia,jb,kc,ijk->abc", P1, P1, P1, bg - Ag).reshape(-1)
+    check(rel(rcf, fullr) <= 1e-13, f"distributed fused residual -> restriction {rel(rcf, fullr)}")
     # two-level V-cycle over the slabs vs the global oracle (p=2: stable smoother)
     devred = os.environ.get("POMS_TEST_DEVRED") == "1"
     mg = TwoLevelVCycle(2, 16, 4, ndim=3, dist=SlabDistribution.from_process_group(18, device_reductions=devred,
                                                                                    host_transport=host_tr,
                                                                                    host_shm=host_shm))
     assert mg.space.lazy_reductions == devred or not devred
+    check(mg.fused_restrict, "the V-cycle takes the fused residual -> restriction")
     bf = mg.rhs_ones()
     xf2, ipre, ipos = mg.cycle(bf)
     got = torch.from_numpy(xf2.toarray())
@@ -489,6 +495,11 @@ def _cart_ops(d, nd, p, N, align):
     else:
         pz = P1 @ xc.reshape(nc, nc) @ P1.T
     check(rel(z.to_local_numpy(), pz[sl]) <= 1e-14, f"{tag}: Cart prolongation")
+    # fused residual -> restriction on the block (G rows sliced like P's) + allreduce
+    rcf = tr.resid_restrict(A, b, x).cpu().numpy()
+    rg = bg - Ag
+    fullr = (np.einsum("ia,jb,kc,ijk->abc", P1, P1, P1, rg) if nd == 3 else P1.T @ rg @ P1).reshape(-1)
+    check(rel(rcf, fullr) <= 1e-13, f"{tag}: Cart fused residual -> restriction {rel(rcf, fullr)}")
 
 
 def run_cart_gpu():

@@ -13,7 +13,8 @@ def test_header_declares_the_boundary():
     syms = _lib.header_symbols()
     assert len(syms) >= 25
     for must in ("poms_op_create", "poms_op_apply", "poms_op_residual", "poms_op_jacobi_sweep",
-                 "poms_kron_dot_2d", "poms_restrict", "poms_prolong_add", "poms_pcg_update"):
+                 "poms_kron_dot_2d", "poms_restrict", "poms_prolong_add", "poms_resid_restrict",
+                 "poms_transfer_set_operator", "poms_pcg_update"):
         assert must in syms
 
 

@@ -11,6 +11,7 @@
 #   prof             rocprofv3 --kernel-trace --stats of a 2-cycle 3D bench
 #   prof2d           the same for the 2D bench
 #   kb:<args>        tools/kernel_bench.py with args (commas for spaces)
+#   py:<script,args> any python script with args (commas for spaces)
 #   proxy            loopback proxy of rank 1 of 8 (tools/slab_proxy.py)
 #   pmc:<tag>:<kernel>:<kb args>   HBM traffic passes (tools/pmc_traffic.sh)
 # Output under gpurun_out/<tag>/.
@@ -39,6 +40,7 @@ for step in "$@"; do
         bench2d) run bench_2d 300 python bench.py --ndim 2 --no-cpu-baseline ;;
         bench:*) a=${step#bench:}; run bench_$i 600 python bench.py ${a//,/ } ;;
         kb:*) a=${step#kb:}; run kb_$i 600 python tools/kernel_bench.py ${a//,/ } ;;
+        py:*) a=${step#py:}; run py_$i 600 python ${a//,/ } ;;
         proxy) run proxy_loop_r1 300 python tools/slab_proxy.py --loopback-rank 1 --world 8 --steps 5 ;;
         prof) (cd /tmp && timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d $R/$O/prof -o run -- \
                   python3 $R/bench.py --steps 2 --warmup 1 --no-cpu-baseline) > $O/prof.log 2>&1
