@@ -13,6 +13,7 @@
 #include "transfer.hpp"
 
 #include <algorithm>
+#include <cstdlib>
 
 namespace poms {
 
@@ -25,34 +26,45 @@ template <int NCM>
 __global__ void __launch_bounds__(256)
 restrict_pass_kernel(const AxisPass ps, const double* __restrict__ Pm,
                      const double* __restrict__ in, double* __restrict__ out, double* __restrict__ part) {
+    // Rows of P are staged through LDS, RB at a time, and read back as broadcasts; the
+    // inputs of BT rows are loaded before any is used (round 6: per-row scalar loads of
+    // P, each waited for, and one input load per wave in flight left the 515^3 axis-0
+    // pass latency-bound).  The FMAs keep their order: the same bits.
+    constexpr int BT = 8, RB = 64;
+    __shared__ double sp[RB * NCM];
     const int64_t tid = (int64_t)blockIdx.x * 256 + threadIdx.x;
     const int64_t nline = ps.nA * ps.nB1 * ps.nB2;
-    if (tid >= nline) return;
+    const bool live = tid < nline;
     const int ks = gridDim.y, kc = (ps.nI + ks - 1) / ks;
     const int i_begin = blockIdx.y * kc, i_end = min(ps.nI, i_begin + kc);
-    const int64_t b2 = tid % ps.nB2;
-    const int64_t t1 = tid / ps.nB2;
+    const int64_t ln = live ? tid : 0;
+    const int64_t b2 = ln % ps.nB2;
+    const int64_t t1 = ln / ps.nB2;
     const int64_t b1 = t1 % ps.nB1;
     const int64_t a = t1 / ps.nB1;
     const double* src = in + ps.in_base + a * ps.in_sa + b1 * ps.in_sb1 + b2 * ps.in_sb2;
     double acc[NCM];
 #pragma unroll
     for (int j = 0; j < NCM; ++j) acc[j] = 0.0;
-    // the loads of BT rows are issued before any is used (one load in flight per
-    // wave left the 515^3 axis-0 pass latency-bound, round 6)
-    constexpr int BT = 8;
-    for (int i0 = i_begin; i0 < i_end; i0 += BT) {
-        double v[BT];
+    for (int c0 = i_begin; c0 < i_end; c0 += RB) {
+        const int nr = min(RB, i_end - c0);
+        __syncthreads();
+        for (int e = threadIdx.x; e < nr * NCM; e += 256) sp[e] = Pm[(int64_t)(ps.goff + c0) * NCM + e];
+        __syncthreads();
+        if (!live) continue;
+        for (int r0 = 0; r0 < nr; r0 += BT) {
+            double v[BT];
 #pragma unroll
-        for (int u = 0; u < BT; ++u) v[u] = (i0 + u < i_end) ? src[(int64_t)(i0 + u) * ps.in_si] : 0.0;
+            for (int u = 0; u < BT; ++u) v[u] = (r0 + u < nr) ? src[(int64_t)(c0 + r0 + u) * ps.in_si] : 0.0;
 #pragma unroll
-        for (int u = 0; u < BT; ++u) {
-            if (i0 + u >= i_end) break;
-            const double* prow = Pm + (int64_t)(ps.goff + i0 + u) * NCM;
+            for (int u = 0; u < BT; ++u) {
+                if (r0 + u >= nr) break;
 #pragma unroll
-            for (int j = 0; j < NCM; ++j) acc[j] = fma(prow[j], v[u], acc[j]);
+                for (int j = 0; j < NCM; ++j) acc[j] = fma(sp[(r0 + u) * NCM + j], v[u], acc[j]);
+            }
         }
     }
+    if (!live) return;
     if (ks > 1) {   // partials [chunk][j][line]: coalesced over lines
 #pragma unroll
         for (int j = 0; j < NCM; ++j)
@@ -93,37 +105,45 @@ template <int NCM>
 __global__ void __launch_bounds__(256)
 prolong_pass_kernel(const AxisPass ps, const double* __restrict__ Pm,
                     const double* __restrict__ in, double* __restrict__ out) {
+    // P rows through LDS and BT rows per step, as restrict_pass_kernel (the accumulated
+    // rows' loads are issued together, before the stores)
+    constexpr int BT = 8, RB = 64;
+    __shared__ double sp[RB * NCM];
     const int64_t tid = (int64_t)blockIdx.x * 256 + threadIdx.x;
     const int64_t nline = ps.nA * ps.nB1 * ps.nB2;
-    if (tid >= nline) return;
-    const int64_t b2 = tid % ps.nB2;
-    const int64_t t1 = tid / ps.nB2;
+    const bool live = tid < nline;
+    const int64_t ln = live ? tid : 0;
+    const int64_t b2 = ln % ps.nB2;
+    const int64_t t1 = ln / ps.nB2;
     const int64_t b1 = t1 % ps.nB1;
     const int64_t a = t1 / ps.nB1;
     const double* src = in + ps.in_base + a * ps.in_sa + b1 * ps.in_sb1 + b2 * ps.in_sb2;
     double cv[NCM];
 #pragma unroll
-    for (int j = 0; j < NCM; ++j) cv[j] = (j < ps.nJ) ? src[(int64_t)j * ps.in_si] : 0.0;
+    for (int j = 0; j < NCM; ++j) cv[j] = (live && j < ps.nJ) ? src[(int64_t)j * ps.in_si] : 0.0;
     double* dst = out + ps.out_base + a * ps.out_sa + b1 * ps.out_sb1 + b2 * ps.out_sb2;
     // outputs are independent: few lines split the expanded axis over blockIdx.y
     const int ks = gridDim.y, kc = (ps.nI + ks - 1) / ks;
-    const int i_end = min(ps.nI, (int)blockIdx.y * kc + kc);
-    // BT rows per step: the accumulated rows' loads are issued together, before the
-    // stores (one read-modify-write in flight per wave was latency-bound)
-    constexpr int BT = 8;
-    for (int i0 = blockIdx.y * kc; i0 < i_end; i0 += BT) {
-        double old[BT];
+    const int i_begin = blockIdx.y * kc, i_end = min(ps.nI, i_begin + kc);
+    for (int c0 = i_begin; c0 < i_end; c0 += RB) {
+        const int nr = min(RB, i_end - c0);
+        __syncthreads();
+        for (int e = threadIdx.x; e < nr * NCM; e += 256) sp[e] = Pm[(int64_t)(ps.goff + c0) * NCM + e];
+        __syncthreads();
+        if (!live) continue;
+        for (int r0 = 0; r0 < nr; r0 += BT) {
+            double old[BT];
 #pragma unroll
-        for (int u = 0; u < BT; ++u)
-            old[u] = (ps.accumulate && i0 + u < i_end) ? dst[(int64_t)(i0 + u) * ps.out_si] : 0.0;
+            for (int u = 0; u < BT; ++u)
+                old[u] = (ps.accumulate && r0 + u < nr) ? dst[(int64_t)(c0 + r0 + u) * ps.out_si] : 0.0;
 #pragma unroll
-        for (int u = 0; u < BT; ++u) {
-            if (i0 + u >= i_end) break;
-            const double* prow = Pm + (int64_t)(ps.goff + i0 + u) * NCM;
-            double s = 0.0;
+            for (int u = 0; u < BT; ++u) {
+                if (r0 + u >= nr) break;
+                double s = 0.0;
 #pragma unroll
-            for (int j = 0; j < NCM; ++j) s = fma(prow[j], cv[j], s);
-            dst[(int64_t)(i0 + u) * ps.out_si] = ps.accumulate ? old[u] + s : s;
+                for (int j = 0; j < NCM; ++j) s = fma(sp[(r0 + u) * NCM + j], cv[j], s);
+                dst[(int64_t)(c0 + r0 + u) * ps.out_si] = ps.accumulate ? old[u] + s : s;
+            }
         }
     }
 }
@@ -189,63 +209,112 @@ prolong_band_kernel(const AxisPass ps, const double* __restrict__ Pb, const int*
 // (rows padded to NCM columns with zeros; a null M[o][k] is no term).  The first pass
 // streams x and b once: 16 B per fine DOF, against 24 (residual) + 8 (restriction).
 // Every thread marches one line; the inputs of BT consecutive rows are loaded before
-// any of them is used, so BT x NI loads per wave are in flight instead of one.
-template <int NCM, int NO>
+// any of them is used.  The (o, k) terms of a pass are a compile-time MASK (bit
+// 3 o + k), and the workgroup stages the matrix rows of RB rows at a time into LDS,
+// read back as broadcasts: per-row scalar loads of the rows, each waited for before
+// its FMAs, left the first version latency-bound (1.5 ms for the 3D headline's
+// passes, against 1.0 ms for the residual and the restriction it replaces).
+constexpr int mask_np(int m) { int c = 0; for (int b = 0; b < 9; ++b) c += (m >> b) & 1; return c; }
+constexpr int mask_bit(int m, int p) {   // bit of the p-th term
+    for (int b = 0, c = 0; b < 9; ++b)
+        if ((m >> b) & 1) { if (c == p) return b; ++c; }
+    return 0;
+}
+constexpr int mask_no(int m) { int n = 0; for (int b = 0; b < 9; ++b) if ((m >> b) & 1) n = b / 3 + 1 > n ? b / 3 + 1 : n; return n; }
+constexpr int mask_ni(int m) { int n = 0; for (int b = 0; b < 9; ++b) if ((m >> b) & 1) n = b % 3 + 1 > n ? b % 3 + 1 : n; return n; }
+
+template <int NCM, int MASK, int LPT>
 __global__ void __launch_bounds__(256)
 mrestrict_kernel(const MultiPass mp, double* __restrict__ part) {
-    constexpr int BT = 4;
+    constexpr int BT = 4, RB = 32;
+    constexpr int NP = mask_np(MASK), NO = mask_no(MASK), NI = mask_ni(MASK);
+    __shared__ double smat[RB * NP * NCM];
     const AxisPass& ps = mp.ps;
-    const int64_t tid = (int64_t)blockIdx.x * 256 + threadIdx.x;
     const int64_t nline = ps.nA * ps.nB1 * ps.nB2;
-    if (tid >= nline) return;
+    // LPT lines per thread, nh apart (each wave's loads stay coalesced): every value read
+    // from LDS feeds LPT FMAs.  (every thread stages rows and takes the barriers)
+    const int64_t nh = (nline + LPT - 1) / LPT;
+    const int64_t tid = (int64_t)blockIdx.x * 256 + threadIdx.x;
     const int ks = gridDim.y, kc = (ps.nI + ks - 1) / ks;
     const int i_begin = blockIdx.y * kc, i_end = min(ps.nI, i_begin + kc);
-    const int64_t b2 = tid % ps.nB2;
-    const int64_t t1 = tid / ps.nB2;
-    const int64_t b1 = t1 % ps.nB1;
-    const int64_t a = t1 / ps.nB1;
-    const int64_t ioff = ps.in_base + a * ps.in_sa + b1 * ps.in_sb1 + b2 * ps.in_sb2;
-    double acc[NO][NCM];
+    bool live[LPT];
+    int64_t ioff[LPT], doff[LPT];
 #pragma unroll
-    for (int o = 0; o < NO; ++o)
+    for (int L = 0; L < LPT; ++L) {
+        const int64_t t = tid + L * nh;
+        live[L] = tid < nh && t < nline;
+        const int64_t ln = live[L] ? t : 0;
+        const int64_t b2 = ln % ps.nB2;
+        const int64_t t1 = ln / ps.nB2;
+        const int64_t b1 = t1 % ps.nB1;
+        const int64_t a = t1 / ps.nB1;
+        ioff[L] = ps.in_base + a * ps.in_sa + b1 * ps.in_sb1 + b2 * ps.in_sb2;
+        doff[L] = ps.out_base + a * ps.out_sa + b1 * ps.out_sb1 + b2 * ps.out_sb2;
+    }
+    double acc[LPT][NO][NCM];
 #pragma unroll
-        for (int j = 0; j < NCM; ++j) acc[o][j] = 0.0;
-    for (int i0 = i_begin; i0 < i_end; i0 += BT) {
-        double v[BT][3];
+    for (int L = 0; L < LPT; ++L)
 #pragma unroll
-        for (int u = 0; u < BT; ++u)
+        for (int o = 0; o < NO; ++o)
 #pragma unroll
-            for (int k = 0; k < 3; ++k)
-                v[u][k] = (k < mp.ni && i0 + u < i_end) ? mp.in[k][ioff + (int64_t)(i0 + u) * ps.in_si] : 0.0;
+            for (int j = 0; j < NCM; ++j) acc[L][o][j] = 0.0;
+    for (int c0 = i_begin; c0 < i_end; c0 += RB) {
+        const int nr = min(RB, i_end - c0);
+        __syncthreads();   // the previous stage's rows are read
+        for (int e = threadIdx.x; e < nr * NP * NCM; e += 256) {
+            const int r = e / (NP * NCM), q = e - r * (NP * NCM), pp = q / NCM, j = q - pp * NCM;
+            const double* m = nullptr;
 #pragma unroll
-        for (int u = 0; u < BT; ++u) {
-            if (i0 + u >= i_end) break;
-            const int64_t row = (int64_t)(ps.goff + i0 + u) * NCM;
+            for (int t = 0; t < NP; ++t)
+                if (t == pp) m = mp.m[mask_bit(MASK, t) / 3][mask_bit(MASK, t) % 3];
+            smat[e] = m[(int64_t)(ps.goff + c0 + r) * NCM + j];
+        }
+        __syncthreads();
+        if (!live[0]) continue;
+        for (int r0 = 0; r0 < nr; r0 += BT) {
+            double v[BT][LPT][NI];
+#pragma unroll
+            for (int u = 0; u < BT; ++u)
+#pragma unroll
+                for (int L = 0; L < LPT; ++L)
+#pragma unroll
+                    for (int k = 0; k < NI; ++k)
+                        v[u][L][k] = (r0 + u < nr && live[L]) ? mp.in[k][ioff[L] + (int64_t)(c0 + r0 + u) * ps.in_si] : 0.0;
+#pragma unroll
+            for (int u = 0; u < BT; ++u) {
+                if (r0 + u >= nr) break;
+                const double* sm = smat + (r0 + u) * NP * NCM;
+#pragma unroll
+                for (int t = 0; t < NP; ++t) {
+                    const int o = mask_bit(MASK, t) / 3, k = mask_bit(MASK, t) % 3;
+#pragma unroll
+                    for (int j = 0; j < NCM; ++j) {
+                        const double mv = sm[t * NCM + j];
+#pragma unroll
+                        for (int L = 0; L < LPT; ++L) acc[L][o][j] = fma(mv, v[u][L][k], acc[L][o][j]);
+                    }
+                }
+            }
+        }
+    }
+#pragma unroll
+    for (int L = 0; L < LPT; ++L) {
+        if (!live[L]) continue;
+        const int64_t t = tid + L * nh;
+        if (ks > 1) {   // partials [chunk][o][j][line]: coalesced over lines
 #pragma unroll
             for (int o = 0; o < NO; ++o)
 #pragma unroll
-                for (int k = 0; k < 3; ++k) {
-                    const double* m = mp.m[o][k];
-                    if (m == nullptr) continue;
-#pragma unroll
-                    for (int j = 0; j < NCM; ++j) acc[o][j] = fma(m[row + j], v[u][k], acc[o][j]);
-                }
+                for (int j = 0; j < NCM; ++j)
+                    if (j < ps.nJ) part[(((int64_t)blockIdx.y * NO + o) * NCM + j) * nline + t] = acc[L][o][j];
+            continue;
         }
-    }
-    if (ks > 1) {   // partials [chunk][o][j][line]: coalesced over lines
 #pragma unroll
         for (int o = 0; o < NO; ++o)
 #pragma unroll
             for (int j = 0; j < NCM; ++j)
-                if (j < ps.nJ) part[(((int64_t)blockIdx.y * NO + o) * NCM + j) * nline + tid] = acc[o][j];
-        return;
+                if (j < ps.nJ) mp.out[o][doff[L] + (int64_t)j * ps.out_si] = acc[L][o][j];
     }
-    const int64_t doff = ps.out_base + a * ps.out_sa + b1 * ps.out_sb1 + b2 * ps.out_sb2;
-#pragma unroll
-    for (int o = 0; o < NO; ++o)
-#pragma unroll
-        for (int j = 0; j < NCM; ++j)
-            if (j < ps.nJ) mp.out[o][doff + (int64_t)j * ps.out_si] = acc[o][j];
 }
 
 // Sum of the ks chunk partials of every output, in chunk order (deterministic); the
@@ -293,11 +362,22 @@ int64_t mrestrict_scratch(const MultiPass& mp, int ncm) {   // doubles of partia
     return ks > 1 ? ks * (int64_t)mp.no * ncm * nline : 0;
 }
 
-template <int NCM>
-static void mrestrict_go(const MultiPass& mp, dim3 grid, double* part, hipStream_t st) {
-    if (mp.no == 1) hipLaunchKernelGGL((mrestrict_kernel<NCM, 1>), grid, dim3(256), 0, st, mp, part);
-    else if (mp.no == 2) hipLaunchKernelGGL((mrestrict_kernel<NCM, 2>), grid, dim3(256), 0, st, mp, part);
-    else hipLaunchKernelGGL((mrestrict_kernel<NCM, 3>), grid, dim3(256), 0, st, mp, part);
+// the term patterns poms_resid_restrict issues (bit 3 o + k): FORM_SUM axis 0 (and
+// 2D's first pass), axis 1, last pass; FORM_SINGLE the same three
+constexpr int kMasks[6] = {(1 << 1) | (1 << 3) | (1 << 6), 1 | (1 << 4) | (1 << 5) | (1 << 8), 7,
+                           (1 << 1) | (1 << 3), 1 | (1 << 4), 3};
+
+template <int NCM, int LPT>
+static int mrestrict_go(int mask, const MultiPass& mp, dim3 grid, double* part, hipStream_t st) {
+    switch (mask) {
+        case kMasks[0]: hipLaunchKernelGGL((mrestrict_kernel<NCM, kMasks[0], LPT>), grid, dim3(256), 0, st, mp, part); return 0;
+        case kMasks[1]: hipLaunchKernelGGL((mrestrict_kernel<NCM, kMasks[1], LPT>), grid, dim3(256), 0, st, mp, part); return 0;
+        case kMasks[2]: hipLaunchKernelGGL((mrestrict_kernel<NCM, kMasks[2], LPT>), grid, dim3(256), 0, st, mp, part); return 0;
+        case kMasks[3]: hipLaunchKernelGGL((mrestrict_kernel<NCM, kMasks[3], LPT>), grid, dim3(256), 0, st, mp, part); return 0;
+        case kMasks[4]: hipLaunchKernelGGL((mrestrict_kernel<NCM, kMasks[4], LPT>), grid, dim3(256), 0, st, mp, part); return 0;
+        case kMasks[5]: hipLaunchKernelGGL((mrestrict_kernel<NCM, kMasks[5], LPT>), grid, dim3(256), 0, st, mp, part); return 0;
+        default: set_error("resid_restrict: unsupported term pattern"); return 1;
+    }
 }
 
 int mrestrict_launch(int ncm, const MultiPass& mp, double* part, hipStream_t st) {
@@ -305,16 +385,30 @@ int mrestrict_launch(int ncm, const MultiPass& mp, double* part, hipStream_t st)
     const int nb = (int)((nline + 255) / 256);
     if (nb == 0) return 0;
     if (mp.no < 1 || mp.no > 3 || mp.ni < 1 || mp.ni > 3) { set_error("resid_restrict: 1..3 inputs / outputs"); return 1; }
+    int mask = 0;
+    for (int o = 0; o < 3; ++o)
+        for (int k = 0; k < 3; ++k)
+            if (mp.m[o][k]) mask |= 1 << (3 * o + k);
+    if (mask_no(mask) != mp.no || mask_ni(mask) != mp.ni) { set_error("resid_restrict: term pattern vs counts"); return 1; }
     const int ks = part ? mrestrict_split(nline, mp.ps.nI, mp.ni, mp.no, ncm) : 1;
-    const dim3 grid(nb, ks);
     double* pk = ks > 1 ? part : nullptr;
-    switch (ncm) {
-        case 8: mrestrict_go<8>(mp, grid, pk, st); break;
-        case 12: mrestrict_go<12>(mp, grid, pk, st); break;
-        case 16: mrestrict_go<16>(mp, grid, pk, st); break;
-        case 32: mrestrict_go<32>(mp, grid, pk, st); break;
-        default: set_error("resid_restrict: coarse extent must be <= 32"); return 1;
+    // two lines per thread on many lines (the 3D axis-0 pass: the LDS reads of the
+    // staged rows, not HBM, bounded the one-line build), up to ncm 16
+    const char* le = std::getenv("POMS_MR_LPT");
+    const int lpt = (le && std::atoi(le) >= 1) ? std::min(2, std::atoi(le)) : (nline >= 65536 && ncm <= 16 ? 2 : 1);
+    const dim3 grid(lpt == 2 ? (unsigned)((nline + 511) / 512) : (unsigned)nb, ks);
+    int rc = 1;
+    switch (ncm * 4 + lpt) {
+        case 8 * 4 + 1: rc = mrestrict_go<8, 1>(mask, mp, grid, pk, st); break;
+        case 12 * 4 + 1: rc = mrestrict_go<12, 1>(mask, mp, grid, pk, st); break;
+        case 16 * 4 + 1: rc = mrestrict_go<16, 1>(mask, mp, grid, pk, st); break;
+        case 32 * 4 + 1: rc = mrestrict_go<32, 1>(mask, mp, grid, pk, st); break;
+        case 8 * 4 + 2: rc = mrestrict_go<8, 2>(mask, mp, grid, pk, st); break;
+        case 12 * 4 + 2: rc = mrestrict_go<12, 2>(mask, mp, grid, pk, st); break;
+        case 16 * 4 + 2: rc = mrestrict_go<16, 2>(mask, mp, grid, pk, st); break;
+        default: set_error("resid_restrict: coarse extent must be <= 32 (two lines per thread: <= 16)"); return 1;
     }
+    if (rc) return 1;
     if (ks > 1) {
         const int64_t nsum = nline * mp.ps.nJ * mp.no;
         hipLaunchKernelGGL(mrestrict_sum_kernel, dim3((unsigned)((nsum + 255) / 256)), dim3(256), 0, st, mp, ncm,
