@@ -211,9 +211,10 @@ prolong_band_kernel(const AxisPass ps, const double* __restrict__ Pb, const int*
 // Every thread marches one line; the inputs of BT consecutive rows are loaded before
 // any of them is used.  The (o, k) terms of a pass are a compile-time MASK (bit
 // 3 o + k), and the workgroup stages the matrix rows of RB rows at a time into LDS,
-// read back as broadcasts: per-row scalar loads of the rows, each waited for before
-// its FMAs, left the first version latency-bound (1.5 ms for the 3D headline's
-// passes, against 1.0 ms for the residual and the restriction it replaces).
+// read back as broadcasts.  Measured at 515^3 (the three passes, round 6): scalar
+// loads of the rows, each waited for before its FMAs, 1.52-1.55 ms; LDS-staged rows
+// 0.69-0.70 ms; the same with two lines per thread (half the LDS reads per line, two
+// waves per SIMD) 0.83 ms.  The residual + restriction pair it replaces: 0.92 ms.
 constexpr int mask_np(int m) { int c = 0; for (int b = 0; b < 9; ++b) c += (m >> b) & 1; return c; }
 constexpr int mask_bit(int m, int p) {   // bit of the p-th term
     for (int b = 0, c = 0; b < 9; ++b)
@@ -223,41 +224,29 @@ constexpr int mask_bit(int m, int p) {   // bit of the p-th term
 constexpr int mask_no(int m) { int n = 0; for (int b = 0; b < 9; ++b) if ((m >> b) & 1) n = b / 3 + 1 > n ? b / 3 + 1 : n; return n; }
 constexpr int mask_ni(int m) { int n = 0; for (int b = 0; b < 9; ++b) if ((m >> b) & 1) n = b % 3 + 1 > n ? b % 3 + 1 : n; return n; }
 
-template <int NCM, int MASK, int LPT>
+template <int NCM, int MASK>
 __global__ void __launch_bounds__(256)
 mrestrict_kernel(const MultiPass mp, double* __restrict__ part) {
     constexpr int BT = 4, RB = 32;
     constexpr int NP = mask_np(MASK), NO = mask_no(MASK), NI = mask_ni(MASK);
     __shared__ double smat[RB * NP * NCM];
     const AxisPass& ps = mp.ps;
-    const int64_t nline = ps.nA * ps.nB1 * ps.nB2;
-    // LPT lines per thread, nh apart (each wave's loads stay coalesced): every value read
-    // from LDS feeds LPT FMAs.  (every thread stages rows and takes the barriers)
-    const int64_t nh = (nline + LPT - 1) / LPT;
     const int64_t tid = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    const int64_t nline = ps.nA * ps.nB1 * ps.nB2;
+    const bool live = tid < nline;   // (every thread stages rows and takes the barriers)
     const int ks = gridDim.y, kc = (ps.nI + ks - 1) / ks;
     const int i_begin = blockIdx.y * kc, i_end = min(ps.nI, i_begin + kc);
-    bool live[LPT];
-    int64_t ioff[LPT], doff[LPT];
+    const int64_t ln = live ? tid : 0;
+    const int64_t b2 = ln % ps.nB2;
+    const int64_t t1 = ln / ps.nB2;
+    const int64_t b1 = t1 % ps.nB1;
+    const int64_t a = t1 / ps.nB1;
+    const int64_t ioff = ps.in_base + a * ps.in_sa + b1 * ps.in_sb1 + b2 * ps.in_sb2;
+    double acc[NO][NCM];
 #pragma unroll
-    for (int L = 0; L < LPT; ++L) {
-        const int64_t t = tid + L * nh;
-        live[L] = tid < nh && t < nline;
-        const int64_t ln = live[L] ? t : 0;
-        const int64_t b2 = ln % ps.nB2;
-        const int64_t t1 = ln / ps.nB2;
-        const int64_t b1 = t1 % ps.nB1;
-        const int64_t a = t1 / ps.nB1;
-        ioff[L] = ps.in_base + a * ps.in_sa + b1 * ps.in_sb1 + b2 * ps.in_sb2;
-        doff[L] = ps.out_base + a * ps.out_sa + b1 * ps.out_sb1 + b2 * ps.out_sb2;
-    }
-    double acc[LPT][NO][NCM];
+    for (int o = 0; o < NO; ++o)
 #pragma unroll
-    for (int L = 0; L < LPT; ++L)
-#pragma unroll
-        for (int o = 0; o < NO; ++o)
-#pragma unroll
-            for (int j = 0; j < NCM; ++j) acc[L][o][j] = 0.0;
+        for (int j = 0; j < NCM; ++j) acc[o][j] = 0.0;
     for (int c0 = i_begin; c0 < i_end; c0 += RB) {
         const int nr = min(RB, i_end - c0);
         __syncthreads();   // the previous stage's rows are read
@@ -270,16 +259,14 @@ mrestrict_kernel(const MultiPass mp, double* __restrict__ part) {
             smat[e] = m[(int64_t)(ps.goff + c0 + r) * NCM + j];
         }
         __syncthreads();
-        if (!live[0]) continue;
+        if (!live) continue;
         for (int r0 = 0; r0 < nr; r0 += BT) {
-            double v[BT][LPT][NI];
+            double v[BT][NI];
 #pragma unroll
             for (int u = 0; u < BT; ++u)
 #pragma unroll
-                for (int L = 0; L < LPT; ++L)
-#pragma unroll
-                    for (int k = 0; k < NI; ++k)
-                        v[u][L][k] = (r0 + u < nr && live[L]) ? mp.in[k][ioff[L] + (int64_t)(c0 + r0 + u) * ps.in_si] : 0.0;
+                for (int k = 0; k < NI; ++k)
+                    v[u][k] = (r0 + u < nr) ? mp.in[k][ioff + (int64_t)(c0 + r0 + u) * ps.in_si] : 0.0;
 #pragma unroll
             for (int u = 0; u < BT; ++u) {
                 if (r0 + u >= nr) break;
@@ -288,33 +275,26 @@ mrestrict_kernel(const MultiPass mp, double* __restrict__ part) {
                 for (int t = 0; t < NP; ++t) {
                     const int o = mask_bit(MASK, t) / 3, k = mask_bit(MASK, t) % 3;
 #pragma unroll
-                    for (int j = 0; j < NCM; ++j) {
-                        const double mv = sm[t * NCM + j];
-#pragma unroll
-                        for (int L = 0; L < LPT; ++L) acc[L][o][j] = fma(mv, v[u][L][k], acc[L][o][j]);
-                    }
+                    for (int j = 0; j < NCM; ++j) acc[o][j] = fma(sm[t * NCM + j], v[u][k], acc[o][j]);
                 }
             }
         }
     }
-#pragma unroll
-    for (int L = 0; L < LPT; ++L) {
-        if (!live[L]) continue;
-        const int64_t t = tid + L * nh;
-        if (ks > 1) {   // partials [chunk][o][j][line]: coalesced over lines
-#pragma unroll
-            for (int o = 0; o < NO; ++o)
-#pragma unroll
-                for (int j = 0; j < NCM; ++j)
-                    if (j < ps.nJ) part[(((int64_t)blockIdx.y * NO + o) * NCM + j) * nline + t] = acc[L][o][j];
-            continue;
-        }
+    if (!live) return;
+    if (ks > 1) {   // partials [chunk][o][j][line]: coalesced over lines
 #pragma unroll
         for (int o = 0; o < NO; ++o)
 #pragma unroll
             for (int j = 0; j < NCM; ++j)
-                if (j < ps.nJ) mp.out[o][doff[L] + (int64_t)j * ps.out_si] = acc[L][o][j];
+                if (j < ps.nJ) part[(((int64_t)blockIdx.y * NO + o) * NCM + j) * nline + tid] = acc[o][j];
+        return;
     }
+    const int64_t doff = ps.out_base + a * ps.out_sa + b1 * ps.out_sb1 + b2 * ps.out_sb2;
+#pragma unroll
+    for (int o = 0; o < NO; ++o)
+#pragma unroll
+        for (int j = 0; j < NCM; ++j)
+            if (j < ps.nJ) mp.out[o][doff + (int64_t)j * ps.out_si] = acc[o][j];
 }
 
 // Sum of the ks chunk partials of every output, in chunk order (deterministic); the
@@ -367,15 +347,15 @@ int64_t mrestrict_scratch(const MultiPass& mp, int ncm) {   // doubles of partia
 constexpr int kMasks[6] = {(1 << 1) | (1 << 3) | (1 << 6), 1 | (1 << 4) | (1 << 5) | (1 << 8), 7,
                            (1 << 1) | (1 << 3), 1 | (1 << 4), 3};
 
-template <int NCM, int LPT>
+template <int NCM>
 static int mrestrict_go(int mask, const MultiPass& mp, dim3 grid, double* part, hipStream_t st) {
     switch (mask) {
-        case kMasks[0]: hipLaunchKernelGGL((mrestrict_kernel<NCM, kMasks[0], LPT>), grid, dim3(256), 0, st, mp, part); return 0;
-        case kMasks[1]: hipLaunchKernelGGL((mrestrict_kernel<NCM, kMasks[1], LPT>), grid, dim3(256), 0, st, mp, part); return 0;
-        case kMasks[2]: hipLaunchKernelGGL((mrestrict_kernel<NCM, kMasks[2], LPT>), grid, dim3(256), 0, st, mp, part); return 0;
-        case kMasks[3]: hipLaunchKernelGGL((mrestrict_kernel<NCM, kMasks[3], LPT>), grid, dim3(256), 0, st, mp, part); return 0;
-        case kMasks[4]: hipLaunchKernelGGL((mrestrict_kernel<NCM, kMasks[4], LPT>), grid, dim3(256), 0, st, mp, part); return 0;
-        case kMasks[5]: hipLaunchKernelGGL((mrestrict_kernel<NCM, kMasks[5], LPT>), grid, dim3(256), 0, st, mp, part); return 0;
+        case kMasks[0]: hipLaunchKernelGGL((mrestrict_kernel<NCM, kMasks[0]>), grid, dim3(256), 0, st, mp, part); return 0;
+        case kMasks[1]: hipLaunchKernelGGL((mrestrict_kernel<NCM, kMasks[1]>), grid, dim3(256), 0, st, mp, part); return 0;
+        case kMasks[2]: hipLaunchKernelGGL((mrestrict_kernel<NCM, kMasks[2]>), grid, dim3(256), 0, st, mp, part); return 0;
+        case kMasks[3]: hipLaunchKernelGGL((mrestrict_kernel<NCM, kMasks[3]>), grid, dim3(256), 0, st, mp, part); return 0;
+        case kMasks[4]: hipLaunchKernelGGL((mrestrict_kernel<NCM, kMasks[4]>), grid, dim3(256), 0, st, mp, part); return 0;
+        case kMasks[5]: hipLaunchKernelGGL((mrestrict_kernel<NCM, kMasks[5]>), grid, dim3(256), 0, st, mp, part); return 0;
         default: set_error("resid_restrict: unsupported term pattern"); return 1;
     }
 }
@@ -391,22 +371,15 @@ int mrestrict_launch(int ncm, const MultiPass& mp, double* part, hipStream_t st)
             if (mp.m[o][k]) mask |= 1 << (3 * o + k);
     if (mask_no(mask) != mp.no || mask_ni(mask) != mp.ni) { set_error("resid_restrict: term pattern vs counts"); return 1; }
     const int ks = part ? mrestrict_split(nline, mp.ps.nI, mp.ni, mp.no, ncm) : 1;
+    const dim3 grid(nb, ks);
     double* pk = ks > 1 ? part : nullptr;
-    // two lines per thread on many lines (the 3D axis-0 pass: the LDS reads of the
-    // staged rows, not HBM, bounded the one-line build), up to ncm 16
-    const char* le = std::getenv("POMS_MR_LPT");
-    const int lpt = (le && std::atoi(le) >= 1) ? std::min(2, std::atoi(le)) : (nline >= 65536 && ncm <= 16 ? 2 : 1);
-    const dim3 grid(lpt == 2 ? (unsigned)((nline + 511) / 512) : (unsigned)nb, ks);
     int rc = 1;
-    switch (ncm * 4 + lpt) {
-        case 8 * 4 + 1: rc = mrestrict_go<8, 1>(mask, mp, grid, pk, st); break;
-        case 12 * 4 + 1: rc = mrestrict_go<12, 1>(mask, mp, grid, pk, st); break;
-        case 16 * 4 + 1: rc = mrestrict_go<16, 1>(mask, mp, grid, pk, st); break;
-        case 32 * 4 + 1: rc = mrestrict_go<32, 1>(mask, mp, grid, pk, st); break;
-        case 8 * 4 + 2: rc = mrestrict_go<8, 2>(mask, mp, grid, pk, st); break;
-        case 12 * 4 + 2: rc = mrestrict_go<12, 2>(mask, mp, grid, pk, st); break;
-        case 16 * 4 + 2: rc = mrestrict_go<16, 2>(mask, mp, grid, pk, st); break;
-        default: set_error("resid_restrict: coarse extent must be <= 32 (two lines per thread: <= 16)"); return 1;
+    switch (ncm) {
+        case 8: rc = mrestrict_go<8>(mask, mp, grid, pk, st); break;
+        case 12: rc = mrestrict_go<12>(mask, mp, grid, pk, st); break;
+        case 16: rc = mrestrict_go<16>(mask, mp, grid, pk, st); break;
+        case 32: rc = mrestrict_go<32>(mask, mp, grid, pk, st); break;
+        default: set_error("resid_restrict: coarse extent must be <= 32"); return 1;
     }
     if (rc) return 1;
     if (ks > 1) {
