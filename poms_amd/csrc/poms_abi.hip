@@ -71,7 +71,7 @@ int band_lu(int64_t n, int kl, int ku, double* ab, int64_t ldab, int* ipiv);
 void band_lu_tables(int64_t n, int kl, int ku, const double* ab, int64_t ldab, const int* ipiv,
                     std::vector<double>& L, std::vector<double>& U, std::vector<int>& piv);
 
-enum { V_AXPBY = 0, V_SCALE = 1, V_FILL = 2, V_DOT = 3, V_PCGUPD = 4, V_RUPD = 5, V_XPUPD = 6 };
+enum { V_AXPBY = 0, V_SCALE = 1, V_FILL = 2, V_DOT = 3, V_PCGUPD = 4, V_RUPD = 5, V_XPUPD = 6, V_SCALEDOT = 7 };   // (vec_ops.hip's VecOp)
 
 }  // namespace poms
 
@@ -1359,6 +1359,26 @@ int poms_vec_scale(poms_ctx* ctx, const poms_layout* L, double a, const double* 
                    void* stream) {
     if (!x || !z) { set_error("scale: null vector"); return 1; }
     return vec_common(ctx, L, V_SCALE, a, 0.0, x, nullptr, z, nullptr, nullptr, nullptr, stream);
+}
+
+// z = x and z.z into out_dev in one pass (pcg from x0 = None: r = b, ||r||^2), with the
+// bits of poms_vec_scale(1.0) + poms_vec_dot(z, z): the same flat grid, the same
+// per-thread order.  Where the flat kernel does not apply (mixed alignment, ghost
+// data) the two calls.
+static int vec_copy_dot(poms_ctx* ctx, const poms_layout* L, const double* x, double* z, double* out_dev,
+                        void* stream) {
+    if (!ctx || !layout_ok(L) || !x || !z || !out_dev) { set_error("copy_dot: bad argument"); return 1; }
+    const RowGeom g = row_geom(L);
+    const int64_t off = (int64_t)g.pd0 * g.s0, count = (int64_t)g.n0 * g.s0;
+    int nb = 0;
+    if (!(L->flags & POMS_LAYOUT_GHOST_DATA) &&
+        vec_flat_launch(V_SCALEDOT, count, 1.0, 0.0, x + off, nullptr, z + off, nullptr, nullptr, ctx->scratch,
+                        as_stream(stream), &nb) == 0) {
+        reduce_wide_launch(ctx->scratch, nb, out_dev, as_stream(stream));
+        POMS_HIP_CHECK(hipGetLastError());
+        return 0;
+    }
+    return poms_vec_scale(ctx, L, 1.0, x, z, stream) || poms_vec_dot(ctx, L, z, z, out_dev, stream);
 }
 
 int poms_vec_fill(poms_ctx* ctx, const poms_layout* L, double v, double* z, void* stream) {
@@ -2703,13 +2723,15 @@ static int spec_issue(PcgRun& R, const double* b, double* x, int has_x0, double*
         POMS_HIP_CHECK(hipMemcpyAsync(op->spec_bak, x, nbak * sizeof(double), hipMemcpyDeviceToDevice, R.st));
     }
     if (!has_x0) {
-        if (poms_vec_fill(ctx, L, 0.0, x, stream) || poms_vec_scale(ctx, L, 1.0, b, r, stream)) return 1;
+        if (poms_vec_fill(ctx, L, 0.0, x, stream)) return 1;
     } else if (R.run(EPI_RESID, x, r, b, nullptr, nullptr)) {
         return 1;
     }
     const int vrr0 = R.svals(1);
     *vrr0_out = vrr0;
-    if (poms_vec_dot(ctx, L, r, r, op->spec_dev + vrr0, stream)) return 1;
+    if (!has_x0 ? vec_copy_dot(ctx, L, b, r, op->spec_dev + vrr0, stream)   // r = b and r.r
+                : poms_vec_dot(ctx, L, r, r, op->spec_dev + vrr0, stream))
+        return 1;
     double* s = nullptr;
     if (R.spec_damped_jacobi(r, z[0], z[1], SC_SR, &s)) return 1;
     double* p = s;   // p keeps this buffer; the later psolves use the other two
@@ -2946,14 +2968,18 @@ static int pcg_jacobi_impl(poms_op* op, poms_comm* comm, const poms_pcg_opts* o,
     double* z[3] = {work[2], work[3], work[4]};
     // x0 = None: x = 0, r = b - A.0 = b exactly; else r = b - A x0
     if (!has_x0) {
-        if (poms_vec_fill(ctx, L, 0.0, x, stream) || poms_vec_scale(ctx, L, 1.0, b, r, stream)) return 1;
+        if (poms_vec_fill(ctx, L, 0.0, x, stream)) return 1;
     } else if (R.run(EPI_RESID, x, r, b, nullptr, nullptr)) {
         return 1;
     }
     const int hrr0 = R.arm(H_RR0, 1);
     {
         double* d = R.hslot(hrr0);
-        if (!d || poms_vec_dot(ctx, L, r, r, d, stream) || R.lazy_post(hrr0, 1)) return 1;
+        if (!d) return 1;
+        if (!has_x0 ? vec_copy_dot(ctx, L, b, r, d, stream)   // r = b and r.r in one pass
+                    : poms_vec_dot(ctx, L, r, r, d, stream))
+            return 1;
+        if (R.lazy_post(hrr0, 1)) return 1;
     }
     const double nrmr0 = std::sqrt(R.get(hrr0));
     if (R.failed) return 1;

@@ -11,7 +11,8 @@
 
 namespace poms {
 
-enum VecOp : int { V_AXPBY = 0, V_SCALE = 1, V_FILL = 2, V_DOT = 3, V_PCGUPD = 4, V_RUPD = 5, V_XPUPD = 6 };
+enum VecOp : int { V_AXPBY = 0, V_SCALE = 1, V_FILL = 2, V_DOT = 3, V_PCGUPD = 4, V_RUPD = 5, V_XPUPD = 6,
+                  V_SCALEDOT = 7 /* z = a x and z.z (flat kernel only) */ };
 
 // grid caps (= partial sums per launch): the flat vector kernels run one pass per
 // thread up to 65536 blocks of 256 (grid-stride beyond): at 515^3 the r update
@@ -98,6 +99,10 @@ __device__ __forceinline__ void vec_elem(double a, double b, const double* x, co
         const double po = w[o];
         z[o] = fma(a, po, z[o]);
         w[o] = x[o] + b * po;
+    } else if constexpr (OP == V_SCALEDOT) {
+        const double zo = a * x[o];
+        z[o] = zo;
+        s = fma(zo, zo, s);
     }
 }
 
@@ -159,7 +164,8 @@ vec_flat_kernel(const int head, const int64_t nd2, const int tail, double a, dou
                 // (tools/ubench_copy.hip: 1 KiB per wave and load, nt loads + nt stores
                 // 6.1-6.2 TB/s against 5.7 with plain loads)
                 auto ld = [](const d2* ptr) { if constexpr (NTL) return __builtin_nontemporal_load(ptr); else return *ptr; };
-                if constexpr (OP == V_AXPBY || OP == V_SCALE || OP == V_DOT || OP == V_XPUPD) xa[u] = ld(X + i);
+                if constexpr (OP == V_AXPBY || OP == V_SCALE || OP == V_DOT || OP == V_XPUPD || OP == V_SCALEDOT)
+                    xa[u] = ld(X + i);
                 if constexpr (OP == V_AXPBY || OP == V_DOT || OP == V_PCGUPD) ya[u] = ld(Y + i);
                 if constexpr (OP == V_PCGUPD || OP == V_XPUPD) za[u] = ld(Z + i);
                 if constexpr (OP == V_PCGUPD || OP == V_RUPD || OP == V_XPUPD) wa[u] = ld(Wv + i);
@@ -174,6 +180,11 @@ vec_flat_kernel(const int head, const int64_t nd2, const int tail, double a, dou
                     __builtin_nontemporal_store(a * xa[u] + b * ya[u], Z + i);
                 } else if constexpr (OP == V_SCALE) {
                     __builtin_nontemporal_store(a * xa[u], Z + i);
+                } else if constexpr (OP == V_SCALEDOT) {   // (with a = 1: the bits of V_SCALE + V_DOT(z, z))
+                    const d2 zn = a * xa[u];
+                    __builtin_nontemporal_store(zn, Z + i);
+                    s = fma(zn.x, zn.x, s);
+                    s = fma(zn.y, zn.y, s);
                 } else if constexpr (OP == V_DOT) {
                     s = fma(xa[u].x, ya[u].x, s);
                     s = fma(xa[u].y, ya[u].y, s);
@@ -208,7 +219,7 @@ vec_flat_kernel(const int head, const int64_t nd2, const int tail, double a, dou
         if (head) vec_elem<OP>(a, b, x, yv, z, w, q, 0, s);
         if (tail) vec_elem<OP>(a, b, x, yv, z, w, q, head + 2 * nd2, s);
     }
-    if constexpr (OP == V_DOT || OP == V_PCGUPD || OP == V_RUPD) {
+    if constexpr (OP == V_DOT || OP == V_PCGUPD || OP == V_RUPD || OP == V_SCALEDOT) {
         const double t = block_sum_256(s, red);
         if (threadIdx.x == 0) partial[blockIdx.x] = t;
     }
@@ -438,6 +449,7 @@ int vec_flat_launch(int op, int64_t count, double a, double b, const double* x, 
         POMS_VF(V_PCGUPD)
         POMS_VF(V_RUPD)
         POMS_VF(V_XPUPD)
+        POMS_VF(V_SCALEDOT)
 #undef POMS_VF
     }
     return 1;

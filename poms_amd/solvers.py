@@ -187,7 +187,9 @@ def _pcg_native(A, b, x0, tol, maxiter, x0_owned=False):
     work = getattr(A, "_pcg_work", None)
     if work is None or work[0].space is not V:
         work = A._pcg_work = [V.empty() for _ in range(5)]
-    x = V.zeros() if x0 is None else (x0 if x0_owned else x0.copy())
+    # (x0 = None: the C loop zero-fills x's interior; empty() zeroes only the ghosts,
+    # instead of a second full-storage fill)
+    x = V.empty() if x0 is None else (x0 if x0_owned else x0.copy())
     if x0 is not None:
         assert x0.shape == (A.shape[0],)
     d = V.dist if V.is_distributed else None
