@@ -29,7 +29,9 @@ restrict_pass_kernel(const AxisPass ps, const double* __restrict__ Pm,
     // Rows of P are staged through LDS, RB at a time, and read back as broadcasts; the
     // inputs of BT rows are loaded before any is used (round 6: per-row scalar loads of
     // P, each waited for, and one input load per wave in flight left the 515^3 axis-0
-    // pass latency-bound).  The FMAs keep their order: the same bits.
+    // pass latency-bound).  The FMAs keep their order: the same bits.  (16 rows and
+    // non-temporal loads, as the fused pass takes them: 249-251 -> 257-258 us; the
+    // prolong-add with nt loads and stores 575-578 -> 634-638 us; not kept.)
     constexpr int BT = 8, RB = 64;
     __shared__ double sp[RB * NCM];
     const int64_t tid = (int64_t)blockIdx.x * 256 + threadIdx.x;
@@ -224,10 +226,9 @@ constexpr int mask_bit(int m, int p) {   // bit of the p-th term
 constexpr int mask_no(int m) { int n = 0; for (int b = 0; b < 9; ++b) if ((m >> b) & 1) n = b / 3 + 1 > n ? b / 3 + 1 : n; return n; }
 constexpr int mask_ni(int m) { int n = 0; for (int b = 0; b < 9; ++b) if ((m >> b) & 1) n = b % 3 + 1 > n ? b % 3 + 1 : n; return n; }
 
-template <int NCM, int MASK>
+template <int NCM, int MASK, int BT = 4, int RB = 32, bool NT = false>
 __global__ void __launch_bounds__(256)
 mrestrict_kernel(const MultiPass mp, double* __restrict__ part) {
-    constexpr int BT = 4, RB = 32;
     constexpr int NP = mask_np(MASK), NO = mask_no(MASK), NI = mask_ni(MASK);
     __shared__ double smat[RB * NP * NCM];
     const AxisPass& ps = mp.ps;
@@ -266,7 +267,8 @@ mrestrict_kernel(const MultiPass mp, double* __restrict__ part) {
             for (int u = 0; u < BT; ++u)
 #pragma unroll
                 for (int k = 0; k < NI; ++k)
-                    v[u][k] = (r0 + u < nr) ? mp.in[k][ioff + (int64_t)(c0 + r0 + u) * ps.in_si] : 0.0;
+                    v[u][k] = (r0 + u < nr) ? (NT ? __builtin_nontemporal_load(mp.in[k] + ioff + (int64_t)(c0 + r0 + u) * ps.in_si)
+                                                  : mp.in[k][ioff + (int64_t)(c0 + r0 + u) * ps.in_si]) : 0.0;
 #pragma unroll
             for (int u = 0; u < BT; ++u) {
                 if (r0 + u >= nr) break;
@@ -343,17 +345,21 @@ int64_t mrestrict_scratch(const MultiPass& mp, int ncm) {   // doubles of partia
 }
 
 // the term patterns poms_resid_restrict issues (bit 3 o + k): FORM_SUM axis 0 (and
-// 2D's first pass), axis 1, last pass; FORM_SINGLE the same three
+// 2D's first pass), axis 1, last pass; FORM_SINGLE the same three.  The first passes
+// (x and b streamed once) load 16 rows per batch with non-temporal loads and stage 64
+// rows: 515^3, interleaved A/B on one box (profiles/r06/resid_restrict/ab_axis0.txt):
+// 4 / 32 / plain 705-710 us, 8 / 64 / nt 633-641, 8 / 128 / nt 632-633, 16 / 64 / nt
+// 622-623, 16 / 128 / nt 623-628.
 constexpr int kMasks[6] = {(1 << 1) | (1 << 3) | (1 << 6), 1 | (1 << 4) | (1 << 5) | (1 << 8), 7,
                            (1 << 1) | (1 << 3), 1 | (1 << 4), 3};
 
 template <int NCM>
 static int mrestrict_go(int mask, const MultiPass& mp, dim3 grid, double* part, hipStream_t st) {
     switch (mask) {
-        case kMasks[0]: hipLaunchKernelGGL((mrestrict_kernel<NCM, kMasks[0]>), grid, dim3(256), 0, st, mp, part); return 0;
+        case kMasks[0]: hipLaunchKernelGGL((mrestrict_kernel<NCM, kMasks[0], 16, 64, true>), grid, dim3(256), 0, st, mp, part); return 0;
         case kMasks[1]: hipLaunchKernelGGL((mrestrict_kernel<NCM, kMasks[1]>), grid, dim3(256), 0, st, mp, part); return 0;
         case kMasks[2]: hipLaunchKernelGGL((mrestrict_kernel<NCM, kMasks[2]>), grid, dim3(256), 0, st, mp, part); return 0;
-        case kMasks[3]: hipLaunchKernelGGL((mrestrict_kernel<NCM, kMasks[3]>), grid, dim3(256), 0, st, mp, part); return 0;
+        case kMasks[3]: hipLaunchKernelGGL((mrestrict_kernel<NCM, kMasks[3], 16, 64, true>), grid, dim3(256), 0, st, mp, part); return 0;
         case kMasks[4]: hipLaunchKernelGGL((mrestrict_kernel<NCM, kMasks[4]>), grid, dim3(256), 0, st, mp, part); return 0;
         case kMasks[5]: hipLaunchKernelGGL((mrestrict_kernel<NCM, kMasks[5]>), grid, dim3(256), 0, st, mp, part); return 0;
         default: set_error("resid_restrict: unsupported term pattern"); return 1;
