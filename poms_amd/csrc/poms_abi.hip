@@ -1371,7 +1371,8 @@ static int vec_copy_dot(poms_ctx* ctx, const poms_layout* L, const double* x, do
     const RowGeom g = row_geom(L);
     const int64_t off = (int64_t)g.pd0 * g.s0, count = (int64_t)g.n0 * g.s0;
     int nb = 0;
-    if (!(L->flags & POMS_LAYOUT_GHOST_DATA) &&
+    static const bool cd_off = [] { const char* e = getenv("POMS_COPY_DOT"); return e && e[0] == '0'; }();
+    if (!cd_off && !(L->flags & POMS_LAYOUT_GHOST_DATA) &&
         vec_flat_launch(V_SCALEDOT, count, 1.0, 0.0, x + off, nullptr, z + off, nullptr, nullptr, ctx->scratch,
                         as_stream(stream), &nb) == 0) {
         reduce_wide_launch(ctx->scratch, nb, out_dev, as_stream(stream));

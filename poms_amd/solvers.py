@@ -36,6 +36,7 @@ Inputs must be :mod:`poms_amd.stencil` device objects; there is no CPU path.
 """
 from __future__ import annotations
 
+import os
 from math import sqrt
 
 from .stencil import KronOperator, StencilVector
@@ -189,7 +190,7 @@ def _pcg_native(A, b, x0, tol, maxiter, x0_owned=False):
         work = A._pcg_work = [V.empty() for _ in range(5)]
     # (x0 = None: the C loop zero-fills x's interior; empty() zeroes only the ghosts,
     # instead of a second full-storage fill)
-    x = V.empty() if x0 is None else (x0 if x0_owned else x0.copy())
+    x = (V.empty() if os.environ.get("POMS_PCG_X_EMPTY", "1") != "0" else V.zeros()) if x0 is None else (x0 if x0_owned else x0.copy())
     if x0 is not None:
         assert x0.shape == (A.shape[0],)
     d = V.dist if V.is_distributed else None
