@@ -99,8 +99,9 @@ class TwoLevelVCycle:
         # False: the residual vector and the restriction, as the reference computes them.
         # None: fused in 3D (515^3: 0.70 ms against 0.92 for the pair), not in 2D, where
         # the passes are latency-bound (1027^2: 44.8 against 42.5 us)
-        if fused_restrict is None:
-            fused_restrict = ndim == 3 and os.environ.get("POMS_FUSED_RESTRICT", "1") != "0"
+        if fused_restrict is None:   # (POMS_FUSED_RESTRICT: 0 never, all in every dimension)
+            fr = os.environ.get("POMS_FUSED_RESTRICT", "1")
+            fused_restrict = fr == "all" or (ndim == 3 and fr != "0")
         self.fused_restrict = bool(fused_restrict) and self.transfer.set_operator(self.A)
         from .splines import band_to_dense
         Md, Kd = band_to_dense(M), band_to_dense(K)
