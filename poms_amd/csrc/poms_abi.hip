@@ -1720,14 +1720,6 @@ int poms_transfer_set_operator(poms_transfer* t, int form, const double* const* 
 static int mpass(poms_transfer* t, const MultiPass& mp, hipStream_t st) {
     const int64_t need = mrestrict_scratch(mp, t->ncf);
     if (need > t->mpart_n) {
-        // (grown on the first call; not while the stream is captured into a graph, whose
-        // replays would keep the freed block -- such a caller runs one call uncaptured first)
-        hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
-        POMS_HIP_CHECK(hipStreamIsCapturing(st, &cs));
-        if (cs != hipStreamCaptureStatusNone) {
-            set_error("resid_restrict: partial-sum buffer must grow; make one uncaptured call first");
-            return 1;
-        }
         if (t->mpart) (void)hipFree(t->mpart);
         t->mpart = nullptr;
         t->mpart_n = 0;
